@@ -1,0 +1,330 @@
+/*
+ * Sparse matrix-vector products on the host (component C5), ref 3-serial-optimization/spmv.c.
+ *
+ *  create_csr_matrix  five symmetric bands (centre a, gap b, band c, gap d, band e) clipped to [0,n),
+ *                     values = rand()/RAND_MAX in row-major nnz order (same rand() call sequence as
+ *                     spmv.c:74-144, so values match the reference bit-for-bit under glibc).
+ *  multiply_naive     plain CSR loop (spmv.c:170-177).
+ *  multiply           banded product with IMPLICIT column indices: every band is a contiguous slice of
+ *                     v and of values, so the inner loop is a unit-stride dot product (AVX2 via gcc
+ *                     vectorisation of the 8-way unrolled loop) instead of spmv.c's SSE x20 unroll.
+ *  compare            |a-b| > 1e-3 error count with the reference's exact output strings (B17 kept:
+ *                     it prints "n-10 more errors...", negative when there are fewer than 10).
+ *  power-law          Chung-Lu style generator for the 1e8-nnz north-star matrix: permuted Zipf row
+ *                     degrees, per-row columns drawn SORTED from a Zipf column density (ordered
+ *                     uniforms via exponential spacings) — O(nnz), no sort pass, deterministic.
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "pcmx_cpu.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+int diag_count(int dim, int n) { return n * dim - ((n * (n + 1)) / 2); }
+
+void pcmx_band_ranges(int n, int a, int b, int c, int d, int e, int row, int lo[5], int hi[5]) {
+    const int ah = a / 2;
+    const int r5 = ah, r6 = ah + b, r7 = ah + b + c, r8 = ah + b + c + d, r9 = ah + b + c + d + e;
+#define PCMX_MAX(x, y) ((x) > (y) ? (x) : (y))
+#define PCMX_MIN(x, y) ((x) < (y) ? (x) : (y))
+    /* left outer band, left inner band, centre, right inner band, right outer band */
+    lo[0] = PCMX_MAX(0, row - r9);
+    hi[0] = PCMX_MAX(0, row - r8);
+    lo[1] = PCMX_MAX(0, row - r7);
+    hi[1] = PCMX_MAX(0, row - r6);
+    lo[2] = PCMX_MAX(0, row - r5);
+    hi[2] = PCMX_MIN(row + r5 + 1, n);
+    lo[3] = PCMX_MIN(n, row + r6 + 1);
+    hi[3] = PCMX_MIN(n, row + r7 + 1);
+    lo[4] = PCMX_MIN(n, row + r8 + 1);
+    hi[4] = PCMX_MIN(n, row + r9 + 1);
+    for (int k = 0; k < 5; ++k)
+        if (hi[k] < lo[k]) hi[k] = lo[k];
+#undef PCMX_MAX
+#undef PCMX_MIN
+}
+
+csr_matrix_t* create_csr_matrix(int n_rows, int n_cols, int a, int b, int c, int d, int e) {
+    /* pass 1: exact nnz per row (the band limits are clipped by n_cols on the right) */
+    int* row_ptr = (int*)malloc(sizeof(int) * (size_t)(n_rows + 1));
+    if (!row_ptr) return NULL;
+    row_ptr[0] = 0;
+    int lo[5], hi[5];
+    for (int i = 0; i < n_rows; ++i) {
+        pcmx_band_ranges(n_cols, a, b, c, d, e, i, lo, hi);
+        int w = 0;
+        for (int k = 0; k < 5; ++k) w += hi[k] - lo[k];
+        row_ptr[i + 1] = row_ptr[i] + w;
+    }
+    const int nnz = row_ptr[n_rows];
+    csr_matrix_t* m = (csr_matrix_t*)malloc(sizeof(csr_matrix_t));
+    int* col = (int*)malloc(sizeof(int) * (size_t)(nnz > 0 ? nnz : 1));
+    float* val = (float*)malloc(sizeof(float) * (size_t)(nnz > 0 ? nnz : 1));
+    if (!m || !col || !val) {
+        free(m), free(col), free(val), free(row_ptr);
+        return NULL;
+    }
+    /* pass 2: columns (parallel, independent rows) */
+#pragma omp parallel for schedule(static) private(lo, hi)
+    for (int i = 0; i < n_rows; ++i) {
+        pcmx_band_ranges(n_cols, a, b, c, d, e, i, lo, hi);
+        int p = row_ptr[i];
+        for (int k = 0; k < 5; ++k)
+            for (int j = lo[k]; j < hi[k]; ++j) col[p++] = j;
+    }
+    /* pass 3: values, sequential rand() to keep the reference's value stream */
+    for (int p = 0; p < nnz; ++p) val[p] = (float)rand() / RAND_MAX;
+    m->n_row_ptr = n_rows + 1;
+    m->row_ptr = row_ptr;
+    m->col_ind = col;
+    m->n_values = nnz;
+    m->values = val;
+    return m;
+}
+
+void free_csr_matrix(csr_matrix_t* m) {
+    if (!m) return;
+    free(m->row_ptr);
+    free(m->col_ind);
+    free(m->values);
+    free(m);
+}
+
+float* create_vector(int n) {
+    float* v = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; v && i < n; ++i) v[i] = (float)rand() / RAND_MAX;
+    return v;
+}
+
+void print_raw_csr_matrix(csr_matrix_t* m) {
+    printf("row_ptr = {");
+    for (int i = 0; i < m->n_row_ptr; ++i) printf("%d ", m->row_ptr[i]);
+    printf("}\ncol_ind = {");
+    for (int i = 0; i < m->n_values; ++i) printf("%d ", m->col_ind[i]);
+    printf("}\nvalues = {");
+    for (int i = 0; i < m->n_values; ++i) printf("%f ", m->values[i]);
+    printf("}\n");
+}
+
+void print_formated_csr_matrix(csr_matrix_t* m) {
+    const char* red = "\x1B[31m";
+    const char* nrm = "\x1B[0m";
+    const int n = m->n_row_ptr - 1;
+    for (int i = 0; i < n; ++i) {
+        int p = m->row_ptr[i];
+        for (int j = 0; j < n; ++j) {
+            if (p < m->row_ptr[i + 1] && m->col_ind[p] == j)
+                printf("%s%.2f ", red, m->values[p++]);
+            else
+                printf("%s%.2f ", nrm, 0.0);
+        }
+        printf("%s\n", nrm);
+    }
+}
+
+void print_vector(float* v, int n, int orientation) {
+    for (int i = 0; i < n; ++i) printf("%f%s", v[i], orientation ? " " : "\n");
+    if (orientation) printf("\n");
+}
+
+void print_time(struct timeval start, struct timeval end) {
+    long long us = (long long)(end.tv_sec - start.tv_sec) * 1000000LL + (end.tv_usec - start.tv_usec);
+    printf("Time : %f s\n", (double)us / 1e6);
+}
+
+void multiply_naive(csr_matrix_t* m, float* v, float* r) {
+    const int n = m->n_row_ptr - 1;
+    for (int i = 0; i < n; ++i) {
+        float acc = r[i];
+        for (int p = m->row_ptr[i]; p < m->row_ptr[i + 1]; ++p) acc += v[m->col_ind[p]] * m->values[p];
+        r[i] = acc;
+    }
+}
+
+void compare(float* a, float* b, int n) {
+    int errors = 0;
+    for (int i = 0; i < n; ++i) {
+        if (fabsf(a[i] - b[i]) > 1e-3f) {
+            ++errors;
+            if (errors < 10) printf("Error at: %d, expected: %f, actual: %f\n", i, a[i], b[i]);
+        }
+    }
+    printf("%d more errors...\n", errors - 10);
+}
+
+s_matrix_t* create_s_matrix(int dim, int a, int b, int c, int d, int e) {
+    /* Generates the banded values directly (no CSR indices at all). */
+    csr_matrix_t* csr = create_csr_matrix(dim, dim, a, b, c, d, e);
+    if (!csr) return NULL;
+    s_matrix_t* s = convert_to_s_matrix(csr, dim, a, b, c, d, e);
+    free(csr->row_ptr);
+    free(csr->col_ind);
+    free(csr); /* values now owned by s */
+    return s;
+}
+
+s_matrix_t* convert_to_s_matrix(csr_matrix_t* csr, int n, int a, int b, int c, int d, int e) {
+    s_matrix_t* s = (s_matrix_t*)malloc(sizeof(s_matrix_t));
+    if (!s) return NULL;
+    s->values = csr->values; /* shares storage, as spmv.c:198-210 does */
+    s->n = n;
+    s->a = a, s->b = b, s->c = c, s->d = d, s->e = e;
+    return s;
+}
+
+static inline float dot_contig(const float* restrict x, const float* restrict y, int len) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int j = 0;
+    for (; j + 8 <= len; j += 8)
+#pragma omp simd
+        for (int t = 0; t < 8; ++t) acc[t] += x[j + t] * y[j + t];
+    float s = 0.0f;
+    for (; j < len; ++j) s += x[j] * y[j];
+    return s + ((acc[0] + acc[4]) + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7]));
+}
+
+static inline float banded_row(const s_matrix_t* s, const float* v, int i, const float* vals_row) {
+    int lo[5], hi[5];
+    pcmx_band_ranges(s->n, s->a, s->b, s->c, s->d, s->e, i, lo, hi);
+    float acc = 0.0f;
+    for (int k = 0; k < 5; ++k) {
+        int len = hi[k] - lo[k];
+        acc += dot_contig(v + lo[k], vals_row, len);
+        vals_row += len;
+    }
+    return acc;
+}
+
+/* row start offsets of a banded matrix in closed form: prefix over rows is cheap to recompute. */
+static long long banded_row_start(const s_matrix_t* s, int i) {
+    /* nnz(row) = sum of clipped widths; rows start at the running total. For OpenMP chunks we compute
+     * the start of each chunk once by summing widths (O(rows) total across threads). */
+    long long off = 0;
+    int lo[5], hi[5];
+    for (int r = 0; r < i; ++r) {
+        pcmx_band_ranges(s->n, s->a, s->b, s->c, s->d, s->e, r, lo, hi);
+        for (int k = 0; k < 5; ++k) off += hi[k] - lo[k];
+    }
+    return off;
+}
+
+void multiply(s_matrix_t* matrix, float* v, float* r) {
+    const float* vals = matrix->values;
+    int lo[5], hi[5];
+    for (int i = 0; i < matrix->n; ++i) {
+        r[i] = banded_row(matrix, v, i, vals);
+        pcmx_band_ranges(matrix->n, matrix->a, matrix->b, matrix->c, matrix->d, matrix->e, i, lo, hi);
+        for (int k = 0; k < 5; ++k) vals += hi[k] - lo[k];
+    }
+}
+
+void pcmx_spmv_banded_omp(const s_matrix_t* s, const float* v, float* r) {
+#pragma omp parallel
+    {
+        int nt = 1, t = 0;
+#ifdef _OPENMP
+        nt = omp_get_num_threads();
+        t = omp_get_thread_num();
+#endif
+        int r0 = (int)((long long)s->n * t / nt), r1 = (int)((long long)s->n * (t + 1) / nt);
+        const float* vals = s->values + banded_row_start(s, r0);
+        int lo[5], hi[5];
+        for (int i = r0; i < r1; ++i) {
+            r[i] = banded_row(s, v, i, vals);
+            pcmx_band_ranges(s->n, s->a, s->b, s->c, s->d, s->e, i, lo, hi);
+            for (int k = 0; k < 5; ++k) vals += hi[k] - lo[k];
+        }
+    }
+}
+
+void pcmx_spmv_csr_omp(int n_rows, const int* row_ptr, const int* col_ind, const float* values, const float* v,
+                       float* r) {
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int i = 0; i < n_rows; ++i) {
+        float acc = 0.0f;
+        for (int p = row_ptr[i]; p < row_ptr[i + 1]; ++p) acc += v[col_ind[p]] * values[p];
+        r[i] = acc;
+    }
+}
+
+/* ---------------------------------------------------------------- power-law generator */
+
+static inline unsigned long long splitmix64(unsigned long long* s) {
+    unsigned long long z = (*s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static inline double u01(unsigned long long* s) { return ((splitmix64(s) >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
+
+/* bijection on [0,n): full-period LCG on the next power of two + cycle walking */
+static inline long long permute_index(long long i, long long n, unsigned long long seed) {
+    unsigned long long m = 1;
+    while (m < (unsigned long long)n) m <<= 1;
+    unsigned long long a = (0x5DEECE66DULL | 1ULL) * 4ULL + 1ULL; /* a = 1 mod 4 */
+    unsigned long long c = (seed * 2ULL) | 1ULL;                   /* odd */
+    unsigned long long x = (unsigned long long)i;
+    do {
+        x = (a * x + c) & (m - 1);
+    } while (x >= (unsigned long long)n);
+    return (long long)x;
+}
+
+long long pcmx_powerlaw_row_counts(int n_rows, long long target_nnz, double alpha, unsigned long long seed,
+                                   long long* row_ptr) {
+    /* Zipf weights w_k = (k+1)^(-1/(alpha-1)) for degree rank k; rank -> row via a bijection. */
+    const double ex = 1.0 / (alpha - 1.0);
+    double z = 0.0;
+#pragma omp parallel for reduction(+ : z)
+    for (int k = 0; k < n_rows; ++k) z += pow((double)k + 1.0, -ex);
+    const double scale = (double)target_nnz / z;
+    long long* deg = (long long*)malloc(sizeof(long long) * (size_t)n_rows);
+#pragma omp parallel for
+    for (int k = 0; k < n_rows; ++k) {
+        double dk = scale * pow((double)k + 1.0, -ex);
+        long long di = (long long)floor(dk);
+        /* stochastic rounding keeps the expected total at target_nnz */
+        unsigned long long s = seed ^ (0xA24BAED4963EE407ULL * (unsigned long long)(k + 1));
+        if (u01(&s) < dk - (double)di) ++di;
+        if (di < 1) di = 1;
+        deg[permute_index(k, n_rows, seed)] = di;
+    }
+    row_ptr[0] = 0;
+    for (int i = 0; i < n_rows; ++i) row_ptr[i + 1] = row_ptr[i] + deg[i];
+    free(deg);
+    return row_ptr[n_rows];
+}
+
+void pcmx_powerlaw_fill(int n_rows, int n_cols, const long long* row_ptr, unsigned long long seed, int* col_ind,
+                        float* values) {
+    /* Column density ~ (c+1)^(-gamma), gamma = 0.5 (a heavy head of popular columns); inverse CDF of
+     * the continuous approximation F(x) = ((x+1)^(1-g) - 1) / ((n+1)^(1-g) - 1). Ordered uniforms are
+     * produced from normalised cumulative exponential spacings, so columns come out sorted. */
+    const double g = 0.5, one_g = 1.0 - g;
+    const double top = pow((double)n_cols + 1.0, one_g) - 1.0;
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int i = 0; i < n_rows; ++i) {
+        long long p0 = row_ptr[i], p1 = row_ptr[i + 1];
+        long long d = p1 - p0;
+        unsigned long long s = seed * 0x9E3779B97F4A7C15ULL + (unsigned long long)i * 0xD1B54A32D192ED03ULL + 1;
+        /* first pass: accumulate spacings into values[] as scratch (doubles would cost 2x memory) */
+        double total = 0.0;
+        for (long long q = 0; q < d; ++q) {
+            double ex = -log(u01(&s));
+            total += ex;
+            values[p0 + q] = (float)total;
+        }
+        total += -log(u01(&s));
+        for (long long q = 0; q < d; ++q) {
+            double u = (double)values[p0 + q] / total;
+            double x = pow(u * top + 1.0, 1.0 / one_g) - 1.0;
+            long long c = (long long)x;
+            if (c >= n_cols) c = n_cols - 1;
+            col_ind[p0 + q] = (int)c;
+        }
+        for (long long q = 0; q < d; ++q) values[p0 + q] = (float)(u01(&s) * 2.0 - 1.0);
+    }
+}

@@ -1,0 +1,81 @@
+/*
+ * pcmx_hip.h — C ABI of libpcmx_hip.so: every MI355X (gfx950) kernel of the framework.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers unless the name says host. Every launcher is asynchronous on the
+ *    given stream, allocates nothing and never synchronises, so a caller may capture it into a hipGraph.
+ *    Workspaces are caller-provided; pcmx_*_workspace_bytes() says how much.
+ *  - Return value: 0 on success, otherwise a hipError_t (or -1 for a shape/alignment precondition).
+ *  - Element counts are 64-bit: 1e9-element arrays (4 GB) are first-class on a 288 GB MI355X.
+ *
+ * Reference parity (file:line in anonyomous4/parallel-c-programs):
+ *  vmul            6-opencl-region-growing/multiply_opencl.cl:1-4
+ *  sgemm           1-introduction/matrix.c:63-81 (matrix_multiply) — fp32 MFMA on gfx950
+ *  histeq          4-histogram-equalization-openmp-pthreads/histogram_serial.c:11-42
+ *  region2d        2-mpi-region-growing/region.c:493-533 (flood fill, tile + 1-px halo)
+ *  region3d_*      5-cuda-region-growing/raycast.cu:534-699 (naive + shared-memory kernels)
+ *  raycast_*       5-cuda-region-growing/raycast.cu:321-433 (global-memory + texture kernels)
+ *  volume_gen      5-cuda-region-growing/raycast.cu:114-158
+ *  spmv_*          3-serial-optimization/spmv.c:170-329
+ */
+#ifndef PCMX_HIP_H
+#define PCMX_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- runtime / device info */
+int pcmx_device_count(void);
+/* Prints count, name, gcnArchName, CUs, LDS/CU, L2, HBM size, clock (replaces print_properties /
+ * printDeviceInfo, ref raycast.cu:99-110, clutil.c:63-122). */
+void pcmx_print_device_info(int device);
+const char* pcmx_error_string(int err);
+/* registers the MFMA SGEMM as matrix_multiply()'s backend (host matrices, copies in/out). */
+void pcmx_register_gemm_backend(long long min_flops);
+int pcmx_sgemm_host_arrays(const float* a, const float* b, float* c, int m, int n, int k);
+
+/* ---------------------------------------------------------------- element-wise (HBM-bound) */
+int pcmx_vmul_f32(const float* a, const float* b, float* r, long long n, hipStream_t s);
+int pcmx_vadd_f32(const float* a, const float* b, float* r, long long n, hipStream_t s);
+int pcmx_axpy_f32(float alpha, const float* x, float* y, long long n, hipStream_t s);
+int pcmx_fill_f32(float* x, float v, long long n, hipStream_t s);
+/* x[i] = uniform[lo,hi) from a counter-based hash of (seed, i): on-device synthetic data */
+int pcmx_rand_uniform_f32(float* x, long long n, unsigned long long seed, float lo, float hi, hipStream_t s);
+
+/* ---------------------------------------------------------------- reductions */
+enum { PCMX_OP_SUM = 0, PCMX_OP_MIN = 1, PCMX_OP_MAX = 2 };
+/* number of first-pass partials the reduce launchers use (workspace = that many elements * 8 B) */
+long long pcmx_reduce_workspace_bytes(long long n);
+/* out[0] = op(x[0..n)) ; two passes, deterministic (fixed grid, fixed combine order) */
+int pcmx_reduce_f32(const float* x, long long n, int op, float* out, void* workspace, hipStream_t s);
+int pcmx_reduce_i32(const int32_t* x, long long n, int op, int32_t* out, void* workspace, hipStream_t s);
+/* out[0] = sum a*b */
+int pcmx_dot_f32(const float* a, const float* b, long long n, float* out, void* workspace, hipStream_t s);
+
+/* ---------------------------------------------------------------- prefix scan */
+long long pcmx_scan_workspace_bytes(long long n);
+/* out[i] = init + sum_{j<=i} x[j] (inclusive) or init + sum_{j<i} x[j] (exclusive), single pass with
+ * decoupled look-back; init is read from device memory (init_dev may be NULL => 0) so a multi-GPU
+ * offset can be fed without a host round trip. In-place (out == x) is allowed. */
+int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
+                  hipStream_t s);
+
+/* ---------------------------------------------------------------- SGEMM (fp32 MFMA) */
+/* C = alpha*A*B + beta*C, row-major. Fast path needs M%256==0, N%256==0 (or %128 for the small-tile
+ * kernel), K%32==0, 16-B aligned rows; anything else returns -1 (the torch layer pads). */
+int pcmx_sgemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
+                   float alpha, float beta, hipStream_t s);
+/* tile selection used by pcmx_sgemm_f32: 0 = 256x256x32 / 8 waves, 1 = 128x128x32 / 4 waves */
+int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
+                           int ldc, float alpha, float beta, int variant, hipStream_t s);
+/* Reference-style f32 VALU GEMM (one thread per output, LDS tiles) for A/B comparisons. */
+int pcmx_sgemm_f32_simt(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCMX_HIP_H */

@@ -1,0 +1,74 @@
+// Shared device-side helpers for the gfx950 kernels (wave64 collectives, vector types, checks).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define PCMX_HIP_RET(expr)                                  \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return (int)_e;               \
+    } while (0)
+
+#define PCMX_HIP_CHECK(expr)                                                                       \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) {                                                                    \
+            fprintf(stderr, "HIP error %s at %s:%d: %s\n", hipGetErrorString(_e), __FILE__, __LINE__, #expr); \
+            abort();                                                                               \
+        }                                                                                          \
+    } while (0)
+
+namespace pcmx {
+
+// Native clang vectors (HIP's float4 is a struct the nontemporal builtins reject).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+template <class V>
+__device__ __forceinline__ V ld_nt(const V* p) { return __builtin_nontemporal_load(p); }
+template <class V>
+__device__ __forceinline__ void st_nt(V* p, V v) { __builtin_nontemporal_store(v, p); }
+
+constexpr int kWave = 64;  // CDNA wavefront: 64 lanes (never 32)
+constexpr int kNumXcd = 8;
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+template <class T>
+__device__ __forceinline__ T op_apply(int op, T a, T b) {
+    return op == 0 ? a + b : (op == 1 ? (a < b ? a : b) : (a > b ? a : b));
+}
+
+// Full-wave butterfly reduction (DPP/permute lowered by the compiler); result in every lane.
+template <class T, int OP>
+__device__ __forceinline__ T wave_reduce(T v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        T o = __shfl_xor(v, off, kWave);
+        v = OP == 0 ? v + o : (OP == 1 ? (o < v ? o : v) : (o > v ? o : v));
+    }
+    return v;
+}
+
+// Inclusive wave scan (Hillis-Steele over 64 lanes).
+__device__ __forceinline__ float wave_inclusive_scan(float v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        float o = __shfl_up(v, off, kWave);
+        if (l >= off) v += o;
+    }
+    return v;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): blocks that the dispatcher deals to one XCD (b, b+8, b+16, ...) get consecutive ids.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int q = nwg / kNumXcd, r = nwg % kNumXcd;
+    const int xcd = bid % kNumXcd, slot = bid / kNumXcd;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
+inline int grid_cap_streaming() { return 256 * 8; }  // 256 CUs x 8 blocks: cap, then grid-stride
+
+}  // namespace pcmx

@@ -1,0 +1,123 @@
+"""Numerics of the core gfx950 kernels against plain PyTorch fp32/fp64 references (GPU only)."""
+import pytest
+import torch
+
+from parallel_c_programs_amd import ops
+from parallel_c_programs_amd._native import ops as native_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def test_extension_is_native(gpu):
+    import parallel_c_programs_amd._C as C
+
+    assert C.device_count() >= 1
+    assert hasattr(native_ops(), "sgemm")
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1000, 4099, 1 << 20, (1 << 22) + 5])
+def test_vmul_vadd_axpy(gpu, n):
+    a = torch.rand(n, device=gpu)
+    b = torch.rand(n, device=gpu)
+    torch.testing.assert_close(ops.vmul(a, b), a * b)
+    torch.testing.assert_close(ops.vadd(a, b), a + b)
+    y = b.clone()
+    ops.axpy_(y, 2.5, a)
+    torch.testing.assert_close(y, 2.5 * a + b)
+
+
+def test_vmul_reference_demo(gpu):
+    # ref multiply_opencl.c:47-50: a[i] = i+1, b[i] = 1/(i+1) -> every product is 1.0
+    i = torch.arange(1024, device=gpu, dtype=torch.float32)
+    r = ops.vmul(i + 1, 1.0 / (i + 1))
+    torch.testing.assert_close(r, torch.ones_like(r), atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 123457, 1 << 24])
+def test_reduce_sum_min_max(gpu, n):
+    x = torch.randn(n, device=gpu)
+    ref = x.double().sum().item()
+    assert abs(ops.reduce(x, "sum").item() - ref) <= 1e-5 * max(1.0, x.abs().double().sum().item())
+    assert ops.reduce(x, "min").item() == x.min().item()
+    assert ops.reduce(x, "max").item() == x.max().item()
+    xi = torch.randint(-1000, 1000, (n,), device=gpu, dtype=torch.int32)
+    assert ops.reduce(xi, "sum").item() == xi.long().sum().item()
+    assert ops.reduce(xi, "min").item() == xi.min().item()
+
+
+def test_reduce_deterministic(gpu):
+    x = torch.randn(10_000_019, device=gpu)
+    r = [ops.reduce(x, "sum").item() for _ in range(3)]
+    assert r[0] == r[1] == r[2]
+
+
+def test_dot(gpu):
+    a = torch.randn(3_000_001, device=gpu)
+    b = torch.randn(3_000_001, device=gpu)
+    ref = (a.double() * b.double()).sum().item()
+    assert abs(ops.dot(a, b).item() - ref) < 1e-3 * (a.abs() * b.abs()).double().sum().item() * 1e-2
+
+
+@pytest.mark.parametrize("n", [1, 5, 8192, 8193, 100_003, 3 << 20])
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_scan(gpu, n, exclusive):
+    x = torch.rand(n, device=gpu) - 0.5
+    ref = torch.cumsum(x.double(), 0)
+    if exclusive:
+        ref = torch.cat([ref.new_zeros(1), ref[:-1]])
+    out = ops.scan(x, exclusive=exclusive)
+    tol = 1e-5 * max(1.0, float(n) ** 0.5) * 4
+    assert (out.double() - ref).abs().max().item() < tol
+
+
+def test_scan_with_device_init(gpu):
+    x = torch.ones(50_000, device=gpu)
+    init = torch.tensor([10.0], device=gpu)
+    out = ops.scan(x, init=init)
+    assert out[0].item() == 11.0 and out[-1].item() == 50_010.0
+
+
+def test_scan_integer_exact(gpu):
+    # small integers sum exactly in f32 -> bit-exact against the integer cumsum
+    x = torch.randint(0, 3, (2_000_000,), device=gpu).float()
+    out = ops.scan(x)
+    assert torch.equal(out.long(), torch.cumsum(x.long(), 0))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 10])
+def test_sgemm_identity_asymmetric(gpu, variant):
+    # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
+    n = 256
+    a = torch.eye(n, device=gpu)
+    b = torch.arange(n * n, device=gpu, dtype=torch.float32).view(n, n) / 7.0
+    c = ops.sgemm(a, b, variant=variant)
+    assert torch.equal(c, b)
+    c2 = ops.sgemm(b, a, variant=variant)
+    assert torch.equal(c2, b)
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 256), (512, 768, 1024), (1024, 1024, 2048), (100, 70, 33), (1000, 1000, 1000)])
+def test_sgemm_vs_fp64(gpu, shape):
+    m, n, k = shape
+    a = torch.rand(m, k, device=gpu) * 2 - 1
+    b = torch.rand(k, n, device=gpu) * 2 - 1
+    c = ops.sgemm(a, b)
+    ref = a.double() @ b.double()
+    scale = (a.abs().double() @ b.abs().double())
+    err = ((c.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+    assert err < 4e-6 * max(1.0, (k / 256) ** 0.5)
+
+
+def test_sgemm_beta(gpu):
+    a = torch.rand(256, 256, device=gpu)
+    b = torch.rand(256, 256, device=gpu)
+    c = torch.rand(256, 256, device=gpu)
+    ref = 2.0 * (a.double() @ b.double()) + 0.5 * c.double()
+    out = ops.sgemm_out(a, b, c.clone(), alpha=2.0, beta=0.5)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+def test_sgemm_simt_baseline(gpu):
+    a = torch.rand(300, 200, device=gpu)
+    b = torch.rand(200, 100, device=gpu)
+    torch.testing.assert_close(ops.sgemm_simt(a, b), a @ b, rtol=1e-4, atol=1e-4)
