@@ -113,6 +113,7 @@ static int volume_shape(int x, int y, int z) {
 }
 
 void pcmx_create_data(unsigned char* data, int dim) {
+    srand(1); /* the reference never seeds: glibc's default sequence is seed 1 */
     for (int z = 0; z < dim; ++z)
         for (int y = 0; y < dim; ++y) {
             unsigned char* row = data + ((size_t)z * dim + y) * dim;

@@ -298,16 +298,17 @@ long long pcmx_powerlaw_row_counts(int n_rows, long long target_nnz, double alph
     return row_ptr[n_rows];
 }
 
-void pcmx_powerlaw_fill(int n_rows, int n_cols, const long long* row_ptr, unsigned long long seed, int* col_ind,
-                        float* values) {
+void pcmx_powerlaw_fill_rows(int row0, int row1, int n_cols, const long long* row_ptr, unsigned long long seed,
+                             int* col_ind, float* values) {
     /* Column density ~ (c+1)^(-gamma), gamma = 0.5 (a heavy head of popular columns); inverse CDF of
      * the continuous approximation F(x) = ((x+1)^(1-g) - 1) / ((n+1)^(1-g) - 1). Ordered uniforms are
      * produced from normalised cumulative exponential spacings, so columns come out sorted. */
     const double g = 0.5, one_g = 1.0 - g;
     const double top = pow((double)n_cols + 1.0, one_g) - 1.0;
+    const long long base = row_ptr[row0];
 #pragma omp parallel for schedule(dynamic, 256)
-    for (int i = 0; i < n_rows; ++i) {
-        long long p0 = row_ptr[i], p1 = row_ptr[i + 1];
+    for (int i = row0; i < row1; ++i) {
+        long long p0 = row_ptr[i] - base, p1 = row_ptr[i + 1] - base;
         long long d = p1 - p0;
         unsigned long long s = seed * 0x9E3779B97F4A7C15ULL + (unsigned long long)i * 0xD1B54A32D192ED03ULL + 1;
         /* first pass: accumulate spacings into values[] as scratch (doubles would cost 2x memory) */
@@ -327,4 +328,9 @@ void pcmx_powerlaw_fill(int n_rows, int n_cols, const long long* row_ptr, unsign
         }
         for (long long q = 0; q < d; ++q) values[p0 + q] = (float)(u01(&s) * 2.0 - 1.0);
     }
+}
+
+void pcmx_powerlaw_fill(int n_rows, int n_cols, const long long* row_ptr, unsigned long long seed, int* col_ind,
+                        float* values) {
+    pcmx_powerlaw_fill_rows(0, n_rows, n_cols, row_ptr, seed, col_ind, values);
 }

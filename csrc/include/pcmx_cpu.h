@@ -101,6 +101,10 @@ long long pcmx_powerlaw_row_counts(int n_rows, long long target_nnz, double alph
                                    long long* row_ptr /* n_rows+1 */);
 void pcmx_powerlaw_fill(int n_rows, int n_cols, const long long* row_ptr, unsigned long long seed,
                         int* col_ind, float* values);
+/* rows [row0, row1) only (a rank's block; bit-identical to the same rows of pcmx_powerlaw_fill);
+ * outputs start at row_ptr[row0]. */
+void pcmx_powerlaw_fill_rows(int row0, int row1, int n_cols, const long long* row_ptr, unsigned long long seed,
+                             int* col_ind, float* values);
 
 /* -------------------------------------------------- histogram equalization (C6-C8) */
 #define PCMX_HIST_BINS 256
@@ -144,6 +148,12 @@ void pcmx_raycast_serial(const unsigned char* data, const unsigned char* region,
 /* ---------------------------------------------------------------- misc */
 double pcmx_wtime(void);
 int pcmx_omp_max_threads(void);
+
+/* ---------------------------------------------------------------- reference programs (demos.c) */
+int pcmx_matrix_demo(int compat);
+int pcmx_spmv_demo(int dim, int a, int b, int c, int d, int e);
+int pcmx_histogram_demo(const char* image, int n_threads, int method);
+int pcmx_vecops_demo(long long n, int n_threads, int reps);
 
 #ifdef __cplusplus
 }

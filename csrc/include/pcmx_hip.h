@@ -74,6 +74,50 @@ int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, int M, int 
                            int ldc, float alpha, float beta, int variant, hipStream_t s);
 /* Reference-style f32 VALU GEMM (one thread per output, LDS tiles) for A/B comparisons. */
 int pcmx_sgemm_f32_simt(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t s);
+/* tile order (remap<<8 | group_m) and the L2-resident timing diagnostic (k0_diag=0) — tuning only */
+int pcmx_sgemm_set_tuning(int tile_order, int k0_diag);
+
+/* ---------------------------------------------------------------- histogram equalisation */
+/* out = tf[img] (bit-identical to the serial reference); hist_ws: 256 u32 (also receives the histogram) */
+int pcmx_histeq_u8(const unsigned char* img, unsigned char* out, long long npix, unsigned* hist_ws, int force_multiblock,
+                   hipStream_t s);
+
+/* ---------------------------------------------------------------- region growing */
+long long pcmx_region2d_workspace_bytes(int H, int W);
+/* padded (H+2) x ld arrays, interior 1..H x 1..W; halo cells are read-only seeds. Blocks once per batch. */
+int pcmx_region2d_grow(const unsigned char* img, unsigned char* region, int H, int W, int ld, int thr, void* ws,
+                       int batch, int max_launches, hipStream_t s, int* launches_out);
+long long pcmx_region3d_workspace_bytes(int dim);
+int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char* region, int dim, int thr, void* ws, int batch,
+                             int max_launches, hipStream_t s, int* launches_out);
+/* reference 0/1/2 frontier semantics, one launch per BFS level */
+int pcmx_region3d_grow_naive(const unsigned char* data, unsigned char* region, int dim, int thr, int* flag_ws,
+                             int max_launches, hipStream_t s, int* launches_out);
+
+/* ---------------------------------------------------------------- volume + ray casting */
+int pcmx_volume_gen_u8(unsigned char* data, int dim, unsigned seed, hipStream_t s);
+int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
+                        int image_dim, const float* cam12, float pixel_width, float step, int max_steps, int f64_color,
+                        hipStream_t s);
+int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, unsigned long long* tex,
+                    hipStream_t s);
+int pcmx_raycast_bricked(const unsigned long long* tex, int dim, unsigned char* image, int image_dim,
+                         const float* cam12, float pixel_width, float step, int max_steps, hipStream_t s);
+
+/* ---------------------------------------------------------------- stencil */
+int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, int ld, int r0, int r1, long long global_row0,
+                       long long global_rows, float k, hipStream_t s);
+
+/* ---------------------------------------------------------------- SpMV */
+long long pcmx_spmv_csr_plan(const long long* row_ptr_host, int n_rows, void* items_host, long long max_items);
+int pcmx_spmv_csr(const long long* row_ptr, const int* col, const float* val, const float* x, float* y, int n_rows,
+                  const void* items, long long n_items, hipStream_t s);
+int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
+                     const float* x, float* y, hipStream_t s);
+
+/* ---------------------------------------------------------------- halo pack/unpack */
+int pcmx_pack_edges(const void* tile, int elem_bytes, int H, int W, int ld, void* buf, hipStream_t s);
+int pcmx_unpack_halo(void* tile, int elem_bytes, int H, int W, int ld, const void* buf, int mask, hipStream_t s);
 
 #ifdef __cplusplus
 }

@@ -178,6 +178,182 @@ at::Tensor sgemm_simt(const at::Tensor& a, const at::Tensor& b) {
 
 void device_info(int64_t device) { pcmx_print_device_info((int)device); }
 
+void check_u8_gpu(const at::Tensor& t, const char* name) {
+    check_gpu(t, name, at::kByte);
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+// ---------------------------------------------------------------- histogram equalisation
+at::Tensor histeq(const at::Tensor& img, bool force_multiblock) {
+    check_u8_gpu(img, "img");
+    const at::DeviceGuard g(img.device());
+    auto ic = aligned_contig(img);
+    auto out = at::empty_like(ic);
+    auto hist = at::empty({256}, img.options().dtype(at::kInt));
+    check_rc(pcmx_histeq_u8(ic.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), ic.numel(),
+                            reinterpret_cast<unsigned*>(hist.data_ptr<int>()), force_multiblock ? 1 : 0, cur_stream(img)),
+             "histeq");
+    return out;
+}
+
+// ---------------------------------------------------------------- region growing
+int64_t region2d_grow_(at::Tensor region, const at::Tensor& img, int64_t thr, int64_t batch, int64_t max_launches) {
+    check_u8_gpu(region, "region"), check_u8_gpu(img, "img");
+    TORCH_CHECK(region.dim() == 2 && img.sizes() == region.sizes(), "region2d: padded (H+2, W+2) uint8 tensors");
+    const at::DeviceGuard g(img.device());
+    const int H = (int)img.size(0) - 2, W = (int)img.size(1) - 2;
+    auto ws = workspace(img, pcmx_region2d_workspace_bytes(H, W));
+    int launches = 0;
+    check_rc(pcmx_region2d_grow(img.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), H, W, (int)img.size(1), (int)thr,
+                                ws.data_ptr(), (int)batch, (int)max_launches, cur_stream(img), &launches),
+             "region2d_grow_");
+    return launches;
+}
+
+int64_t region3d_grow_(at::Tensor region, const at::Tensor& data, int64_t thr, bool tiled, int64_t batch,
+                       int64_t max_launches) {
+    check_u8_gpu(region, "region"), check_u8_gpu(data, "data");
+    TORCH_CHECK(data.dim() == 3 && data.size(0) == data.size(1) && data.size(1) == data.size(2) &&
+                    region.sizes() == data.sizes(),
+                "region3d: cubic uint8 volumes");
+    const at::DeviceGuard g(data.device());
+    const int dim = (int)data.size(0);
+    int launches = 0;
+    if (tiled) {
+        auto ws = workspace(data, pcmx_region3d_workspace_bytes(dim));
+        check_rc(pcmx_region3d_grow_tiled(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), dim, (int)thr, ws.data_ptr(),
+                                          (int)batch, (int)max_launches, cur_stream(data), &launches),
+                 "region3d_grow_ (tiled)");
+    } else {
+        auto flag = at::empty({4}, data.options().dtype(at::kInt));
+        check_rc(pcmx_region3d_grow_naive(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), dim, (int)thr,
+                                          flag.data_ptr<int>(), (int)max_launches, cur_stream(data), &launches),
+                 "region3d_grow_ (naive)");
+    }
+    return launches;
+}
+
+// ---------------------------------------------------------------- volume + ray casting
+at::Tensor volume_gen_(at::Tensor data, int64_t seed) {
+    check_u8_gpu(data, "data");
+    const at::DeviceGuard g(data.device());
+    check_rc(pcmx_volume_gen_u8(data.data_ptr<uint8_t>(), (int)data.size(0), (unsigned)seed, cur_stream(data)), "volume_gen_");
+    return data;
+}
+
+std::vector<float> cam_vec(at::ArrayRef<double> cam12) {
+    TORCH_CHECK(cam12.size() == 12, "camera: 12 floats (camera, forward, right, up)");
+    std::vector<float> c(12);
+    for (int i = 0; i < 12; ++i) c[i] = (float)cam12[i];
+    return c;
+}
+
+at::Tensor raycast_global(const at::Tensor& data, const at::Tensor& region, int64_t image_dim, at::ArrayRef<double> cam12,
+                          double pixel_width, double step, int64_t max_steps, bool f64_color) {
+    check_u8_gpu(data, "data"), check_u8_gpu(region, "region");
+    const at::DeviceGuard g(data.device());
+    auto img = at::empty({image_dim, image_dim}, data.options());
+    auto c = cam_vec(cam12);
+    check_rc(pcmx_raycast_global(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0), img.data_ptr<uint8_t>(),
+                                 (int)image_dim, c.data(), (float)pixel_width, (float)step, (int)max_steps, f64_color ? 1 : 0,
+                                 cur_stream(data)),
+             "raycast_global");
+    return img;
+}
+
+at::Tensor brick_pack(const at::Tensor& data, const at::Tensor& region) {
+    check_u8_gpu(data, "data"), check_u8_gpu(region, "region");
+    const at::DeviceGuard g(data.device());
+    auto tex = at::empty(data.sizes(), data.options().dtype(at::kLong));
+    check_rc(pcmx_brick_pack(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0),
+                             reinterpret_cast<unsigned long long*>(tex.data_ptr<int64_t>()), cur_stream(data)),
+             "brick_pack");
+    return tex;
+}
+
+at::Tensor raycast_bricked(const at::Tensor& tex, int64_t image_dim, at::ArrayRef<double> cam12, double pixel_width,
+                           double step, int64_t max_steps) {
+    check_gpu(tex, "tex", at::kLong);
+    const at::DeviceGuard g(tex.device());
+    auto img = at::empty({image_dim, image_dim}, tex.options().dtype(at::kByte));
+    auto c = cam_vec(cam12);
+    check_rc(pcmx_raycast_bricked(reinterpret_cast<const unsigned long long*>(tex.data_ptr<int64_t>()), (int)tex.size(0),
+                                  img.data_ptr<uint8_t>(), (int)image_dim, c.data(), (float)pixel_width, (float)step,
+                                  (int)max_steps, cur_stream(tex)),
+             "raycast_bricked");
+    return img;
+}
+
+// ---------------------------------------------------------------- stencil
+void stencil5_(const at::Tensor& u, at::Tensor out, int64_t r0, int64_t r1, int64_t global_row0, int64_t global_rows,
+               double k) {
+    check_gpu(u, "u", at::kBFloat16), check_gpu(out, "out", at::kBFloat16);
+    TORCH_CHECK(u.dim() == 2 && u.sizes() == out.sizes() && u.is_contiguous() && out.is_contiguous(),
+                "stencil5: slabs of shape (rows+2, cols)");
+    const at::DeviceGuard g(u.device());
+    const int rows = (int)u.size(0) - 2, cols = (int)u.size(1);
+    check_rc(pcmx_stencil5_bf16(u.data_ptr(), out.data_ptr(), rows, cols, cols, (int)r0, (int)r1, global_row0, global_rows,
+                                (float)k, cur_stream(u)),
+             "stencil5_");
+}
+
+// ---------------------------------------------------------------- SpMV
+at::Tensor spmv_csr(const at::Tensor& row_ptr, const at::Tensor& col, const at::Tensor& val, const at::Tensor& x,
+                    const at::Tensor& items) {
+    check_gpu(row_ptr, "row_ptr", at::kLong), check_gpu(col, "col", at::kInt), check_gpu(val, "val", at::kFloat);
+    check_gpu(x, "x", at::kFloat), check_gpu(items, "items", at::kLong);
+    const at::DeviceGuard g(val.device());
+    const int n_rows = (int)row_ptr.numel() - 1;
+    auto y = at::empty({n_rows}, val.options());
+    check_rc(pcmx_spmv_csr((const long long*)row_ptr.data_ptr<int64_t>(), col.data_ptr<int>(), val.data_ptr<float>(), x.data_ptr<float>(),
+                           y.data_ptr<float>(), n_rows, items.data_ptr(), items.size(0), cur_stream(val)),
+             "spmv_csr");
+    return y;
+}
+
+at::Tensor spmv_banded(const at::Tensor& vals, const at::Tensor& row_off, int64_t n, int64_t a, int64_t b, int64_t c,
+                       int64_t d, int64_t e, const at::Tensor& x) {
+    check_gpu(vals, "vals", at::kFloat), check_gpu(row_off, "row_off", at::kLong), check_gpu(x, "x", at::kFloat);
+    const at::DeviceGuard g(vals.device());
+    auto y = at::empty({n}, vals.options());
+    check_rc(pcmx_spmv_banded(vals.data_ptr<float>(), (const long long*)row_off.data_ptr<int64_t>(), (int)n, (int)a, (int)b, (int)c, (int)d,
+                              (int)e, x.data_ptr<float>(), y.data_ptr<float>(), cur_stream(vals)),
+             "spmv_banded");
+    return y;
+}
+
+// ---------------------------------------------------------------- halo pack/unpack
+at::Tensor pack_edges(const at::Tensor& tile) {
+    TORCH_CHECK(tile.is_cuda() && tile.dim() == 2 && tile.is_contiguous(), "pack_edges: contiguous padded 2-D GPU tile");
+    const at::DeviceGuard g(tile.device());
+    const int H = (int)tile.size(0) - 2, W = (int)tile.size(1) - 2;
+    auto buf = at::empty({2 * W + 2 * H}, tile.options());
+    check_rc(pcmx_pack_edges(tile.data_ptr(), (int)tile.element_size(), H, W, (int)tile.size(1), buf.data_ptr(), cur_stream(tile)),
+             "pack_edges");
+    return buf;
+}
+
+void unpack_halo_(at::Tensor tile, const at::Tensor& buf, int64_t mask) {
+    TORCH_CHECK(tile.is_cuda() && tile.dim() == 2 && tile.is_contiguous() && buf.dtype() == tile.dtype(), "unpack_halo_");
+    const at::DeviceGuard g(tile.device());
+    const int H = (int)tile.size(0) - 2, W = (int)tile.size(1) - 2;
+    TORCH_CHECK(buf.numel() == 2 * W + 2 * H, "unpack_halo_: buffer size");
+    check_rc(pcmx_unpack_halo(tile.data_ptr(), (int)tile.element_size(), H, W, (int)tile.size(1), buf.data_ptr(), (int)mask,
+                              cur_stream(tile)),
+             "unpack_halo_");
+}
+
+// host-side CSR analysis (CPU int64 row_ptr -> int64 [n_items, 3] work items)
+at::Tensor spmv_csr_plan(const at::Tensor& row_ptr) {
+    TORCH_CHECK(!row_ptr.is_cuda() && row_ptr.scalar_type() == at::kLong, "spmv_csr_plan: CPU int64 row_ptr");
+    auto rp = row_ptr.contiguous();
+    const int n_rows = (int)rp.numel() - 1;
+    const long long k = pcmx_spmv_csr_plan((const long long*)rp.data_ptr<int64_t>(), n_rows, nullptr, 0);
+    auto items = at::empty({k, 3}, rp.options());
+    pcmx_spmv_csr_plan((const long long*)rp.data_ptr<int64_t>(), n_rows, items.data_ptr(), k);
+    return items;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(pcmx, m) {
@@ -194,6 +370,18 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("sgemm_out(Tensor a, Tensor b, Tensor(a!) c, float alpha=1., float beta=0., int variant=-1) -> Tensor(a!)");
     m.def("sgemm_simt(Tensor a, Tensor b) -> Tensor");
     m.def("device_info(int device=0) -> ()", device_info);
+    m.def("histeq(Tensor img, bool force_multiblock=False) -> Tensor");
+    m.def("region2d_grow_(Tensor(a!) region, Tensor img, int thr, int batch=4, int max_launches=100000) -> int");
+    m.def("region3d_grow_(Tensor(a!) region, Tensor data, int thr, bool tiled=True, int batch=8, int max_launches=1000000) -> int");
+    m.def("volume_gen_(Tensor(a!) data, int seed) -> Tensor(a!)");
+    m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True) -> Tensor");
+    m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
+    m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps) -> Tensor");
+    m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
+    m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
+    m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x) -> Tensor");
+    m.def("pack_edges(Tensor tile) -> Tensor");
+    m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
@@ -209,9 +397,23 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("sgemm", sgemm);
     m.impl("sgemm_out", sgemm_out);
     m.impl("sgemm_simt", sgemm_simt);
+    m.impl("histeq", histeq);
+    m.impl("region2d_grow_", region2d_grow_);
+    m.impl("region3d_grow_", region3d_grow_);
+    m.impl("volume_gen_", volume_gen_);
+    m.impl("raycast_global", raycast_global);
+    m.impl("brick_pack", brick_pack);
+    m.impl("raycast_bricked", raycast_bricked);
+    m.impl("stencil5_", stencil5_);
+    m.impl("spmv_csr", spmv_csr);
+    m.impl("spmv_banded", spmv_banded);
+    m.impl("pack_edges", pack_edges);
+    m.impl("unpack_halo_", unpack_halo_);
 }
 
 PYBIND11_MODULE(_C, mod) {
     mod.doc() = "pcmx MI355X kernels (ops live under torch.ops.pcmx)";
     mod.def("device_count", []() { return pcmx_device_count(); });
+    mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr");
+    mod.def("sgemm_set_tuning", [](int order, int diag) { return pcmx_sgemm_set_tuning(order, diag); });
 }

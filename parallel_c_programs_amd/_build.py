@@ -61,7 +61,8 @@ def _run(cmd, cwd=None):
     return r.stdout
 
 
-CPU_SRCS = ["cpu/bmp.c", "cpu/matrix.c", "cpu/spmv.c", "cpu/histogram.c", "cpu/vec.c", "cpu/oracles.c"]
+CPU_SRCS = ["cpu/bmp.c", "cpu/matrix.c", "cpu/spmv.c", "cpu/histogram.c", "cpu/vec.c", "cpu/oracles.c",
+            "cpu/demos.c"]
 CFLAGS = ["-O3", "-fPIC", "-std=gnu11", "-fopenmp", "-march=x86-64-v3", "-Wall", "-Wno-unknown-pragmas",
           f"-I{CSRC / 'include'}"]
 # files whose float rounding must match the reference build bit-for-bit
@@ -165,13 +166,14 @@ def build_bin(force=False, jobs=8):
         if not (force or _newer(out, deps)):
             continue
         variant = f"-DPCMX_TOOL_{name.upper()}"
+        rpath = "-Wl,-rpath,$ORIGIN/../parallel_c_programs_amd/lib"
         if kind == "c":
             todo.append(["gcc", "-O2", "-std=gnu11", "-fopenmp", variant, f"-I{CSRC / 'include'}", str(s),
-                         "-o", str(out), f"-L{LIB}", "-lpcmx_cpu", "-lm", f"-Wl,-rpath,{LIB}"])
+                         "-o", str(out), f"-L{LIB}", "-lpcmx_cpu", "-lm", rpath])
         else:
-            todo.append([HIPCC, "-O2", "-std=c++17", variant, f"-I{CSRC / 'include'}", str(s), "-o", str(out),
-                         f"-L{LIB}", f"-L{tlib}", "-lpcmx_hip", "-lpcmx_cpu", "-lamdhip64",
-                         f"-Wl,-rpath,{LIB}", f"-Wl,-rpath,{tlib}"])
+            todo.append([HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", variant, f"-I{CSRC / 'include'}",
+                         str(s), "-o", str(out), f"-L{LIB}", f"-L{tlib}", "-lpcmx_hip", "-lpcmx_cpu", "-lamdhip64",
+                         rpath, f"-Wl,-rpath,{tlib}"])
     with cf.ThreadPoolExecutor(jobs) as ex:
         list(ex.map(_run, todo))
 

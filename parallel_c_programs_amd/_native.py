@@ -119,6 +119,7 @@ def _declare_cpu(lib: ctypes.CDLL) -> ctypes.CDLL:
         "pcmx_band_ranges": (None, [I, I, I, I, I, I, I, P, P]),
         "pcmx_powerlaw_row_counts": (LL, [I, LL, D, ctypes.c_ulonglong, P]),
         "pcmx_powerlaw_fill": (None, [I, I, P, ctypes.c_ulonglong, P, P]),
+        "pcmx_powerlaw_fill_rows": (None, [I, I, I, P, ctypes.c_ulonglong, P, P]),
         "pcmx_wtime": (D, []),
         "pcmx_omp_max_threads": (I, []),
         "diag_count": (I, [I, I]),

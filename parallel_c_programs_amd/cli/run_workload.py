@@ -1,0 +1,62 @@
+"""Generic north-star driver: `run_workload <name> [--steps K] [--warmup W] [--set key=value ...]`.
+
+One process per GPU (launch with torch.distributed.run for N > 1); prints one JSON line on rank 0 with the
+whole-job throughput (sum over ranks), the max-over-ranks step time and the workload's numerics check."""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+
+from ..models import WORKLOADS, build_workload
+from ..parallel import finalize, init
+from ..utils.harness import timed
+
+
+def _val(s: str):
+    for cast in (int, float):
+        try:
+            return cast(s)
+        except ValueError:
+            pass
+    return {"true": True, "false": False}.get(s.lower(), s)
+
+
+def run(name: str, argv=None, defaults: dict | None = None) -> dict | None:
+    ap = argparse.ArgumentParser(prog=f"run_{name}")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--backend", default=None)
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="workload config")
+    a = ap.parse_args(argv)
+    cfg = dict(defaults or {})
+    cfg.update({k: _val(v) for k, v in (s.split("=", 1) for s in a.set)})
+    ctx = init(a.backend, a.device)
+    try:
+        w = build_workload(name, ctx, **cfg)
+        secs = timed(ctx, w.step, a.steps, a.warmup)
+        rep = w.report(secs, a.steps)
+        chk = {} if a.no_check else w.check()
+        out = {"workload": name, "n_ranks": ctx.world, "device": ctx.device.type, "steps": a.steps,
+               "warmup": a.warmup, "config": w.cfg, **{k: (round(v, 4) if isinstance(v, float) else v)
+                                                       for k, v in rep.items()}, **chk}
+        if ctx.is_root:
+            print(json.dumps(out), flush=True)
+        return out
+    finally:
+        finalize(ctx)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    if not argv or argv[0] not in WORKLOADS:
+        print(f"usage: run_workload {{{'|'.join(WORKLOADS)}}} [--steps K] [--warmup W] [--set k=v]")
+        return 2
+    run(argv[0], argv[1:])
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,214 @@
+"""Step-able workloads with work models. Every workload owns its per-rank data (weak scaling unless noted),
+exposes step() (one timed unit of work, including its collectives) and report(seconds, steps) (whole-job
+throughput = sum over ranks), and check() (a numerics check against an independent reference)."""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from ..parallel.collectives import global_scan
+from ..parallel.dist import Context
+
+
+@dataclass
+class Workload:
+    ctx: Context
+    cfg: dict = field(default_factory=dict)
+    name: str = ""
+    unit: str = ""
+
+    def step(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def work_per_step(self) -> float:
+        """Units of work per step per rank (flops, bytes, updates...)."""
+        raise NotImplementedError
+
+    def scale(self) -> float:
+        return 1e12 if self.unit == "TFLOPS" else 1e9
+
+    def report(self, seconds: float, steps: int) -> dict:
+        total = self.ctx.world * self.work_per_step() * steps / seconds / self.scale()
+        return {"value": total, "unit": self.unit, "ms_per_step": 1e3 * seconds / steps}
+
+    def check(self) -> dict:
+        return {}
+
+
+class Sgemm(Workload):
+    """C = A @ B, fp32 exact (MFMA v_mfma_f32_32x32x2_f32), per-rank operands (data-parallel, weak)."""
+
+    def __init__(self, ctx, n=8192, variant=-1, **_):
+        super().__init__(ctx, {"n": n, "variant": variant}, "sgemm", "TFLOPS")
+        dev = ctx.device
+        self.a = torch.empty(n, n, device=dev)
+        self.b = torch.empty(n, n, device=dev)
+        self.c = torch.empty(n, n, device=dev)
+        ops.rand_uniform_(self.a, 1000 + ctx.rank)
+        ops.rand_uniform_(self.b, 2000 + ctx.rank)
+        self.n, self.variant = n, variant
+
+    def step(self):
+        if self.ctx.device.type == "cuda":
+            ops.sgemm_out(self.a, self.b, self.c, variant=self.variant)
+        else:
+            torch.matmul(self.a, self.b, out=self.c)
+
+    def work_per_step(self):
+        return 2.0 * self.n ** 3
+
+    def check(self):
+        rows = torch.arange(0, self.n, max(1, self.n // 8), device=self.a.device)
+        ref = self.a[rows].double() @ self.b.double()
+        return {"max_rel_err_vs_fp64": ((self.c[rows].double() - ref).abs().max() / ref.abs().max()).item()}
+
+
+class Reduce(Workload):
+    """Global sum of world x n f32: local HBM-bound reduction + one-scalar RCCL all-reduce."""
+
+    def __init__(self, ctx, n=10**9, **_):
+        super().__init__(ctx, {"n": n}, "reduce", "GB/s")
+        self.x = torch.empty(int(n), device=ctx.device)
+        ops.rand_uniform_(self.x, 3000 + ctx.rank, 0.0, 1.0)
+        self.total = torch.zeros((), device=ctx.device)
+
+    def step(self):
+        s = ops.reduce(self.x, "sum").reshape(1).float()
+        self.ctx.all_reduce_(s)
+        self.total.copy_(s.reshape(()))
+
+    def work_per_step(self):
+        return 4.0 * self.x.numel()
+
+    def check(self):
+        ref = self.x.double().sum().reshape(1)
+        self.ctx.all_reduce_(ref)
+        return {"rel_err_vs_fp64": abs(self.total.item() - ref.item()) / abs(ref.item())}
+
+
+class Scan(Workload):
+    """Inclusive prefix sum across ranks: local totals all-gathered, rank offset fed to the single-pass
+    decoupled look-back scan as its initial value."""
+
+    def __init__(self, ctx, n=10**9, **_):
+        super().__init__(ctx, {"n": n}, "scan", "GB/s")
+        self.x = torch.empty(int(n), device=ctx.device)
+        ops.rand_uniform_(self.x, 4000 + ctx.rank, 0.0, 1.0)
+        self.y = None
+
+    def step(self):
+        self.y = global_scan(self.x, self.ctx)
+
+    def work_per_step(self):
+        return 12.0 * self.x.numel()  # reduce pass (4 B) + scan read (4 B) + write (4 B)
+
+    def check(self):
+        n = min(self.x.numel(), 1 << 20)
+        ref = torch.cumsum(self.x[:n].double(), 0)
+        # offset of this rank = sum of lower ranks' totals
+        tot = self.x.double().sum().reshape(1)
+        totals = self.ctx.all_gather(tot)
+        off = sum(float(t) for t in totals[: self.ctx.rank])
+        err = ((self.y[:n].double() - (ref + off)).abs().max() / (ref[-1] + off)).item()
+        return {"rel_err_vs_fp64": err}
+
+
+class Stencil(Workload):
+    """16384^2 bf16 5-point stencil, row slabs + 2-row halo exchange overlapped with the interior update.
+    Strong scaling across ranks when `global_n` is fixed (the grid is split); weak when `per_rank`."""
+
+    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, **_):
+        from ..parallel.stencil import StencilSlab
+
+        rows = n * (ctx.world if per_rank else 1)
+        super().__init__(ctx, {"n": n, "rows": rows}, "stencil", "GLUP/s")
+        self.slab = StencilSlab(ctx, rows, n)
+        self.overlap = overlap
+        self.cells_local = self.slab.rows * n
+
+    def step(self):
+        self.slab.step(self.overlap)
+
+    def work_per_step(self):
+        return float(self.cells_local)
+
+
+class SpMV(Workload):
+    """Power-law CSR SpMV (nnz-balanced row blocks) + all-gather of y: x <- A x."""
+
+    def __init__(self, ctx, n_rows=10_000_000, nnz=100_000_000, alpha=2.5, **_):
+        from ..parallel.spmv import DistributedSpMV
+
+        super().__init__(ctx, {"n_rows": n_rows, "nnz": nnz}, "spmv", "GFLOP/s")
+        self.d = DistributedSpMV.powerlaw(ctx, n_rows, nnz, alpha)
+        self.x = torch.empty(n_rows, device=ctx.device)
+        ops.rand_uniform_(self.x, 5, 0.0, 1.0)
+        self.y = None
+
+    def step(self):
+        self.y = self.d.step(self.x)
+
+    def work_per_step(self):
+        return 2.0 * self.d.local_nnz
+
+    def report(self, seconds, steps):
+        r = super().report(seconds, steps)
+        nnz_all = self.d.local_nnz
+        t = torch.tensor([float(nnz_all)], dtype=torch.float64, device=self.ctx.device)
+        self.ctx.all_reduce_(t)
+        r["value"] = 2.0 * t.item() * steps / seconds / 1e9  # strong scaling: fixed matrix, world-summed
+        bytes_ = t.item() * 8 + self.d.n * 8 * 2
+        r["effective_gbps"] = bytes_ * steps / seconds / 1e9
+        return r
+
+
+class Region3D(Workload):
+    """3-D region growing on the reference volume (512^3, seed (50,300,300)), LDS-tiled kernel."""
+
+    def __init__(self, ctx, dim=512, method="tiled", **_):
+        super().__init__(ctx, {"dim": dim}, "region3d", "Gvox/s")
+        self.data = ops.create_volume(dim, device=ctx.device)
+        self.method, self.region, self.launches = method, None, 0
+
+    def step(self):
+        self.region, self.launches = ops.region3d(self.data, method=self.method)
+
+    def work_per_step(self):
+        return float(self.data.numel())
+
+
+class Raycast(Workload):
+    def __init__(self, ctx, dim=512, image_dim=512, method="texture", **_):
+        super().__init__(ctx, {"dim": dim, "image_dim": image_dim}, "raycast", "Grays/s")
+        self.data = ops.create_volume(dim, device=ctx.device)
+        self.region, _ = ops.region3d(self.data)
+        self.image_dim, self.method = image_dim, method
+
+    def step(self):
+        self.image = ops.raycast(self.data, self.region, self.image_dim, method=self.method)
+
+    def work_per_step(self):
+        return float(self.image_dim ** 2)
+
+
+class Histeq(Workload):
+    def __init__(self, ctx, side=4096, **_):
+        super().__init__(ctx, {"side": side}, "histeq", "Gpix/s")
+        g = torch.Generator().manual_seed(7)
+        self.img = torch.randint(0, 200, (side, side), dtype=torch.uint8, generator=g).to(ctx.device)
+
+    def step(self):
+        self.out = ops.histeq(self.img)
+
+    def work_per_step(self):
+        return float(self.img.numel())
+
+
+WORKLOADS = {"sgemm": Sgemm, "reduce": Reduce, "scan": Scan, "stencil": Stencil, "spmv": SpMV,
+             "region3d": Region3D, "raycast": Raycast, "histeq": Histeq}
+
+
+def build_workload(name: str, ctx: Context, **cfg) -> Workload:
+    return WORKLOADS[name](ctx, **cfg)

@@ -1,0 +1,62 @@
+"""2-D 5-point stencil (explicit heat step) on bf16 slabs — north-star config "16384^2 bf16 + halo exchange".
+
+    u'[i][j] = c + k * (((n + s) + (w + e)) - 4c),  f32 arithmetic (no contraction), bf16 (RNE) storage;
+    the global boundary rows/columns are Dirichlet (copied).
+
+A slab is a (rows + 2, cols) bf16 tensor: row 0 and row rows+1 are halo rows (neighbour ranks' boundary
+rows, or unused at the global edge). Ancestor in the reference: the 4-neighbour update with a 1-cell halo of
+2-mpi-region-growing/region.c:250-353, 499-527.
+"""
+from __future__ import annotations
+
+import torch
+
+from .._native import ops
+
+DEFAULT_K = 0.2
+
+
+def stencil5_reference(slab: torch.Tensor, global_row0: int, global_rows: int, k: float = DEFAULT_K) -> torch.Tensor:
+    """Plain PyTorch f32 reference of one step on a slab (same operation order, bf16 rounding)."""
+    u = slab.float()
+    c = u[1:-1]
+    n, s = u[:-2], u[2:]
+    w = torch.roll(c, 1, dims=1)
+    e = torch.roll(c, -1, dims=1)
+    lap = ((n + s) + (w + e)) - 4.0 * c
+    res = c + torch.tensor(k, dtype=torch.float32) * lap
+    rows = torch.arange(slab.shape[0] - 2, device=slab.device) + global_row0
+    fixed = (rows == 0) | (rows == global_rows - 1)
+    res[fixed] = c[fixed]
+    res[:, 0] = c[:, 0]
+    res[:, -1] = c[:, -1]
+    out = slab.clone()
+    out[1:-1] = res.to(torch.bfloat16)
+    return out
+
+
+def stencil5_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, global_rows: int | None = None,
+                   k: float = DEFAULT_K, row_range: tuple[int, int] | None = None) -> torch.Tensor:
+    """One step u -> out over local rows [r0, r1) (default: all). Halo rows of `out` are untouched."""
+    rows = u.shape[0] - 2
+    global_rows = rows if global_rows is None else global_rows
+    r0, r1 = row_range or (0, rows)
+    if u.is_cuda:
+        ops().stencil5_(u, out, int(r0), int(r1), int(global_row0), int(global_rows), float(k))
+        return out
+    ref = stencil5_reference(u, global_row0, global_rows, k)
+    out[1 + r0:1 + r1] = ref[1 + r0:1 + r1]
+    return out
+
+
+def init_grid(rows: int, cols: int, global_row0: int = 0, global_rows: int | None = None, device="cpu",
+              halo: int = 1) -> torch.Tensor:
+    """Deterministic initial condition: hot top boundary row (1.0), a hot square in the middle, 0 elsewhere."""
+    global_rows = rows if global_rows is None else global_rows
+    g = torch.arange(global_row0 - halo, global_row0 + rows + halo, device=device).view(-1, 1).float()
+    c = torch.arange(cols, device=device).view(1, -1).float()
+    hot = ((g - global_rows / 2).abs() < global_rows / 8) & ((c - cols / 2).abs() < cols / 8)
+    u = hot.float() * 0.5
+    u = torch.where(g == 0, torch.ones_like(u), u)
+    u = torch.where((g < 0) | (g >= global_rows), torch.zeros_like(u), u)
+    return u.to(torch.bfloat16).contiguous()

@@ -1,0 +1,122 @@
+"""Process-group context: one process per GPU over RCCL (torch.distributed backend "nccl" is RCCL on ROCm,
+riding xGMI between MI355Xs), or gloo on CPU for GPU-less tests.
+
+Replaces the reference's MPI bootstrap (MPI_Init / Comm_size / Comm_rank / Finalize: 1-introduction/mpi.c:10-44,
+2-mpi-region-growing/region.c:537-548). Launch with
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 <script> ...
+or, for tests, `spawn(fn, world, backend="gloo")`.
+"""
+from __future__ import annotations
+
+import os
+import socket
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Context:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1 and dist.is_initialized()
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.distributed:
+            dist.all_reduce(t, op=_OPS[op])
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> list[torch.Tensor]:
+        if not self.distributed:
+            return [t]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t.contiguous())
+        return out
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.distributed:
+            dist.broadcast(t, src)
+        return t
+
+    def scalar(self, v, dtype=torch.float64) -> torch.Tensor:
+        return torch.tensor([v], dtype=dtype, device=self.device)
+
+    def max_over_ranks(self, v: float) -> float:
+        t = self.scalar(float(v))
+        self.all_reduce_(t, "max")
+        return float(t.item())
+
+
+_OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+
+
+def init(backend: str | None = None, device: str | None = None) -> Context:
+    """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
+
+    backend: "nccl" (RCCL, default when a GPU is visible) or "gloo" (CPU tensors)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = torch.cuda.is_available() if device is None else device.startswith("cuda")
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return Context(rank, world, local, dev, backend if world > 1 else "none")
+
+
+def finalize(ctx: Context | None = None) -> None:
+    if dist.is_initialized():
+        try:
+            if ctx is not None:
+                ctx.barrier()
+        finally:
+            dist.destroy_process_group()
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_entry(rank, fn, world, port, backend, args):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    ctx = init(backend=backend, device="cpu" if backend == "gloo" else None)
+    try:
+        fn(ctx, *args)
+    finally:
+        finalize(ctx)
+
+
+def spawn(fn, world: int, backend: str = "gloo", args: tuple = ()) -> None:
+    """Run fn(ctx, *args) in `world` local processes (CPU/gloo test harness; rendezvous on 127.0.0.1)."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_spawn_entry, args=(fn, world, free_port(), backend, args), nprocs=world, join=True)

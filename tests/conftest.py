@@ -31,6 +31,21 @@ def gpu():
     return torch.device("cuda", 0)
 
 
+def cli_env(**extra) -> dict:
+    """Environment for `python -m parallel_c_programs_amd.cli.*` subprocesses run from a tmp cwd."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env.update(extra)
+    return env
+
+
+def run_cli(module: str, *args, check=True, timeout=600, **env):
+    import subprocess
+
+    return subprocess.run([sys.executable, "-m", f"parallel_c_programs_amd.cli.{module}", *map(str, args)],
+                          capture_output=True, text=True, check=check, timeout=timeout, env=cli_env(**env))
+
+
 @pytest.fixture(autouse=True)
 def _chdir_tmp(tmp_path, monkeypatch):
     # tools that write ./out.bmp (reference contract) must not litter the repo

@@ -1,0 +1,177 @@
+"""GPU numerics of the image/volume/stencil/sparse/halo kernels against the host C oracles and plain
+PyTorch references (GPU only)."""
+import pytest
+import torch
+
+from parallel_c_programs_amd import ops
+from parallel_c_programs_amd.utils import bmp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["dark", "light", "peppers", "pic2"])
+def test_histeq_bit_exact(gpu, assets, name):
+    img = torch.from_numpy(bmp.read(assets / f"{name}.bmp").copy())
+    ref = ops.histeq(img, "serial")
+    for method in ("auto", "multiblock"):
+        out = ops.histeq(img.to(gpu), method).cpu()
+        assert torch.equal(out, ref), method
+
+
+def test_histeq_large_random(gpu):
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (3000, 2999), dtype=torch.uint8, generator=g)
+    ref = ops.histeq(img, "serial")
+    assert torch.equal(ops.histeq(img.to(gpu)).cpu(), ref)
+    assert torch.equal(ops.histeq(img.to(gpu), "multiblock").cpu(), ref)
+
+
+def test_region2d_golden(gpu, assets):
+    img = torch.from_numpy(bmp.read(assets / "pic1.bmp").copy())
+    gold = torch.from_numpy(bmp.read(assets / "region_pic1_golden.bmp").copy())
+    reg = ops.region2d(img.to(gpu)).cpu()
+    assert int(reg.sum()) == 64420
+    assert torch.equal(ops.apply_region_mask(img, reg), gold)
+
+
+@pytest.mark.parametrize("name", ["pic2", "pic3", "pic4"])
+def test_region2d_vs_serial(gpu, assets, name):
+    img = torch.from_numpy(bmp.read(assets / f"{name}.bmp").copy())
+    assert torch.equal(ops.region2d(img.to(gpu)).cpu(), ops.region2d(img))
+
+
+def test_region2d_random_maze(gpu):
+    g = torch.Generator().manual_seed(5)
+    img = (torch.rand(700, 900, generator=g) < 0.45).to(torch.uint8) * 9  # 0/9 maze, threshold 2
+    seeds = [(3, 3), (450, 350), (899, 699)]
+    ref = ops.region2d(img, seeds=seeds)
+    assert torch.equal(ops.region2d(img.to(gpu), seeds=seeds).cpu(), ref)
+
+
+def test_volume_gen_matches_host(gpu):
+    v_gpu = ops.create_volume(128, device=gpu, seed=7).cpu()
+    v_cpu = ops.create_volume(128, device="cpu", seed=7)
+    assert torch.equal(v_gpu, v_cpu)
+
+
+@pytest.mark.parametrize("method", ["tiled", "naive"])
+def test_region3d_small(gpu, method):
+    vol = ops.create_volume(128, device="cpu", seed=3)
+    ref, _ = ops.region3d(vol, seed=(50, 100, 100), threshold=1)
+    reg, n = ops.region3d(vol.to(gpu), seed=(50, 100, 100), threshold=1, method=method)
+    assert torch.equal((reg.cpu() != 0).to(torch.uint8), ref)
+    assert n >= 1
+
+
+def test_region3d_reference_box(gpu):
+    # T2: the region from seed (50,300,300) is exactly the 99x149x149 box (2,197,899 voxels)
+    vol = ops.create_volume(512, device=gpu, seed=0)
+    reg, launches = ops.region3d(vol, threshold=1, method="tiled")
+    assert int((reg != 0).sum().item()) == 2_197_899
+    box = torch.zeros(512, 512, 512, dtype=torch.bool, device=gpu)
+    box[251:400, 251:400, 1:100] = True
+    assert torch.equal(reg != 0, box)
+
+
+@pytest.mark.parametrize("image_dim", [64, 128])
+def test_raycast_global_bit_exact(gpu, image_dim):
+    vol = ops.create_volume(512, device="cpu", seed=0)
+    reg, _ = ops.region3d(vol, threshold=1)
+    ref = ops.raycast(vol, reg, image_dim)
+    out = ops.raycast(vol.to(gpu), reg.to(gpu), image_dim, method="global").cpu()
+    assert torch.equal(out, ref)
+
+
+def test_raycast_reference_data_golden(gpu):
+    # T5: glibc-rand reference volume, 64x64 image sum = 127180 with 100 saturated pixels
+    vol = ops.create_volume(512, background="rand")
+    reg, _ = ops.region3d(vol.to(gpu), threshold=1)
+    img = ops.raycast(vol.to(gpu), (reg != 0).to(torch.uint8), 64, method="global").cpu()
+    assert int(img.sum()) == 127180 and int((img == 255).sum()) == 100
+
+
+def test_raycast_texture_close(gpu):
+    vol = ops.create_volume(512, device=gpu, seed=0)
+    reg, _ = ops.region3d(vol, threshold=1)
+    reg = (reg != 0).to(torch.uint8)
+    a = ops.raycast(vol, reg, 128, method="global").float()
+    b = ops.raycast(vol, reg, 128, method="texture").float()
+    assert (a - b).abs().mean().item() < 6.0
+    assert abs(a.mean().item() - b.mean().item()) < 3.0
+
+
+@pytest.mark.parametrize("shape", [(256, 512), (1000, 1024), (515, 4096)])
+def test_stencil_bit_exact(gpu, shape):
+    rows, cols = shape
+    u = ops.init_grid(rows, cols, device="cpu")
+    ref = u.clone()
+    for _ in range(3):
+        ref = ops.stencil5_reference(ref, 0, rows)
+    a = u.to(gpu)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    for _ in range(3):
+        ops.stencil5_step_(a, b, 0, rows)
+        a, b = b, a
+    assert torch.equal(a.cpu()[1:-1], ref[1:-1])
+
+
+def test_stencil_row_range_split(gpu):
+    rows, cols = 512, 1024
+    u = ops.init_grid(rows, cols, device=gpu)
+    full = u.clone()
+    ops.stencil5_step_(u, full, 0, rows)
+    part = u.clone()
+    ops.stencil5_step_(u, part, 0, rows, row_range=(1, rows - 1))
+    ops.stencil5_step_(u, part, 0, rows, row_range=(0, 1))
+    ops.stencil5_step_(u, part, 0, rows, row_range=(rows - 1, rows))
+    assert torch.equal(full, part)
+
+
+def test_spmv_banded_vs_host(gpu):
+    m = ops.banded_csr(20000, 41, 20, 10, 20, 5)
+    x = ops.create_vector(20000)
+    ref = ops.spmv(m, x)
+    out = ops.spmv_banded(m.val.to(gpu), m.row_ptr.to(gpu), 20000, 41, 20, 10, 20, 5, x.to(gpu)).cpu()
+    assert (out - ref).abs().max().item() < 1e-3
+    out_csr = ops.spmv(m.to(gpu), x.to(gpu)).cpu()
+    assert (out_csr - ref).abs().max().item() < 1e-3
+
+
+def test_spmv_powerlaw_vs_dense(gpu):
+    m = ops.powerlaw_csr(3000, 200_000, alpha=2.2, seed=11)
+    x = torch.rand(3000)
+    ref = m.dense().double() @ x.double()
+    out = ops.spmv(m.to(gpu), x.to(gpu)).cpu().double()
+    assert ((out - ref).abs() / (ref.abs() + 1)).max().item() < 1e-4
+
+
+def test_spmv_long_rows(gpu):
+    # rows longer than one work item (split + atomics) next to empty rows
+    n = 50
+    lens = torch.tensor([0, 5000, 3, 0, 2049, 1] + [7] * (n - 6))
+    rp = torch.zeros(n + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(lens, 0)
+    nnz = int(rp[-1])
+    g = torch.Generator().manual_seed(2)
+    col = torch.randint(0, 4000, (nnz,), dtype=torch.int32, generator=g)
+    val = torch.rand(nnz, generator=g)
+    m = ops.CSR(rp, col, val, 4000)
+    x = torch.rand(4000, generator=g)
+    ref = m.dense().double() @ x.double()
+    out = ops.spmv(m.to(gpu), x.to(gpu)).cpu().double()
+    assert (out - ref).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.uint8, torch.bfloat16, torch.float32])
+def test_halo_pack_unpack(gpu, dtype):
+    H, W = 37, 53
+    t = (torch.arange((H + 2) * (W + 2)) % 251).to(dtype).view(H + 2, W + 2).contiguous()
+    buf_ref = ops.pack_edges(t)
+    buf = ops.pack_edges(t.to(gpu)).cpu()
+    assert torch.equal(buf, buf_ref)
+    dst = torch.zeros_like(t)
+    ops.unpack_halo_(dst, buf_ref)
+    dg = torch.zeros_like(t).to(gpu)
+    ops.unpack_halo_(dg, buf_ref.to(gpu))
+    assert torch.equal(dg.cpu(), dst)

@@ -1,0 +1,235 @@
+"""Distributed layer on the CPU (gloo backend, real multi-process rendezvous on 127.0.0.1).
+
+The same code paths run over RCCL on MI355X; here every distributed result is compared with the
+single-process oracle of the same operation (SURVEY §4 strategy: golden outputs + independent models).
+"""
+import numpy as np
+import pytest
+import torch
+from conftest import ASSETS, run_cli
+
+from parallel_c_programs_amd import ops
+from parallel_c_programs_amd.parallel import (CartTopology, DistributedSpMV, HaloExchanger2D, StencilSlab,
+                                              dims_create, global_reduce, global_scan, grow_distributed,
+                                              nnz_balanced_cuts, reference_run, spawn, split, token_ring)
+from parallel_c_programs_amd.utils import bmp
+
+
+# ------------------------------------------------------------------ pure topology (no processes)
+
+@pytest.mark.parametrize("n,dims", [(1, [1, 1]), (2, [2, 1]), (4, [2, 2]), (6, [3, 2]), (8, [4, 2]), (12, [4, 3]),
+                                    (16, [4, 4]), (7, [7, 1])])
+def test_dims_create_matches_mpi(n, dims):
+    assert dims_create(n) == dims
+
+
+def test_cart_topology_tiles_cover_image():
+    for world in (1, 2, 3, 4, 8):
+        topo = CartTopology.create(world)
+        H, W = 37, 53
+        cover = np.zeros((H, W), dtype=int)
+        for r in range(world):
+            r0, r1, c0, c1 = topo.tile(r, H, W)
+            cover[r0:r1, c0:c1] += 1
+            nb = topo.neighbours(r)
+            row, col = topo.coords(r)
+            assert nb["north"] == (topo.rank_of(row - 1, col))
+            if nb["east"] >= 0:
+                assert topo.coords(nb["east"]) == (row, col + 1)
+        assert (cover == 1).all()
+
+
+def test_split_balanced():
+    sizes = [split(10, 4, i) for i in range(4)]
+    assert sizes == [(0, 3), (3, 6), (6, 8), (8, 10)]
+
+
+def test_nnz_cuts_balance():
+    rp = ops.sparse.powerlaw_row_ptr(20000, 400000)
+    cuts = nnz_balanced_cuts(rp, 4)
+    nnz = [int(rp[cuts[i + 1]] - rp[cuts[i]]) for i in range(4)]
+    assert cuts[0] == 0 and cuts[-1] == 20000
+    assert max(nnz) < 1.25 * (sum(nnz) / 4)
+
+
+def test_powerlaw_rows_bit_identical():
+    full = ops.powerlaw_csr(5000, 60000, seed=3)
+    part = ops.sparse.powerlaw_csr_rows(full.row_ptr, 1200, 3100, 5000, seed=3)
+    a, b = int(full.row_ptr[1200]), int(full.row_ptr[3100])
+    assert torch.equal(part.col, full.col[a:b]) and torch.equal(part.val, full.val[a:b])
+
+
+# ------------------------------------------------------------------ multi-process (gloo)
+
+def _ring(ctx, out_q):
+    out_q.put((ctx.rank, token_ring(ctx, verbose=False)))
+
+
+class _Out:
+    """Per-rank result sink backed by files (a pipe-backed queue would block writers of large results
+    until the parent reads, but the parent only reads after the ranks are joined)."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def put(self, kv):
+        import pickle
+
+        k, v = kv
+        with open(f"{self.d}/{k}.pkl", "wb") as f:
+            pickle.dump(v, f)
+
+
+def _collect(world, fn, *args):
+    import os
+    import pickle
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        spawn(fn, world, "gloo", (_Out(d), *args))
+        res = {}
+        for name in os.listdir(d):
+            with open(os.path.join(d, name), "rb") as f:  # files written by this test's own ranks
+                res[int(name.split(".")[0])] = pickle.load(f)
+    return res
+
+
+def test_token_ring_world4():
+    res = _collect(4, _ring)
+    assert res[0] == 2 * 4 - 2
+    assert res[3] == 3  # top of the chain: received 3, no increment after
+
+
+def _halo(ctx, q):
+    topo = CartTopology.create(ctx.world)
+    H, W = 12, 10
+    full = torch.arange(H * W, dtype=torch.float32).view(H, W)
+    r0, r1, c0, c1 = topo.tile(ctx.rank, H, W)
+    padded = torch.nn.functional.pad(full, (1, 1, 1, 1), value=-1.0)
+    tile = torch.full((r1 - r0 + 2, c1 - c0 + 2), -1.0)
+    tile[1:-1, 1:-1] = full[r0:r1, c0:c1]
+    HaloExchanger2D(ctx, topo).exchange_(tile)
+    expect = padded[r0:r1 + 2, c0:c1 + 2].clone()
+    # corners are not exchanged (4-connectivity); compare edges only
+    for t in (tile, expect):
+        t[0, 0] = t[0, -1] = t[-1, 0] = t[-1, -1] = 0
+    q.put((ctx.rank, bool(torch.equal(tile, expect))))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_halo_exchange_matches_padded_slices(world):
+    res = _collect(world, _halo)
+    assert all(res.values()) and len(res) == world
+
+
+def _reduce_scan(ctx, q):
+    g = torch.Generator().manual_seed(10 + ctx.rank)
+    x = torch.rand(1000 + 37 * ctx.rank, generator=g)
+    s = global_reduce(x, ctx)
+    mx = global_reduce(x, ctx, "max")
+    y = global_scan(x, ctx)
+    q.put((ctx.rank, (float(s), float(mx), y.numpy(), x.numpy())))
+
+
+def test_global_reduce_and_scan_world3():
+    res = _collect(3, _reduce_scan)
+    xs = [torch.from_numpy(res[r][3]) for r in range(3)]
+    cat = torch.cat(xs).double()
+    for r in range(3):
+        assert abs(res[r][0] - cat.sum().item()) < 1e-3
+        assert res[r][1] == pytest.approx(cat.max().item())
+    ys = torch.cat([torch.from_numpy(res[r][2]) for r in range(3)]).double()
+    assert torch.allclose(ys, torch.cumsum(cat, 0), rtol=1e-5, atol=1e-3)
+
+
+def _region(ctx, q, path):
+    img = torch.from_numpy(bmp.read(path)) if ctx.is_root else None
+    stats = {}
+    reg = grow_distributed(ctx, img, 2, stats=stats)
+    if ctx.is_root:
+        q.put((0, (reg.numpy(), stats)))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_distributed_region_equals_serial(world):
+    path = str(ASSETS / "pic1.bmp")
+    res = _collect(world, _region, path)
+    reg, stats = res[0]
+    reg = torch.from_numpy(reg)
+    img = torch.from_numpy(bmp.read(path))
+    serial = ops.region2d(img)
+    assert torch.equal(reg, serial)
+    assert stats["outer_steps"] >= 2  # the region crosses tile borders
+
+
+def _stencil(ctx, q, n, cols, steps, overlap):
+    slab = StencilSlab(ctx, n, cols)
+    slab.run(steps, overlap)
+    full = slab.gather()
+    if ctx.is_root:
+        q.put((0, full.view(torch.int16).numpy()))
+
+
+@pytest.mark.parametrize("world,overlap", [(2, True), (3, False), (4, True)])
+def test_distributed_stencil_bit_exact(world, overlap):
+    n, cols, steps = 64, 48, 7
+    res = _collect(world, _stencil, n, cols, steps, overlap)
+    ref = reference_run(n, steps, cols)
+    assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
+
+
+def _spmv(ctx, q, n, nnz):
+    d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1)
+    x = torch.linspace(0, 1, n)
+    y = d.step(x)
+    y2 = d.step(y / y.abs().max())
+    q.put((ctx.rank, (y.numpy(), y2.numpy())))
+
+
+def test_distributed_spmv_world3():
+    n, nnz = 3000, 40000
+    res = _collect(3, _spmv, n, nnz)
+    m = ops.powerlaw_csr(n, nnz, seed=1)
+    x = torch.linspace(0, 1, n)
+    y = ops.spmv(m, x)
+    y2 = ops.spmv(m, y / y.abs().max())
+    for r in range(3):
+        assert torch.allclose(torch.from_numpy(res[r][0]), y, rtol=1e-5, atol=1e-5)
+        assert torch.allclose(torch.from_numpy(res[r][1]), y2, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------ launcher-level (torch.distributed.run)
+
+def _torchrun(nproc, module, *args):
+    import subprocess
+    import sys
+
+    from conftest import cli_env
+    from parallel_c_programs_amd.parallel import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+           f"parallel_c_programs_amd.cli.{module}", *map(str, args)]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=cli_env(OMP_NUM_THREADS="1"))
+
+
+def test_cli_region_torchrun_writes_golden(tmp_path):
+    r = _torchrun(4, "run_region", ASSETS / "pic1.bmp", "--backend", "gloo")
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = bmp.read(tmp_path / "out.bmp")
+    golden = bmp.read(ASSETS / "region_pic1_golden.bmp")
+    assert np.array_equal(out, golden)
+
+
+def test_cli_mpi_ring_prints_reference_lines():
+    r = _torchrun(3, "run_mpi_ring", "--backend", "gloo")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = set(r.stdout.splitlines())
+    for want in ["Rank 0 sent 0 ", "Rank 1 received 0 ", "Rank 1 sent 1 ", "Rank 2 received 1 ",
+                 "Rank 2 sent 2 ", "Rank 1 received 2 ", "Rank 1 sent 3 ", "Rank 0 received 3 "]:
+        assert want in lines
+
+
+def test_cli_region_usage_message():
+    r = run_cli("run_region", check=False)
+    assert r.stdout == "Useage: region file" and r.returncode == 255
