@@ -25,22 +25,40 @@ struct Item {
     long long nz0, nz1;    // nonzeros [nz0, nz1)
 };
 
+constexpr int kItemRows = 1024;           // rows per multi-row item (bounds the row-pointer LDS stage)
+constexpr int kPerLane = kItemNnz / kWave;  // nonzeros per lane in phase 1
+
+// One wave per item. Phase 1 issues every column/value load of the item up front (kPerLane coalesced
+// 256-B wave loads each), then all x gathers, so a lane keeps 2 x kPerLane loads in flight instead of a
+// dependent load chain. Products are parked in LDS with the item's row pointers; phase 2 reduces rows
+// with L lanes per row out of LDS only.
 __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_csr_items_kernel(
     const long long* __restrict__ row_ptr, const int* __restrict__ col, const float* __restrict__ val,
     const float* __restrict__ x, float* __restrict__ y, const Item* __restrict__ items, long long n_items) {
     __shared__ float prod[kWavesPerBlock][kItemNnz];
+    __shared__ int rps[kWavesPerBlock][kItemRows + 1];
     const int lane = pcmx::lane_id(), w = threadIdx.x / kWave;
     const long long it = (long long)blockIdx.x * kWavesPerBlock + w;
     if (it >= n_items) return;
     const Item item = items[it];
-    const long long nz0 = item.nz0, nz1 = item.nz1;
+    const long long nz0 = item.nz0;
+    const int n = (int)(item.nz1 - nz0);
     const int nrows = item.row1 - item.row0;
+    int cj[kPerLane];
+    float vj[kPerLane];
+#pragma unroll
+    for (int j = 0; j < kPerLane; ++j) {
+        const int i = j * kWave + lane;
+        cj[j] = i < n ? __builtin_nontemporal_load(col + nz0 + i) : 0;
+        vj[j] = i < n ? __builtin_nontemporal_load(val + nz0 + i) : 0.f;
+    }
     if (nrows == 1) {  // single row (whole short row, or one piece of a long row)
         float acc = 0.f;
-        for (long long p = nz0 + lane; p < nz1; p += kWave) acc += val[p] * x[col[p]];
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) acc += vj[j] * x[cj[j]];
         acc = pcmx::wave_reduce<float, 0>(acc);
         if (lane == 0) {
-            const bool whole = nz0 == row_ptr[item.row0] && nz1 == row_ptr[item.row0 + 1];
+            const bool whole = nz0 == row_ptr[item.row0] && item.nz1 == row_ptr[item.row0 + 1];
             if (whole)
                 y[item.row0] = acc;
             else
@@ -49,20 +67,23 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_csr_items_kernel(
         return;
     }
     float* pr = prod[w];
-    const int n = (int)(nz1 - nz0);
-    for (int i = lane; i < n; i += kWave) pr[i] = val[nz0 + i] * x[col[nz0 + i]];
+    int* rp = rps[w];
+#pragma unroll
+    for (int j = 0; j < kPerLane; ++j) pr[j * kWave + lane] = vj[j] * x[cj[j]];
+    for (int i = lane; i <= nrows; i += kWave) rp[i] = (int)(row_ptr[item.row0 + i] - nz0);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // L lanes per row, L = largest power of two with nrows * L <= 64 (at least 1)
-    int L = 64;
-    while (L > 1 && nrows * L > kWave) L >>= 1;
-    const int sub = lane % L, grp = lane / L, ngrp = kWave / L;
-    for (int r = item.row0 + grp; r < item.row1; r += ngrp) {
-        const int b = (int)(row_ptr[r] - nz0), e = (int)(row_ptr[r + 1] - nz0);
+    // L lanes per row: about avg-row-length / 4 lanes, power of two, at most 64 / (rows per pass)
+    const int avg = n / nrows;
+    int L = 1;
+    while (L < 64 && L * 4 < avg) L <<= 1;
+    const int sub = lane & (L - 1), grp = lane / L, ngrp = kWave / L;
+    for (int r = grp; r < nrows; r += ngrp) {
+        const int b = rp[r], e = rp[r + 1];
         float acc = 0.f;
         for (int i = b + sub; i < e; i += L) acc += pr[i];
         for (int off = L >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
-        if (sub == 0) y[r] = acc;
+        if (sub == 0) y[item.row0 + r] = acc;
     }
 }
 
@@ -113,7 +134,7 @@ extern "C" long long pcmx_spmv_csr_plan(const long long* row_ptr, int n_rows, vo
             continue;
         }
         int r1 = r + 1;
-        while (r1 < n_rows && row_ptr[r1 + 1] - row_ptr[r] <= kItemNnz && r1 - r < 4096) ++r1;
+        while (r1 < n_rows && row_ptr[r1 + 1] - row_ptr[r] <= kItemNnz && r1 - r < kItemRows) ++r1;
         if (items && k < max_items) items[k] = Item{r, r1, row_ptr[r], row_ptr[r1]};
         ++k;
         r = r1;

@@ -62,7 +62,7 @@ def _run(cmd, cwd=None):
 
 
 CPU_SRCS = ["cpu/bmp.c", "cpu/matrix.c", "cpu/spmv.c", "cpu/histogram.c", "cpu/vec.c", "cpu/oracles.c",
-            "cpu/demos.c"]
+            "cpu/demos.c", "comm/comm_tcp.c", "comm/region_dist.c"]
 CFLAGS = ["-O3", "-fPIC", "-std=gnu11", "-fopenmp", "-march=x86-64-v3", "-Wall", "-Wno-unknown-pragmas",
           f"-I{CSRC / 'include'}"]
 # files whose float rounding must match the reference build bit-for-bit
@@ -90,7 +90,8 @@ def build_cpu(force=False, jobs=8):
 
 
 HIP_SRCS = sorted(str(p.relative_to(CSRC)) for p in (CSRC / "kernels").glob("*.hip")) + \
-    sorted(str(p.relative_to(CSRC)) for p in (CSRC / "runtime").glob("*.hip"))
+    sorted(str(p.relative_to(CSRC)) for p in (CSRC / "runtime").glob("*.hip")) + \
+    sorted(str(p.relative_to(CSRC)) for p in (CSRC / "comm").glob("*.hip"))
 HIPFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
             f"-I{CSRC / 'include'}", f"-I{CSRC / 'kernels'}", f"-I{CSRC / 'runtime'}",
             "-Wno-unused-result", "-Wno-pass-failed"]
@@ -150,6 +151,9 @@ BIN_TOOLS = {
     "vecops": ("bin/vecops_main.c", "c"),
     "raycast": ("bin/raycast_main.cpp", "hip"),
     "device_info": ("bin/device_info_main.cpp", "hip"),
+    "region": ("bin/region_main.cpp", "hip"),
+    "mpi_ring": ("bin/mpi_ring_main.cpp", "hip"),
+    "pcmx_launch": ("bin/launch_main.c", "c"),
 }
 
 

@@ -1,0 +1,106 @@
+"""End-to-end GPU runs of the application layer: CLIs with the reference's argv/outputs and the north-star
+workloads at reduced sizes, each with its numerics check (fp64 / host oracle)."""
+import numpy as np
+import pytest
+import torch
+from conftest import ASSETS, run_cli
+
+from parallel_c_programs_amd import ops
+from parallel_c_programs_amd.models import build_workload
+from parallel_c_programs_amd.parallel import Context, grow_distributed
+from parallel_c_programs_amd.utils import bmp
+from parallel_c_programs_amd.utils.harness import timed
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    return Context(device=torch.device("cuda", 0))
+
+
+def test_region_cli_gpu_golden(gpu, tmp_path):
+    run_cli("run_region", ASSETS / "pic1.bmp")
+    assert np.array_equal(bmp.read(tmp_path / "out.bmp"), bmp.read(ASSETS / "region_pic1_golden.bmp"))
+
+
+def test_grow_distributed_single_rank_gpu(gpu, ctx):
+    img = torch.from_numpy(bmp.read(ASSETS / "pic2.bmp"))
+    reg = grow_distributed(ctx, img, 2)
+    assert torch.equal(reg.cpu(), ops.region2d(img))
+
+
+@pytest.mark.parametrize("method", ["serial", "gpu"])
+def test_histogram_cli(gpu, tmp_path, method):
+    run_cli("run_histogram", ASSETS / "peppers.bmp", 4, "--method", method)
+    out = bmp.read(tmp_path / "out.bmp")
+    ref = ops.histeq(torch.from_numpy(bmp.read(ASSETS / "peppers.bmp")))
+    assert np.array_equal(out, ref.numpy())
+
+
+def test_vmul_cli_table(gpu):
+    lines = run_cli("run_vmul").stdout.splitlines()
+    i = lines.index("Host\tDevice")
+    assert lines[i + 1:i + 11] == ["1.00\t1.00"] * 10
+
+
+def test_raycast_cli_opencl_variant(gpu, tmp_path):
+    run_cli("run_raycast", "--opencl", timeout=900)
+    img = bmp.read(tmp_path / "out.bmp")
+    assert img.shape == (64, 64) and img.max() > 0
+
+
+def test_raycast_cli_cuda_variant(gpu, tmp_path):
+    r = run_cli("run_raycast", timeout=900)
+    assert "Grow time:" in r.stdout and "Raycast time: " in r.stdout
+    img = bmp.read(tmp_path / "out.bmp")
+    assert img.shape == (512, 512) and img.max() > 0
+
+
+def test_spmv_cli_gpu(gpu):
+    r = run_cli("run_spmv", 20000, 41, 20, 10, 20, 10, "--gpu")
+    lines = r.stdout.splitlines()
+    assert sum(ln.startswith("Time : ") for ln in lines) == 2
+    assert any(ln.startswith("GPU CSR-adaptive") for ln in lines)
+
+
+@pytest.mark.parametrize("name,cfg,key,tol", [
+    ("sgemm", {"n": 1024}, "max_rel_err_vs_fp64", 1e-5),
+    ("reduce", {"n": 10_000_000}, "rel_err_vs_fp64", 1e-5),
+    ("scan", {"n": 10_000_000}, "rel_err_vs_fp64", 1e-4),
+])
+def test_workloads_numerics(gpu, ctx, name, cfg, key, tol):
+    w = build_workload(name, ctx, **cfg)
+    secs = timed(ctx, w.step, 2, 1)
+    rep = w.report(secs, 2)
+    assert rep["value"] > 0
+    assert w.check()[key] < tol
+
+
+def test_stencil_workload_matches_reference(gpu, ctx):
+    from parallel_c_programs_amd.parallel import reference_run
+
+    w = build_workload("stencil", ctx, n=512)
+    for _ in range(5):
+        w.step()
+    ref = reference_run(512, 5, device="cpu")
+    assert torch.equal(w.slab.interior().cpu().view(torch.int16), ref.view(torch.int16))
+
+
+def test_spmv_workload_matches_host(gpu, ctx):
+    w = build_workload("spmv", ctx, n_rows=200_000, nnz=2_000_000)
+    w.step()
+    m = ops.powerlaw_csr(200_000, 2_000_000)
+    ref = ops.spmv(m, w.x.cpu())
+    assert torch.allclose(w.y.cpu(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_region3d_raycast_workloads(gpu, ctx):
+    r = build_workload("region3d", ctx, dim=512)
+    r.step()
+    assert r.launches > 0 and int(r.region.sum()) > 0
+    rc = build_workload("raycast", ctx, dim=512, image_dim=256)
+    rc.step()
+    assert rc.image.shape == (256, 256)
