@@ -10,6 +10,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
+#include <unistd.h>
+#include <vector>
 
 #include "pcmx_comm.h"
 #include "pcmx_hip.h"
@@ -49,7 +52,48 @@ int r_allreduce(pcmx_comm_t* c, void* b, size_t n, int dt, int op) {
 int r_bcast(pcmx_comm_t* c, void* b, size_t n, int root) {
     return rc_of(ncclBroadcast(b, b, n, ncclUint8, root, impl(c)->comm, impl(c)->stream));
 }
-int r_sync(pcmx_comm_t* c) { return (int)hipStreamSynchronize(impl(c)->stream); }
+// Failure detection: wait for the stream while polling RCCL's asynchronous error state, with a deadline
+// (PCMX_COMM_TIMEOUT seconds, default 600). On error/timeout the communicator is aborted so peers blocked in
+// collectives fail too instead of hanging.
+double g_timeout_s = -1.0;
+double comm_timeout() {
+    if (g_timeout_s < 0) {
+        const char* v = getenv("PCMX_COMM_TIMEOUT");
+        g_timeout_s = v && *v ? atof(v) : 600.0;
+    }
+    return g_timeout_s;
+}
+double wall() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+int r_sync(pcmx_comm_t* c) {
+    RcclImpl* r = impl(c);
+    const double t0 = wall();
+    for (;;) {
+        hipError_t q = hipStreamQuery(r->stream);
+        if (q == hipSuccess) return 0;
+        if (q != hipErrorNotReady) return (int)q;
+        ncclResult_t async = ncclSuccess;
+        ncclCommGetAsyncError(r->comm, &async);
+        if (async != ncclSuccess && async != ncclInProgress) {
+            fprintf(stderr, "pcmx_comm: rank %d RCCL async error %d (%s); aborting communicator\n", c->rank,
+                    (int)async, ncclGetErrorString(async));
+            ncclCommAbort(r->comm);
+            r->comm = nullptr;
+            return 1000 + (int)async;
+        }
+        if (wall() - t0 > comm_timeout()) {
+            fprintf(stderr, "pcmx_comm: rank %d timed out after %.0f s; aborting communicator\n", c->rank,
+                    comm_timeout());
+            ncclCommAbort(r->comm);
+            r->comm = nullptr;
+            return -110;
+        }
+        usleep(50);
+    }
+}
 void r_destroy(pcmx_comm_t* c) {
     RcclImpl* r = impl(c);
     if (r) {
@@ -63,6 +107,103 @@ void r_destroy(pcmx_comm_t* c) {
 }
 
 const pcmx_comm_ops_t kRcclOps = {r_group_start, r_group_end, r_send, r_recv, r_allreduce, r_bcast, r_sync, r_destroy};
+
+// ---------------------------------------------------------------- staged TCP transport (device buffers)
+// Device buffers moved through host memory over the TCP transport: lets P ranks share ONE GPU (RCCL refuses
+// duplicate devices), so the multi-rank GPU path (kernels + pack/unpack + exchange schedule) is testable on a
+// single MI355X — the loopback fixture of SURVEY §4 layer 3. Not a performance path.
+struct StagedOp {
+    void* dev;
+    std::vector<unsigned char> host;
+};
+struct StagedImpl {
+    hipStream_t stream = nullptr;
+    int depth = 0;
+    std::vector<StagedOp> recvs;  // completed into device memory at group end
+    std::vector<std::vector<unsigned char>> sends;
+};
+StagedImpl* simpl(pcmx_comm_t* c) { return static_cast<StagedImpl*>(c->impl); }
+int s_group_start(pcmx_comm_t* c) {
+    if (simpl(c)->depth++ == 0) return c->host->ops->group_start(c->host);
+    return 0;
+}
+int s_finish(pcmx_comm_t* c) {
+    StagedImpl* s = simpl(c);
+    int rc = c->host->ops->group_end(c->host);
+    for (auto& r : s->recvs)
+        if (!rc) rc = (int)hipMemcpyAsync(r.dev, r.host.data(), r.host.size(), hipMemcpyHostToDevice, s->stream);
+    if (!rc) rc = (int)hipStreamSynchronize(s->stream);
+    s->recvs.clear();
+    s->sends.clear();
+    return rc;
+}
+int s_group_end(pcmx_comm_t* c) {
+    if (--simpl(c)->depth == 0) return s_finish(c);
+    return 0;
+}
+int s_send(pcmx_comm_t* c, const void* b, size_t n, int peer) {
+    StagedImpl* s = simpl(c);
+    s->sends.emplace_back(n);
+    int rc = (int)hipMemcpyAsync(s->sends.back().data(), b, n, hipMemcpyDeviceToHost, s->stream);
+    if (!rc) rc = (int)hipStreamSynchronize(s->stream);
+    if (rc) return rc;
+    if (s->depth == 0) {
+        s_group_start(c);
+        rc = c->host->ops->send(c->host, s->sends.back().data(), n, peer);
+        int rc2 = s_group_end(c);
+        return rc ? rc : rc2;
+    }
+    return c->host->ops->send(c->host, s->sends.back().data(), n, peer);
+}
+int s_recv(pcmx_comm_t* c, void* b, size_t n, int peer) {
+    StagedImpl* s = simpl(c);
+    const bool lone = s->depth == 0;
+    if (lone) s_group_start(c);
+    s->recvs.push_back(StagedOp{b, std::vector<unsigned char>(n)});
+    int rc = c->host->ops->recv(c->host, s->recvs.back().host.data(), n, peer);
+    if (lone) {
+        int rc2 = s_group_end(c);
+        return rc ? rc : rc2;
+    }
+    return rc;
+}
+size_t dt_size(int dt) { return dt == PCMX_F64 || dt == PCMX_I64 ? 8 : dt == PCMX_U8 ? 1 : 4; }
+int s_allreduce(pcmx_comm_t* c, void* b, size_t n, int dt, int op) {
+    StagedImpl* s = simpl(c);
+    std::vector<unsigned char> h(n * dt_size(dt));
+    int rc = (int)hipMemcpyAsync(h.data(), b, h.size(), hipMemcpyDeviceToHost, s->stream);
+    if (!rc) rc = (int)hipStreamSynchronize(s->stream);
+    if (!rc) rc = c->host->ops->allreduce(c->host, h.data(), n, dt, op);
+    if (!rc) rc = (int)hipMemcpyAsync(b, h.data(), h.size(), hipMemcpyHostToDevice, s->stream);
+    if (!rc) rc = (int)hipStreamSynchronize(s->stream);
+    return rc;
+}
+int s_bcast(pcmx_comm_t* c, void* b, size_t n, int root) {
+    StagedImpl* s = simpl(c);
+    std::vector<unsigned char> h(n);
+    int rc = 0;
+    if (c->rank == root) {
+        rc = (int)hipMemcpyAsync(h.data(), b, n, hipMemcpyDeviceToHost, s->stream);
+        if (!rc) rc = (int)hipStreamSynchronize(s->stream);
+    }
+    if (!rc) rc = c->host->ops->bcast(c->host, h.data(), n, root);
+    if (!rc && c->rank != root) {
+        rc = (int)hipMemcpyAsync(b, h.data(), n, hipMemcpyHostToDevice, s->stream);
+        if (!rc) rc = (int)hipStreamSynchronize(s->stream);
+    }
+    return rc;
+}
+int s_sync(pcmx_comm_t* c) { return (int)hipStreamSynchronize(simpl(c)->stream); }
+void s_destroy(pcmx_comm_t* c) {
+    StagedImpl* s = simpl(c);
+    if (s) {
+        if (s->stream) hipStreamDestroy(s->stream);
+        delete s;
+    }
+    if (c->host && c->host != c) pcmx_comm_destroy(c->host);
+    free(c);
+}
+const pcmx_comm_ops_t kStagedOps = {s_group_start, s_group_end, s_send, s_recv, s_allreduce, s_bcast, s_sync, s_destroy};
 
 // ---------------------------------------------------------------- device backend
 struct DevCtx {
@@ -121,6 +262,33 @@ extern "C" int pcmx_region_backend_hip(pcmx_region_backend_t* be, void* stream) 
     be->alloc = d_alloc, be->release = d_release, be->memset0 = d_memset0, be->h2d = d_h2d, be->d2h = d_d2h;
     be->copy2d = d_copy2d, be->grow = d_grow, be->pack = d_pack, be->unpack = d_unpack, be->sync = d_sync;
     be->ctx = c;
+    return 0;
+}
+
+extern "C" int pcmx_comm_init_env_staged(pcmx_comm_t** out) {
+    *out = nullptr;
+    pcmx_comm_t* host = nullptr;
+    int rc = pcmx_comm_init_env_tcp(&host);
+    if (rc) {
+        pcmx_comm_destroy(host);
+        return rc;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || hipSetDevice(host->local_rank % ndev) != hipSuccess) {
+        pcmx_comm_destroy(host);
+        return -20;
+    }
+    StagedImpl* s = new StagedImpl;
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete s;
+        pcmx_comm_destroy(host);
+        return -22;
+    }
+    pcmx_comm_t* c = static_cast<pcmx_comm_t*>(calloc(1, sizeof(pcmx_comm_t)));
+    c->rank = host->rank, c->world = host->world, c->local_rank = host->local_rank % ndev;
+    c->transport = PCMX_TRANSPORT_TCP_STAGED;
+    c->ops = &kStagedOps, c->impl = s, c->host = host, c->stream = s->stream;
+    *out = c;
     return 0;
 }
 

@@ -5,6 +5,8 @@
  *                    point-to-point (ncclGroupStart/End) — stream-ordered on the communicator's HIP stream.
  *   transport TCP  : host buffers over loopback/LAN sockets (full mesh, poll-driven group progress) — the
  *                    GPU-less path used by the CPU tests, and the host side-channel/bootstrap of RCCL.
+ *   transport TCP_STAGED : device buffers staged through host memory over TCP, so several ranks can share
+ *                    one GPU (single-GPU test fixture for the multi-rank device path).
  *
  * Launch contract = torchrun's env: RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT (+ PCMX_PORT to
  * override the bootstrap port). `bin/pcmx_launch -n P prog ...` is the native mpirun equivalent.
@@ -17,7 +19,7 @@
 extern "C" {
 #endif
 
-enum { PCMX_TRANSPORT_TCP = 0, PCMX_TRANSPORT_RCCL = 1 };
+enum { PCMX_TRANSPORT_TCP = 0, PCMX_TRANSPORT_RCCL = 1, PCMX_TRANSPORT_TCP_STAGED = 2 };
 enum { PCMX_I32 = 0, PCMX_F32 = 1, PCMX_F64 = 2, PCMX_I64 = 3, PCMX_U8 = 4 };
 enum { PCMX_SUM = 0, PCMX_MIN = 1, PCMX_MAX = 2 };
 
@@ -48,6 +50,9 @@ struct pcmx_comm {
 int pcmx_comm_init_tcp(int rank, int world, const char* addr, int port, pcmx_comm_t** out);
 int pcmx_comm_init_env_tcp(pcmx_comm_t** out);
 int pcmx_comm_init_env_rccl(pcmx_comm_t** out); /* in libpcmx_hip: sets the device to LOCAL_RANK % count */
+/* in libpcmx_hip: device buffers staged through host memory over TCP — several ranks may share one GPU
+ * (single-GPU test fixture for the multi-rank device path; not a performance path) */
+int pcmx_comm_init_env_staged(pcmx_comm_t** out);
 void pcmx_comm_destroy(pcmx_comm_t* c);
 int pcmx_env_port(void);
 

@@ -104,3 +104,20 @@ def test_native_region_rccl_golden(gpu, tmp_path):
 def test_native_mpi_ring_rccl_single_rank(gpu):
     r = _launch(1, BIN / "mpi_ring")
     assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4])
+def test_native_region_multirank_one_gpu_staged(gpu, tmp_path, n):
+    """P ranks share the single GPU: gfx950 tile kernels + device pack/unpack + grouped exchange schedule,
+    with halos staged over TCP (RCCL refuses two ranks per device)."""
+    r = _launch(n, BIN / "region", "--staged", ASSETS / "pic1.bmp")
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(bmp.read(tmp_path / "out.bmp"), bmp.read(ASSETS / "region_pic1_golden.bmp"))
+
+
+@pytest.mark.gpu
+def test_native_mpi_ring_staged(gpu):
+    r = _launch(3, BIN / "mpi_ring", "--staged")
+    assert r.returncode == 0, r.stderr
+    assert "Rank 0 received 3 " in r.stdout.splitlines()
