@@ -31,6 +31,7 @@ class StencilSlab:
             raise ValueError("each rank needs at least 2 rows")
         self.u = init_grid(self.rows, self.cols, self.row0, n, device=ctx.device)
         self.v = self.u.clone()
+        self.steps_done = 0
         self.north = ctx.rank - 1 if ctx.rank > 0 else -1
         self.south = ctx.rank + 1 if ctx.rank < ctx.world - 1 else -1
 
@@ -59,6 +60,24 @@ class StencilSlab:
                 r.wait()
             stencil5_step_(self.u, self.v, self.row0, self.n, self.k)
         self.u, self.v = self.v, self.u
+        self.steps_done += 1
+
+    # ---- checkpoint / resume: each rank writes its own slab; tensors only (weights_only load)
+    def checkpoint(self, prefix: str) -> str:
+        path = f"{prefix}.rank{self.ctx.rank}-of-{self.ctx.world}.pt"
+        torch.save({"u": self.u.cpu(), "row0": self.row0, "rows": self.rows, "n": self.n, "cols": self.cols,
+                    "k": self.k, "steps_done": self.steps_done}, path)
+        self.ctx.barrier()
+        return path
+
+    def restore(self, prefix: str) -> None:
+        path = f"{prefix}.rank{self.ctx.rank}-of-{self.ctx.world}.pt"
+        st = torch.load(path, map_location="cpu", weights_only=True)
+        if (st["row0"], st["rows"], st["n"], st["cols"]) != (self.row0, self.rows, self.n, self.cols):
+            raise ValueError(f"checkpoint {path} does not match this decomposition")
+        self.u.copy_(st["u"].to(self.u.device))
+        self.v.copy_(self.u)
+        self.k, self.steps_done = st["k"], st["steps_done"]
 
     def run(self, steps: int, overlap: bool = True) -> torch.Tensor:
         for _ in range(steps):

@@ -178,6 +178,26 @@ def test_distributed_stencil_bit_exact(world, overlap):
     assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
 
 
+def _stencil_ckpt(ctx, q, prefix):
+    a = StencilSlab(ctx, 40, 24)
+    a.run(4)
+    a.checkpoint(prefix)
+    a.run(3)
+    b = StencilSlab(ctx, 40, 24)
+    b.restore(prefix)
+    b.run(3)
+    fa, fb = a.gather(), b.gather()
+    if ctx.is_root:
+        q.put((0, (fa.view(torch.int16).numpy(), fb.view(torch.int16).numpy(), b.steps_done)))
+
+
+def test_stencil_checkpoint_resume_world2(tmp_path):
+    res = _collect(2, _stencil_ckpt, str(tmp_path / "ck"))
+    fa, fb, steps = res[0]
+    assert steps == 7 and np.array_equal(fa, fb)
+    assert np.array_equal(fa, reference_run(40, 7, 24).view(torch.int16).numpy())
+
+
 def _spmv(ctx, q, n, nnz):
     d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1)
     x = torch.linspace(0, 1, n)
