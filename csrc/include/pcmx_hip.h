@@ -58,6 +58,7 @@ int pcmx_dot_f32(const float* a, const float* b, long long n, float* out, void* 
 
 /* ---------------------------------------------------------------- prefix scan */
 long long pcmx_scan_workspace_bytes(long long n);
+int pcmx_scan_set_rows(int rows); /* tile size knob: f32x4 rows per lane, 4 / 8 (default) / 16 */
 /* out[i] = init + sum_{j<=i} x[j] (inclusive) or init + sum_{j<i} x[j] (exclusive), single pass with
  * decoupled look-back; init is read from device memory (init_dev may be NULL => 0) so a multi-GPU
  * offset can be fed without a host round trip. In-place (out == x) is allowed. */

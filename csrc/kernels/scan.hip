@@ -19,9 +19,8 @@ namespace {
 using pcmx::kWave;
 constexpr int kWaves = 8;
 constexpr int kThreads = kWaves * kWave;
-constexpr int kRows = 4;                       // pcmx::f32x4 rows per lane
-constexpr int kWaveItems = kRows * 4 * kWave;  // 1024
-constexpr int kTile = kWaves * kWaveItems;     // 8192
+constexpr int kMinRows = 4;                          // smallest tile variant (sizes the workspace)
+constexpr int kMinTile = kWaves * kMinRows * 4 * kWave;  // 8192
 constexpr unsigned kFlagAgg = 1u, kFlagIncl = 2u;
 constexpr unsigned kSpinLimit = 1u << 26;
 
@@ -36,6 +35,9 @@ __device__ __forceinline__ unsigned long long pack(unsigned flag, float v) {
     return ((unsigned long long)flag << 32) | (unsigned long long)__float_as_uint(v);
 }
 
+// kRows pcmx::f32x4 rows per lane: tile = 8 waves x kRows x 256 elements. Larger tiles amortise the
+// look-back round trips (agent-scope polls cross the XCD L2s) over more bytes.
+template <int kRows>
 __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                                 long long n, int exclusive, const float* init_dev,
                                                                 ScanWs* ws) {
@@ -43,6 +45,8 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __
     __shared__ float s_wave_tot[kWaves];
     __shared__ float s_prefix;
     __shared__ unsigned s_tile;
+    constexpr int kWaveItems = kRows * 4 * kWave;
+    constexpr int kTile = kWaves * kWaveItems;
     const int lane = pcmx::lane_id();
     const int wave = threadIdx.x / kWave;
 
@@ -166,21 +170,39 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __
     }
 }
 
-inline long long num_tiles(long long n) { return (n + kTile - 1) / kTile; }
+inline long long num_tiles(long long n, int tile) { return (n + tile - 1) / tile; }
+int g_scan_rows = 8;
+template <int R>
+void launch_scan(const float* x, float* out, long long n, int exclusive, const float* init_dev, ScanWs* ws,
+                 hipStream_t s) {
+    constexpr int tile = kWaves * R * 4 * kWave;
+    scan_lookback_kernel<R><<<(unsigned)num_tiles(n, tile), kThreads, 0, s>>>(x, out, n, exclusive, init_dev, ws);
+}
 }  // namespace
 
+extern "C" int pcmx_scan_set_rows(int rows) {
+    if (rows != 4 && rows != 8 && rows != 16) return -1;
+    g_scan_rows = rows;
+    return 0;
+}
+
 extern "C" long long pcmx_scan_workspace_bytes(long long n) {
-    return (long long)sizeof(ScanWs) + num_tiles(n) * 8;
+    return (long long)sizeof(ScanWs) + num_tiles(n, kMinTile) * 8;
 }
 
 extern "C" int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
                              hipStream_t s) {
     if (n <= 0) return 0;
     if ((((uintptr_t)x) & 15u) || (((uintptr_t)out) & 15u) || !workspace) return -1;
-    const long long tiles = num_tiles(n);
+    const long long tiles = num_tiles(n, kMinTile);
     if (tiles > 0x7fffffffLL) return -1;
-    PCMX_HIP_RET(hipMemsetAsync(workspace, 0, (size_t)pcmx_scan_workspace_bytes(n), s));
-    scan_lookback_kernel<<<(unsigned)tiles, kThreads, 0, s>>>(x, out, n, exclusive, init_dev,
-                                                               reinterpret_cast<ScanWs*>(workspace));
+    // only the ticket/timeout header and the status words of the tiles actually launched need zeroing
+    const int rows = g_scan_rows;
+    const long long used = num_tiles(n, kWaves * rows * 4 * kWave);
+    PCMX_HIP_RET(hipMemsetAsync(workspace, 0, sizeof(ScanWs) + (size_t)used * 8, s));
+    ScanWs* ws = reinterpret_cast<ScanWs*>(workspace);
+    if (rows == 16) launch_scan<16>(x, out, n, exclusive, init_dev, ws, s);
+    else if (rows == 4) launch_scan<4>(x, out, n, exclusive, init_dev, ws, s);
+    else launch_scan<8>(x, out, n, exclusive, init_dev, ws, s);
     return (int)hipGetLastError();
 }

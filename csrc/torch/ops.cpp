@@ -416,4 +416,5 @@ PYBIND11_MODULE(_C, mod) {
     mod.def("device_count", []() { return pcmx_device_count(); });
     mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr");
     mod.def("sgemm_set_tuning", [](int order, int diag) { return pcmx_sgemm_set_tuning(order, diag); });
+    mod.def("scan_set_rows", [](int rows) { return pcmx_scan_set_rows(rows); }, "scan tile: f32x4 rows per lane (4/8/16)");
 }

@@ -66,7 +66,7 @@ CPU_SRCS = ["cpu/bmp.c", "cpu/matrix.c", "cpu/spmv.c", "cpu/histogram.c", "cpu/v
 CFLAGS = ["-O3", "-fPIC", "-std=gnu11", "-fopenmp", "-march=x86-64-v3", "-Wall", "-Wno-unknown-pragmas",
           f"-I{CSRC / 'include'}"]
 # files whose float rounding must match the reference build bit-for-bit
-NO_CONTRACT = {"cpu/oracles.c", "cpu/histogram.c"}
+NO_CONTRACT = {"cpu/oracles.c", "cpu/histogram.c", "cpu/spmv.c"}
 
 
 def build_cpu(force=False, jobs=8):

@@ -119,20 +119,24 @@ class Stencil(Workload):
     """16384^2 bf16 5-point stencil, row slabs + 2-row halo exchange overlapped with the interior update.
     Strong scaling across ranks when `global_n` is fixed (the grid is split); weak when `per_rank`."""
 
-    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, **_):
+    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, **_):
         from ..parallel.stencil import StencilSlab
 
         rows = n * (ctx.world if per_rank else 1)
-        super().__init__(ctx, {"n": n, "rows": rows}, "stencil", "GLUP/s")
+        super().__init__(ctx, {"n": n, "rows": rows, "graph_steps": graph_steps}, "stencil", "GLUP/s")
         self.slab = StencilSlab(ctx, rows, n)
         self.overlap = overlap
+        self.graph_steps = graph_steps  # >0: one step() = graph_steps updates replayed from a HIP graph
         self.cells_local = self.slab.rows * n
 
     def step(self):
-        self.slab.step(self.overlap)
+        if self.graph_steps:
+            self.slab.run(self.graph_steps, self.overlap, graph=True)
+        else:
+            self.slab.step(self.overlap)
 
     def work_per_step(self):
-        return float(self.cells_local)
+        return float(self.cells_local) * max(1, self.graph_steps)
 
 
 class SpMV(Workload):

@@ -89,6 +89,16 @@ def test_stencil_workload_matches_reference(gpu, ctx):
     assert torch.equal(w.slab.interior().cpu().view(torch.int16), ref.view(torch.int16))
 
 
+def test_stencil_hip_graph_replay_matches_eager(gpu, ctx):
+    from parallel_c_programs_amd.parallel import StencilSlab, reference_run
+
+    s = StencilSlab(ctx, 256, 512)
+    s.run(7, graph=True)  # capture-warm-up pair + 2 replays + 1 eager step
+    s.run(4, graph=True)  # the odd eager step swapped the buffers: re-capture, then replay
+    assert s.steps_done == 11
+    assert torch.equal(s.interior().cpu().view(torch.int16), reference_run(256, 11, 512).view(torch.int16))
+
+
 def test_spmv_workload_matches_host(gpu, ctx):
     w = build_workload("spmv", ctx, n_rows=200_000, nnz=2_000_000)
     w.step()
@@ -104,3 +114,36 @@ def test_region3d_raycast_workloads(gpu, ctx):
     rc = build_workload("raycast", ctx, dim=512, image_dim=256)
     rc.step()
     assert rc.image.shape == (256, 256)
+
+
+def test_matrix_multiply_dispatches_to_mfma_backend(gpu):
+    """matrix_t's matrix_multiply (ref 1-introduction/matrix.c:63-81) hands large products to the MFMA SGEMM
+    once libpcmx_hip registers itself as the GEMM backend; result checked against fp64."""
+    import ctypes
+
+    from parallel_c_programs_amd._native import cpu_lib, hip_lib
+
+    class Mat(ctypes.Structure):
+        _fields_ = [("data", ctypes.POINTER(ctypes.POINTER(ctypes.c_float))), ("rows", ctypes.c_int),
+                    ("cols", ctypes.c_int)]
+
+    lib, hip = cpu_lib(), hip_lib()
+    lib.new_matrix.restype = ctypes.POINTER(Mat)
+    lib.new_matrix.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.matrix_multiply.argtypes = [ctypes.POINTER(Mat), ctypes.POINTER(Mat), ctypes.POINTER(ctypes.POINTER(Mat))]
+    lib.free_matrix.argtypes = [ctypes.POINTER(Mat)]
+    hip.pcmx_register_gemm_backend.argtypes = [ctypes.c_longlong]
+    hip.pcmx_register_gemm_backend(0)
+    g = np.random.default_rng(3)
+    a_np = g.standard_normal((300, 200), dtype=np.float32)
+    b_np = g.standard_normal((200, 260), dtype=np.float32)
+    a, b = lib.new_matrix(300, 200), lib.new_matrix(200, 260)
+    ctypes.memmove(a.contents.data[0], a_np.ctypes.data, a_np.nbytes)
+    ctypes.memmove(b.contents.data[0], b_np.ctypes.data, b_np.nbytes)
+    c = ctypes.POINTER(Mat)()
+    assert lib.matrix_multiply(a, b, ctypes.byref(c)) == 0
+    out = np.ctypeslib.as_array(c.contents.data[0], shape=(300 * 260,)).reshape(300, 260).copy()
+    ref = a_np.astype(np.float64) @ b_np.astype(np.float64)
+    assert np.abs(out - ref).max() / np.abs(ref).max() < 1e-5
+    for m in (a, b, c):
+        lib.free_matrix(m)
