@@ -638,10 +638,16 @@ struct CfgRS {
     static constexpr int kStage = kAFloats + kBFloats;
     static constexpr int kAPW = BM / 8 / kWaves;   // A pieces (8 rows x 128 B) per wave: 8
     static constexpr int kBPW = BK / kWaves;       // B pieces (one 1-KiB k-row) per wave: 8
+    // padded-A layout (PADA): rows of BK+4 floats (144 B): 8 consecutive rows of a ds_read_b128 group hit
+    // disjoint 16-B bank slots (144r mod 256 = 0,144,32,176,...), so the k-chunk enters the address as a
+    // compile-time constant (ds_read offset field) instead of an XOR with a lane-dependent swizzle.
+    static constexpr int kAStridePad = BK + 4;
+    static constexpr int kAFloatsPad = BM * kAStridePad;
+    static constexpr int kStagePad = kAFloatsPad + kBFloats;
     static_assert(NT == 4, "interleaved-column B read assumes 4 N-tiles per wave");
 };
 
-template <bool BETA, int SCHED>
+template <bool BETA, int SCHED, bool PADA = false>
 __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const float* __restrict__ A,
                                                                      const float* __restrict__ B,
                                                                      float* __restrict__ Cmat, int M, int N, int K,
@@ -649,7 +655,10 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
                                                                      float beta) {
     using C = CfgRS;
     typedef __attribute__((address_space(3))) pcmx::f32x4 lds_f4;
-    __shared__ __attribute__((aligned(16))) float smem[2 * C::kStage];
+    constexpr int kSt = PADA ? C::kStagePad : C::kStage;      // floats per LDS stage
+    constexpr int kAF = PADA ? C::kAFloatsPad : C::kAFloats;  // floats of the A part of a stage
+    constexpr int kAS = PADA ? C::kAStridePad : C::BK;        // A row stride in LDS (floats)
+    __shared__ __attribute__((aligned(16))) float smem[2 * kSt];
     lds_float* lds = (lds_float*)smem;
     const int lane = pcmx::lane_id();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -670,9 +679,9 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
 #pragma unroll
     for (int i = 0; i < C::kAPW; ++i) {
         const int r = (wave * C::kAPW + i) * 8 + (lane >> 3);
-        lwA[i] = r * C::BK * 4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16);
+        lwA[i] = r * kAS * 4 + (PADA ? (lane & 7) * 16 : (((lane & 7) ^ ((r >> 1) & 7)) * 16));
     }
-    const int lwB = (C::kAFloats + wave * C::kBPW * C::BN) * 4 + lane * 16;
+    const int lwB = (kAF + wave * C::kBPW * C::BN) * 4 + lane * 16;
 
     pcmx::f32x4 R[C::kAPW + C::kBPW];
     auto gload = [&](int q, int k0) {  // piece q (0..7 A, 8..15 B) of the stage starting at k0
@@ -703,14 +712,19 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
 #pragma unroll
     for (int i = 0; i < C::MT; ++i) {
         const int r = wm * C::kWaveM + i * 32 + l32;
-        a_off[i] = r * C::BK;
+        a_off[i] = r * kAS + (PADA ? 4 * h : 0);
         a_swz[i] = (r >> 1) & 7;
     }
-    const int b_off = C::kAFloats + wn * C::kWaveN + 4 * l32;
+    const int b_off = kAF + wn * C::kWaveN + 4 * l32;
 
     auto read = [&](const lds_float* stage, int kc, pcmx::f32x4(&a)[C::MT], pcmx::f32x4(&b)[4]) {
 #pragma unroll
-        for (int i = 0; i < C::MT; ++i) a[i] = *(const lds_f4*)(stage + a_off[i] + (((2 * kc + h) ^ a_swz[i]) * 4));
+        for (int i = 0; i < C::MT; ++i) {
+            if constexpr (PADA)
+                a[i] = *(const lds_f4*)(stage + a_off[i] + 8 * kc);
+            else
+                a[i] = *(const lds_f4*)(stage + a_off[i] + (((2 * kc + h) ^ a_swz[i]) * 4));
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) b[s] = *(const lds_f4*)(stage + b_off + (kc * 8 + 4 * h + s) * C::BN);
     };
@@ -749,8 +763,8 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
     auto stage = [&](int t, auto write_c, auto load_c) {
         constexpr bool WRITE = decltype(write_c)::value;  // registers hold stage t+1
         constexpr bool LOAD = decltype(load_c)::value;    // stage t+2 exists
-        lds_float* cur = lds + (t & 1) * C::kStage;
-        lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
+        lds_float* cur = lds + (t & 1) * kSt;
+        lds_float* nxt = lds + ((t + 1) & 1) * kSt;
         const int k2 = (t + 2) * C::BK;
         // SCHED 0: pieces 0..15 after every 8 MFMAs of chunks 0-1 (pinned); 1: one piece per 16 MFMAs over
         // all 4 chunks (pinned); 2: as 0 without sched_barrier pinning.
@@ -799,7 +813,7 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
         }
 }
 
-template <int SCHED>
+template <int SCHED, bool PADA = false>
 int launch_rs(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
               float beta, hipStream_t s) {
     using C = CfgRS;
@@ -809,9 +823,9 @@ int launch_rs(const float* A, const float* B, float* Cm, int M, int N, int K, in
     if ((long long)C::BM * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31)) return -1;
     const int grid = (M / C::BM) * (N / C::BN);
     if (beta != 0.f)
-        sgemm_rs_kernel<true, SCHED><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_rs_kernel<true, SCHED, PADA><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     else
-        sgemm_rs_kernel<false, SCHED><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_rs_kernel<false, SCHED, PADA><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     return (int)hipGetLastError();
 }
 
@@ -1003,6 +1017,209 @@ int launch_rs16(const float* A, const float* B, float* Cm, int M, int N, int K, 
     return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Variant 13: v_mfma_f32_16x16x4_f32 with low register pressure (no spills, unlike variant 8).
+//  * Same tile / staging / LDS layouts as variant 8 (256x256x32, 4 waves 2x2, wave 128x128 = 8x8 tiles).
+//  * MFMA order is i-major (A tile i, then k-step s, then the 8 N tiles), so an A fragment is dead after
+//    its 32 MFMAs: A is read just in time into a 4-slot ring, two i-iterations (2 x 1024 cycles) ahead.
+//    B fragments (32 VGPRs per 16-k chunk) are double-buffered by chunk. Per wave: ~12 + 64 + 64 staging
+//    VGPRs instead of 2 x 64 fragment + 64 staging.
+//  * One barrier per stage, placed after the first 6 of the 8 i-iterations of chunk 1: every read of the
+//    current stage and every LDS write of the next stage (16 fillers, lwrite + global load two stages
+//    ahead) is issued before it, and the next stage's first fragments are read right after it while the
+//    last 2 x 32 MFMAs run.
+template <bool BETA>
+__global__ __launch_bounds__(CfgRS16::kThreads, 1) void sgemm_rs16i_kernel(const float* __restrict__ A,
+                                                                          const float* __restrict__ B,
+                                                                          float* __restrict__ Cmat, int M, int N,
+                                                                          int K, int lda, int ldb, int ldc,
+                                                                          float alpha, float beta) {
+    using C = CfgRS16;
+    typedef __attribute__((address_space(3))) pcmx::f32x4 lds_f4;
+    typedef __attribute__((address_space(3))) char lds_char;
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    constexpr int kAS = C::BK + 4;          // padded A row (144 B): conflict-free b128 reads, additive k
+    constexpr int kAF = C::BM * kAS;        // A floats per stage
+    constexpr int kSt = kAF + C::kBFloats;  // floats per stage
+    __shared__ __attribute__((aligned(16))) float smem[2 * kSt];
+    lds_float* lds = (lds_float*)smem;
+    const int lane = pcmx::lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int q = lane >> 4, l16 = lane & 15;
+    int m0, n0;
+    tile_coords<Cfg<256, 256, 2, 4>>(M, N, m0, n0);
+
+    const __amdgpu_buffer_rsrc_t rA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, C::BM * lda * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(B + n0), (short)0, K * ldb * 4, 0x00020000);
+    const int voA = ((lane >> 3) * lda + (lane & 7) * 4) * 4;
+    const int voB = lane * 16;
+    int lwA[C::kAPW];
+#pragma unroll
+    for (int i = 0; i < C::kAPW; ++i) {
+        const int r = (wave * C::kAPW + i) * 8 + (lane >> 3);
+        lwA[i] = r * kAS * 4 + (lane & 7) * 16;
+    }
+    int lwB[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) lwB[par] = (lane ^ par) * 16;
+
+    pcmx::f32x4 R[C::kAPW + C::kBPW];
+    auto gload = [&](int qq, int k0) __attribute__((always_inline)) {
+        if (qq < C::kAPW) {
+            const int so = ((wave * C::kAPW + qq) * 8 * lda + k0) * 4;
+            R[qq] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, voA, so, 0));
+        } else {
+            const int so = (k0 + wave * C::kBPW + (qq - C::kAPW)) * ldb * 4;
+            R[qq] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, voB, so, 0));
+        }
+    };
+    auto lwrite = [&](int qq, lds_float* stage) __attribute__((always_inline)) {
+        lds_char* base = (lds_char*)stage;
+        if (qq < C::kAPW) {
+            *(lds_f4*)(base + lwA[qq]) = R[qq];
+        } else {
+            const int kr = wave * C::kBPW + (qq - C::kAPW);
+            *(lds_f4*)(base + (kAF + kr * C::BN) * 4 + lwB[(kr >> 2) & 1]) = R[qq];
+        }
+    };
+
+    f32x4v acc[C::MT][C::NT];
+#pragma unroll
+    for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+        for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    // lane base of the A reads: row wm*128 + l16, k-chunk q; tile i and chunk c add compile-time offsets
+    const int a_lane = (wm * C::kWaveM + l16) * kAS + 4 * q;
+    const int b_row0 = kAF + 4 * q * C::BN;
+    const int b_ch0 = (2 * (wn * 16 + l16)) ^ (q & 1);
+    const int b_ch1 = (2 * (wn * 16 + l16) + 1) ^ (q & 1);
+    const int b_lane0 = b_row0 + b_ch0 * 4, b_lane1 = b_row0 + b_ch1 * 4;
+
+    f32x4v ring[4];            // A fragments, slot = (16*stage + 8*chunk + i) % 4
+    f32x4v bA[4][2], bB[4][2];  // B fragments of chunk 0 (bA) and chunk 1 (bB)
+    auto readA = [&](const lds_float* stage, int c, int i, f32x4v& dst) __attribute__((always_inline)) {
+        dst = *(const lds_f4*)(stage + a_lane + i * 16 * kAS + 16 * c);
+    };
+    auto readB = [&](const lds_float* stage, int c, int s, f32x4v(&dst)[4][2]) __attribute__((always_inline)) {
+        dst[s][0] = *(const lds_f4*)(stage + b_lane0 + (16 * c + s) * C::BN);
+        dst[s][1] = *(const lds_f4*)(stage + b_lane1 + (16 * c + s) * C::BN);
+    };
+    auto pin = [](auto&& f) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        f();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mma_i = [&](int i, const f32x4v& a, const f32x4v(&b)[4][2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < C::NT; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][j >> 2][j & 3], acc[i][j], 0, 0, 0);
+    };
+
+    const int nk = K / C::BK;
+#pragma unroll
+    for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) gload(qq, 0);
+#pragma unroll
+    for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) lwrite(qq, lds);
+    if (nk > 1) {
+#pragma unroll
+        for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) gload(qq, C::BK);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) readB(lds, 0, s, bA);
+    readA(lds, 0, 0, ring[0]);
+    readA(lds, 0, 1, ring[1]);
+
+    auto stage = [&](int t, auto write_c, auto load_c) __attribute__((always_inline)) {
+        constexpr bool WRITE = decltype(write_c)::value;  // registers hold stage t+1 (and stage t+1 exists)
+        constexpr bool LOAD = decltype(load_c)::value;    // stage t+2 exists
+        lds_float* cur = lds + (t & 1) * kSt;
+        lds_float* nxt = lds + ((t + 1) & 1) * kSt;
+        const int k2 = (t + 2) * C::BK;
+        auto fill = [&](int qq) __attribute__((always_inline)) {
+            if constexpr (WRITE) {
+                pin([&] {
+                    lwrite(qq, nxt);
+                    if constexpr (LOAD) gload(qq, k2);
+                });
+            }
+        };
+        // ---- chunk 0: A ring slots 0..7 (mod 4); B chunk 1 prefetched into bB during i = 0..3
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            pin([&] {
+                if (i <= 5) readA(cur, 0, i + 2, ring[(i + 2) & 3]);
+                else readA(cur, 1, i - 6, ring[(i + 2) & 3]);
+                if (i <= 3) readB(cur, 1, i, bB);
+            });
+            mma_i(i, ring[i & 3], bA);
+            fill(i);
+        }
+        // ---- chunk 1
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i == 6) {
+                __syncthreads();  // all reads of `cur` issued, all fillers of `nxt` written
+                if constexpr (WRITE) {
+                    pin([&] {
+#pragma unroll
+                        for (int s = 0; s < 4; ++s) readB(nxt, 0, s, bA);
+                        readA(nxt, 0, 0, ring[0]);
+                        readA(nxt, 0, 1, ring[1]);
+                    });
+                }
+            }
+            if (i <= 5) pin([&] { readA(cur, 1, i + 2, ring[(i + 2) & 3]); });
+            mma_i(i, ring[i & 3], bB);
+            if (i < 2) {
+                fill(8 + 2 * i);
+                fill(9 + 2 * i);
+            } else if (i < 6) {
+                fill(10 + i);
+            }
+        }
+    };
+    int t = 0;
+    for (; t + 2 < nk; ++t) stage(t, std::true_type{}, std::true_type{});
+    if (t + 1 < nk) stage(t++, std::true_type{}, std::false_type{});
+    stage(t, std::false_type{}, std::false_type{});
+
+#pragma unroll
+    for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wm * C::kWaveM + i * 16 + 4 * q + r;
+            pcmx::f32x4* p = reinterpret_cast<pcmx::f32x4*>(Cmat + (size_t)row * ldc + n0 + wn * C::kWaveN + 8 * l16);
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                pcmx::f32x4 v{alpha * acc[i][4 * g][r], alpha * acc[i][4 * g + 1][r], alpha * acc[i][4 * g + 2][r],
+                              alpha * acc[i][4 * g + 3][r]};
+                if constexpr (BETA) v += beta * p[g];
+                p[g] = v;
+            }
+        }
+}
+
+int launch_rs16i(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc,
+                 float alpha, float beta, hipStream_t s) {
+    using C = CfgRS16;
+    if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
+    if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return -1;
+    if ((long long)C::BM * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31)) return -1;
+    const int grid = (M / C::BM) * (N / C::BN);
+    if (beta != 0.f)
+        sgemm_rs16i_kernel<true><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+    else
+        sgemm_rs16i_kernel<false><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+    return (int)hipGetLastError();
+}
+
 using Big = Cfg<256, 256, 2, 4>;
 using Small = Cfg<128, 128, 2, 2>;
 
@@ -1031,7 +1248,10 @@ extern "C" int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, 
         case 5: return launch1w<false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 7: return launch_rs<0>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 10: return launch_rs<2>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 11: return launch_rs<0, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 12: return launch_rs<1, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 8: return launch_rs16(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 13: return launch_rs16i(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         default: return -1;
     }
 }
