@@ -58,7 +58,7 @@ int pcmx_dot_f32(const float* a, const float* b, long long n, float* out, void* 
 
 /* ---------------------------------------------------------------- prefix scan */
 long long pcmx_scan_workspace_bytes(long long n);
-int pcmx_scan_set_rows(int rows); /* tile size knob: f32x4 rows per lane, 4 / 8 (default) / 16 */
+int pcmx_scan_set_rows(int rows); /* tile shape knob: f32x4 rows per lane, 16 (8 waves, default) or 8 (16 waves) */
 /* out[i] = init + sum_{j<=i} x[j] (inclusive) or init + sum_{j<i} x[j] (exclusive), single pass with
  * decoupled look-back; init is read from device memory (init_dev may be NULL => 0) so a multi-GPU
  * offset can be fed without a host round trip. In-place (out == x) is allowed. */
@@ -108,6 +108,10 @@ int pcmx_raycast_bricked(const unsigned long long* tex, int dim, unsigned char* 
 /* ---------------------------------------------------------------- stencil */
 int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, int ld, int r0, int r1, long long global_row0,
                        long long global_rows, float k, hipStream_t s);
+/* TWO fused updates (temporal blocking, bit-identical to two single steps) over local rows [r0, r1) of a
+ * (rows + 2*halo) x ld slab; cols % 512 == 0; rows within 2 of a non-global slab edge need halo >= 2. */
+int pcmx_stencil5x2_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int r0, int r1,
+                         long long global_row0, long long global_rows, float k, hipStream_t s);
 
 /* ---------------------------------------------------------------- SpMV */
 long long pcmx_spmv_csr_plan(const long long* row_ptr_host, int n_rows, void* items_host, long long max_items);

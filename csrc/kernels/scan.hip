@@ -2,27 +2,29 @@
 // "prefix-scan 1e9 f32" kernel. Reference ancestor: the histogram CDF (ref 4-histogram-equalization-
 // openmp-pthreads/histogram_serial.c:29-34) generalised to 1e9 elements.
 //
-// MI355X design
-//  * Tile = 8 waves x 1024 elements (16 per lane = 4 x pcmx::f32x4, each wave instruction a contiguous 1 KiB),
-//    so HBM traffic is one read + one write of the array (8 B/element).
-//  * Tiles are taken in launch order from an atomic ticket, so every predecessor tile is already running
-//    and the look-back cannot deadlock whatever the dispatcher does.
-//  * Inter-workgroup hand-off uses 8-byte {flag, value} granules written with ONE agent-scope relaxed
-//    atomic store (write-through) and polled with agent-scope relaxed loads: the data IS the flag, so no
-//    fence is needed (cdna_hip_programming.md G16 recipe R2). One wave looks back 64 tiles per poll.
-//  * Status words and the ticket are zeroed by a hipMemsetAsync on the same stream before every launch
-//    (G16 "Re-initialise every call"); spins are bounded and report through a timeout flag.
+// MI355X design (measured in scripts/scan_lab.hip; 1e9 f32 on one MI355X):
+//  * HBM traffic is one read + one write of the array (8 B/element); the roofline is a tiled copy
+//    (~1.28 ms = 6.2 TB/s for 128-KiB tiles; 64-KiB tiles stream markedly worse on this part).
+//  * Tile = 128 KiB: 8 waves x 16 f32x4 rows per lane (or 16 waves x 8 rows), in-register wave scans.
+//  * PERSISTENT + SOFTWARE-PIPELINED: one 512-thread block per CU walks tiles in ticket order and keeps
+//    the NEXT tile's loads in flight (second register buffer) while the current tile's look-back polls its
+//    predecessors, so the look-back latency (agent-scope polls cross the 8 XCD L2s) hides behind HBM
+//    traffic. A one-tile-per-block grid pays that latency in the open: 1.9 ms -> 1.55 ms here.
+//  * Tiles come from an atomic ticket, so a tile is only ever owned by a RUNNING block and every predecessor
+//    of the oldest unfinished tile has published: the look-back cannot deadlock whatever the dispatcher does.
+//  * Hand-off = 8-byte {flag, value} granules written with ONE agent-scope relaxed atomic store and polled
+//    with agent-scope relaxed loads (cdna_hip_programming.md G16 recipe R2); one wave looks back 64 tiles per
+//    poll (wider per-lane windows measured slower). Status words and the ticket are zeroed by a
+//    hipMemsetAsync on the same stream before every launch; spins are bounded and report a timeout flag.
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 
 namespace {
+using pcmx::f32x4;
 using pcmx::kWave;
-constexpr int kWaves = 8;
-constexpr int kThreads = kWaves * kWave;
-constexpr int kMinRows = 4;                          // smallest tile variant (sizes the workspace)
-constexpr int kMinTile = kWaves * kMinRows * 4 * kWave;  // 8192
 constexpr unsigned kFlagAgg = 1u, kFlagIncl = 2u;
 constexpr unsigned kSpinLimit = 1u << 26;
+constexpr int kTileElems = 32768;  // 128 KiB of f32 for every variant
 
 struct ScanWs {
     unsigned ticket;
@@ -35,45 +37,49 @@ __device__ __forceinline__ unsigned long long pack(unsigned flag, float v) {
     return ((unsigned long long)flag << 32) | (unsigned long long)__float_as_uint(v);
 }
 
-// kRows pcmx::f32x4 rows per lane: tile = 8 waves x kRows x 256 elements. Larger tiles amortise the
-// look-back round trips (agent-scope polls cross the XCD L2s) over more bytes.
-template <int kRows>
-__global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                                long long n, int exclusive, const float* init_dev,
-                                                                ScanWs* ws) {
-    unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
-    __shared__ float s_wave_tot[kWaves];
-    __shared__ float s_prefix;
-    __shared__ unsigned s_tile;
-    constexpr int kWaveItems = kRows * 4 * kWave;
-    constexpr int kTile = kWaves * kWaveItems;
-    const int lane = pcmx::lane_id();
-    const int wave = threadIdx.x / kWave;
+// W waves x R f32x4 rows per lane; wave w owns the contiguous R*256 elements starting at w*R*256.
+template <int R, int W>
+struct Tile {
+    static constexpr int kWaveItems = R * 4 * kWave, kElems = W * kWaveItems;
+    static_assert(kElems == kTileElems, "all variants use 128-KiB tiles");
+};
 
-    if (threadIdx.x == 0) s_tile = atomicAdd(&ws->ticket, 1u);
-    __syncthreads();
-    const long long tile = s_tile;
-    const long long base = tile * kTile + (long long)wave * kWaveItems;
-
-    // ---- load 4 rows of pcmx::f32x4 (row r covers elements base + r*256 + lane*4 .. +3)
-    pcmx::f32x4 v[kRows];
+template <int R, int W>
+__device__ __forceinline__ void load_tile(const float* __restrict__ in, long long n, long long tile, f32x4 (&v)[R]) {
+    const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
+    const long long base = tile * Tile<R, W>::kElems + (long long)wave * Tile<R, W>::kWaveItems;
+    if ((tile + 1) * Tile<R, W>::kElems <= n) {  // block-uniform: full tiles take the branch-free path
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
+        for (int r = 0; r < R; ++r)
+            v[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in + base + r * 256 + lane * 4));
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
         const long long e = base + r * 256 + lane * 4;
         if (e + 3 < n) {
-            v[r] = __builtin_nontemporal_load(reinterpret_cast<const pcmx::f32x4*>(in + e));
+            v[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in + e));
         } else {
             v[r].x = e < n ? in[e] : 0.f;
             v[r].y = e + 1 < n ? in[e + 1] : 0.f;
             v[r].z = e + 2 < n ? in[e + 2] : 0.f;
-            v[r].w = e + 3 < n ? in[e + 3] : 0.f;
+            v[r].w = 0.f;
         }
     }
+}
+
+// Scans tile `tile` held in v, publishes it, issues the loads of `next` into vn, looks back, stores.
+template <int R, int W>
+__device__ __forceinline__ void finish_tile(const float* __restrict__ in, float* __restrict__ out, long long n, long long tile,
+                                            f32x4 (&v)[R], long long next, f32x4 (&vn)[R], long long ntiles, int exclusive,
+                                            float init, ScanWs* ws, float* s_wave_tot, float* s_prefix) {
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
+    const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
     // ---- in-wave scan: per row, lane-local prefix, then a wave scan of the lane totals
     float carry = 0.f;
-    float lane_excl[kRows];
+    float lane_excl[R];
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
+    for (int r = 0; r < R; ++r) {
         v[r].y += v[r].x;
         v[r].z += v[r].y;
         v[r].w += v[r].z;
@@ -85,23 +91,30 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __
     }
     if (lane == 0) s_wave_tot[wave] = carry;
     __syncthreads();
-
-    // ---- wave 0: tile aggregate, publish, decoupled look-back
-    if (wave == 0) {
-        float agg = 0.f;
+    float agg = 0.f, wexcl = 0.f;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) agg += s_wave_tot[w];
+    for (int w = 0; w < W; ++w) {
+        const float t = s_wave_tot[w];
+        wexcl += w < wave ? t : 0.f;
+        agg += t;
+    }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&status[tile], pack(tile == 0 ? kFlagIncl : kFlagAgg, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    // ---- the next tile's loads go out now and overlap the look-back below
+    if (next < ntiles) load_tile<R, W>(in, n, next, vn);
+
+    // ---- wave 0: decoupled look-back over the predecessors' {flag, value} granules
+    if (wave == 0) {
         float prefix = 0.f;
-        if (tile == 0) {
-            if (lane == 0) __hip_atomic_store(&status[0], pack(kFlagIncl, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(&status[tile], pack(kFlagAgg, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tile != 0) {
             long long look = tile - 1;  // newest predecessor still to account for
             unsigned spins = 0;
             while (true) {
                 const long long idx = look - lane;
-                unsigned long long sv = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                 : pack(kFlagIncl, 0.f);
+                const unsigned long long sv =
+                    idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : pack(kFlagIncl, 0.f);
                 const unsigned flag = (unsigned)(sv >> 32);
                 const float val = __uint_as_float((unsigned)sv);
                 const unsigned long long m_incl = __ballot(flag == kFlagIncl);
@@ -110,8 +123,7 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __
                     const int first = __builtin_ctzll(m_incl);
                     const unsigned long long need = (first == 63) ? ~0ull : ((1ull << (first + 1)) - 1ull);
                     if ((m_zero & need) == 0ull) {
-                        float contrib = lane <= first ? val : 0.f;
-                        prefix += pcmx::wave_reduce<float, 0>(contrib);
+                        prefix += pcmx::wave_reduce<float, 0>(lane <= first ? val : 0.f);
                         break;
                     }
                 } else if (m_zero == 0ull) {
@@ -126,42 +138,32 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __
                 __builtin_amdgcn_s_sleep(1);
             }
             if (lane == 0)
-                __hip_atomic_store(&status[tile], pack(kFlagIncl, prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&status[tile], pack(kFlagIncl, prefix + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (lane == 0) {
-            float init = init_dev ? *init_dev : 0.f;
-            float wo = 0.f;
-            for (int w = 0; w < kWaves; ++w) {
-                float t = s_wave_tot[w];
-                s_wave_tot[w] = wo;  // becomes the exclusive wave offset
-                wo += t;
-            }
-            s_prefix = init + prefix;
-        }
+        if (lane == 0) *s_prefix = init + prefix;
     }
     __syncthreads();
-    const float off = s_prefix + s_wave_tot[wave];
+    const float off = *s_prefix + wexcl;
 
     // ---- write (inclusive or exclusive) results
+    const long long base = tile * Tile<R, W>::kElems + (long long)wave * Tile<R, W>::kWaveItems;
+    const bool full = (tile + 1) * Tile<R, W>::kElems <= n;  // block-uniform
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
+    for (int r = 0; r < R; ++r) {
         const float b = off + lane_excl[r];
-        pcmx::f32x4 o;
+        f32x4 o;
         if (exclusive) {
-            const pcmx::f32x4 x = v[r];
             o.x = b;
-            o.y = b + x.x;
-            o.z = b + x.y;
-            o.w = b + x.z;
+            o.y = b + v[r].x;
+            o.z = b + v[r].y;
+            o.w = b + v[r].z;
         } else {
-            o.x = b + v[r].x;
-            o.y = b + v[r].y;
-            o.z = b + v[r].z;
-            o.w = b + v[r].w;
+            o = v[r] + b;
         }
         const long long e = base + r * 256 + lane * 4;
-        if (e + 3 < n) {
-            __builtin_nontemporal_store(o, reinterpret_cast<pcmx::f32x4*>(out + e));
+        if (full || e + 3 < n) {
+            __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + e));
         } else {
             if (e < n) out[e] = o.x;
             if (e + 1 < n) out[e + 1] = o.y;
@@ -170,39 +172,69 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const float* __
     }
 }
 
-inline long long num_tiles(long long n, int tile) { return (n + tile - 1) / tile; }
-int g_scan_rows = 8;
-template <int R>
-void launch_scan(const float* x, float* out, long long n, int exclusive, const float* init_dev, ScanWs* ws,
-                 hipStream_t s) {
-    constexpr int tile = kWaves * R * 4 * kWave;
-    scan_lookback_kernel<R><<<(unsigned)num_tiles(n, tile), kThreads, 0, s>>>(x, out, n, exclusive, init_dev, ws);
+template <int R, int W>
+__global__ __launch_bounds__(W * kWave) void scan_persistent_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                    long long n, long long ntiles, int exclusive,
+                                                                    const float* init_dev, ScanWs* ws) {
+    // two LDS slots so consecutive tiles never race on the broadcast values
+    __shared__ float s_wave_tot[2][W];
+    __shared__ float s_prefix[2];
+    __shared__ unsigned s_tile[2];
+    const float init = init_dev ? *init_dev : 0.f;
+    f32x4 va[R], vb[R];
+    if (threadIdx.x == 0) s_tile[0] = atomicAdd(&ws->ticket, 1u);
+    __syncthreads();
+    long long ta = s_tile[0];
+    if (ta >= ntiles) return;
+    load_tile<R, W>(in, n, ta, va);
+    // unrolled by two so both register buffers are statically named (every exit is block-uniform)
+    while (true) {
+        if (threadIdx.x == 0) s_tile[1] = atomicAdd(&ws->ticket, 1u);
+        __syncthreads();
+        const long long tb = s_tile[1];
+        finish_tile<R, W>(in, out, n, ta, va, tb, vb, ntiles, exclusive, init, ws, s_wave_tot[0], &s_prefix[0]);
+        if (tb >= ntiles) break;
+        if (threadIdx.x == 0) s_tile[0] = atomicAdd(&ws->ticket, 1u);
+        __syncthreads();
+        ta = s_tile[0];
+        finish_tile<R, W>(in, out, n, tb, vb, ta, va, ntiles, exclusive, init, ws, s_wave_tot[1], &s_prefix[1]);
+        if (ta >= ntiles) break;
+    }
+}
+
+inline long long num_tiles(long long n) { return (n + kTileElems - 1) / kTileElems; }
+int g_scan_rows = 16;
+
+int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+    return cus[dev] > 0 ? cus[dev] : 256;
 }
 }  // namespace
 
 extern "C" int pcmx_scan_set_rows(int rows) {
-    if (rows != 4 && rows != 8 && rows != 16) return -1;
+    if (rows != 8 && rows != 16) return -1;
     g_scan_rows = rows;
     return 0;
 }
 
-extern "C" long long pcmx_scan_workspace_bytes(long long n) {
-    return (long long)sizeof(ScanWs) + num_tiles(n, kMinTile) * 8;
-}
+extern "C" long long pcmx_scan_workspace_bytes(long long n) { return (long long)sizeof(ScanWs) + num_tiles(n) * 8; }
 
 extern "C" int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
                              hipStream_t s) {
     if (n <= 0) return 0;
     if ((((uintptr_t)x) & 15u) || (((uintptr_t)out) & 15u) || !workspace) return -1;
-    const long long tiles = num_tiles(n, kMinTile);
+    const long long tiles = num_tiles(n);
     if (tiles > 0x7fffffffLL) return -1;
-    // only the ticket/timeout header and the status words of the tiles actually launched need zeroing
-    const int rows = g_scan_rows;
-    const long long used = num_tiles(n, kWaves * rows * 4 * kWave);
-    PCMX_HIP_RET(hipMemsetAsync(workspace, 0, sizeof(ScanWs) + (size_t)used * 8, s));
+    PCMX_HIP_RET(hipMemsetAsync(workspace, 0, sizeof(ScanWs) + (size_t)tiles * 8, s));
     ScanWs* ws = reinterpret_cast<ScanWs*>(workspace);
-    if (rows == 16) launch_scan<16>(x, out, n, exclusive, init_dev, ws, s);
-    else if (rows == 4) launch_scan<4>(x, out, n, exclusive, init_dev, ws, s);
-    else launch_scan<8>(x, out, n, exclusive, init_dev, ws, s);
+    const unsigned grid = (unsigned)(tiles < device_cus() ? tiles : device_cus());  // one resident block per CU
+    if (g_scan_rows == 8)
+        scan_persistent_kernel<8, 16><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws);
+    else
+        scan_persistent_kernel<16, 8><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws);
     return (int)hipGetLastError();
 }

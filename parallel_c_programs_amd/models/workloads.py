@@ -102,7 +102,9 @@ class Scan(Workload):
         self.y = global_scan(self.x, self.ctx)
 
     def work_per_step(self):
-        return 12.0 * self.x.numel()  # reduce pass (4 B) + scan read (4 B) + write (4 B)
+        # effective bandwidth: the 8 B/element a scan must move (read + write); with several ranks the extra
+        # 4 B/element reduce pass that seeds each rank's offset counts as time, not as work
+        return 8.0 * self.x.numel()
 
     def check(self):
         n = min(self.x.numel(), 1 << 20)
@@ -116,15 +118,17 @@ class Scan(Workload):
 
 
 class Stencil(Workload):
-    """16384^2 bf16 5-point stencil, row slabs + 2-row halo exchange overlapped with the interior update.
-    Strong scaling across ranks when `global_n` is fixed (the grid is split); weak when `per_rank`."""
+    """16384^2 bf16 5-point stencil, row slabs + halo exchange overlapped with the interior update.
+    Strong scaling across ranks when `global_n` is fixed (the grid is split); weak when `per_rank`.
+    fuse=2 (default): two time steps per kernel (temporal blocking, bit-identical to single steps) and a
+    2-row halo exchange every two steps; one step() then advances two time steps and counts 2 updates/cell."""
 
-    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, **_):
+    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, fuse=2, **_):
         from ..parallel.stencil import StencilSlab
 
         rows = n * (ctx.world if per_rank else 1)
-        super().__init__(ctx, {"n": n, "rows": rows, "graph_steps": graph_steps}, "stencil", "GLUP/s")
-        self.slab = StencilSlab(ctx, rows, n)
+        super().__init__(ctx, {"n": n, "rows": rows, "graph_steps": graph_steps, "fuse": fuse}, "stencil", "GLUP/s")
+        self.slab = StencilSlab(ctx, rows, n, fuse=fuse)
         self.overlap = overlap
         self.graph_steps = graph_steps  # >0: one step() = graph_steps updates replayed from a HIP graph
         self.cells_local = self.slab.rows * n
@@ -136,7 +140,7 @@ class Stencil(Workload):
             self.slab.step(self.overlap)
 
     def work_per_step(self):
-        return float(self.cells_local) * max(1, self.graph_steps)
+        return float(self.cells_local) * (self.graph_steps or self.slab.fuse)
 
 
 class SpMV(Workload):

@@ -49,6 +49,29 @@ def stencil5_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, glo
     return out
 
 
+def stencil5x2_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, global_rows: int | None = None,
+                     k: float = DEFAULT_K, halo: int = 1, row_range: tuple[int, int] | None = None) -> torch.Tensor:
+    """TWO fused updates u -> out (temporal blocking: one HBM read + write per cell per two steps), bit-identical
+    to two stencil5_step_ calls. Slabs are (rows + 2*halo, cols); rows within 2 of a rank boundary need halo 2
+    (the halo rows must hold the neighbour's two boundary rows); GPU path needs cols % 512 == 0."""
+    rows = u.shape[0] - 2 * halo
+    global_rows = rows if global_rows is None else global_rows
+    r0, r1 = row_range or (0, rows)
+    if u.is_cuda:
+        ops().stencil5x2_(u, out, int(halo), int(r0), int(r1), int(global_row0), int(global_rows), float(k))
+        return out
+    # CPU oracle: two plain steps. With halo 2 the first step also updates local rows -1 and rows (from the
+    # second halo row), which the second step reads as its halo; with halo 1 only global edges are allowed
+    # and the (unused) halo rows simply keep their values.
+    if halo >= 2:
+        s1 = stencil5_reference(u[halo - 2:rows + halo + 2], global_row0 - 1, global_rows, k)[1:-1]
+    else:
+        s1 = stencil5_reference(u, global_row0, global_rows, k)
+    s2 = stencil5_reference(s1, global_row0, global_rows, k)
+    out[halo + r0:halo + r1] = s2[1 + r0:1 + r1]
+    return out
+
+
 def init_grid(rows: int, cols: int, global_row0: int = 0, global_rows: int | None = None, device="cpu",
               halo: int = 1) -> torch.Tensor:
     """Deterministic initial condition: hot top boundary row (1.0), a hot square in the middle, 0 elsewhere."""

@@ -7,15 +7,19 @@ columns) instead of four strided edges for a 2-D grid — fewer, larger, contigu
 own point-to-point link.
 
 Overlap: the halo exchange is posted as one grouped RCCL send/recv (RCCL runs it on its own stream);
-the interior rows, which do not read the halo, are computed on the compute stream meanwhile; only the two
+the interior rows, which do not read the halo, are computed on the compute stream meanwhile; only the
 boundary rows wait for the halo.
+
+Temporal blocking (fuse=2): the slab keeps TWO halo rows per side, one grouped exchange moves 2 rows per
+neighbour every two updates (half the messages — the halos are latency-bound on xGMI), and one fused kernel
+performs both updates with a single HBM read + write per cell. Results are bit-identical to fuse=1.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from ..ops.stencil import DEFAULT_K, init_grid, stencil5_step_
+from ..ops.stencil import DEFAULT_K, init_grid, stencil5_step_, stencil5x2_step_
 from .dist import Context
 from .topology import split
 
@@ -23,49 +27,61 @@ from .topology import split
 class StencilSlab:
     """One rank's (rows + 2, cols) bf16 slab and its double buffer."""
 
-    def __init__(self, ctx: Context, n: int, cols: int | None = None, k: float = DEFAULT_K):
+    def __init__(self, ctx: Context, n: int, cols: int | None = None, k: float = DEFAULT_K, fuse: int = 1):
         self.ctx, self.n, self.cols, self.k = ctx, n, (n if cols is None else cols), k
+        if fuse not in (1, 2):
+            raise ValueError("fuse: 1 or 2 updates per kernel")
+        self.fuse, self.halo = fuse, fuse  # two fused updates read two rows beyond the slab
         self.row0, row1 = split(n, ctx.world, ctx.rank)
         self.rows = row1 - self.row0
-        if self.rows < 2:
-            raise ValueError("each rank needs at least 2 rows")
-        self.u = init_grid(self.rows, self.cols, self.row0, n, device=ctx.device)
+        if self.rows < 2 * self.halo:
+            raise ValueError(f"each rank needs at least {2 * self.halo} rows")
+        self.u = init_grid(self.rows, self.cols, self.row0, n, device=ctx.device, halo=self.halo)
         self.v = self.u.clone()
         self.steps_done = 0
         self.north = ctx.rank - 1 if ctx.rank > 0 else -1
         self.south = ctx.rank + 1 if ctx.rank < ctx.world - 1 else -1
 
     def _post_exchange(self):
-        u, ops = self.u, []
+        """One grouped send/recv of `halo` contiguous boundary rows per neighbour."""
+        u, h, rows, ops = self.u, self.halo, self.rows, []
         if self.north >= 0:
-            ops += [dist.P2POp(dist.isend, u[1], self.north), dist.P2POp(dist.irecv, u[0], self.north)]
+            ops += [dist.P2POp(dist.isend, u[h:2 * h], self.north), dist.P2POp(dist.irecv, u[0:h], self.north)]
         if self.south >= 0:
-            ops += [dist.P2POp(dist.isend, u[self.rows], self.south),
-                    dist.P2POp(dist.irecv, u[self.rows + 1], self.south)]
+            ops += [dist.P2POp(dist.isend, u[rows:rows + h], self.south),
+                    dist.P2POp(dist.irecv, u[rows + h:rows + 2 * h], self.south)]
         return dist.batch_isend_irecv(ops) if ops else []
 
+    def _update(self, u, v, row_range=None):
+        """`fuse` updates u -> v over local rows row_range (default all)."""
+        if self.fuse == 2:
+            stencil5x2_step_(u, v, self.row0, self.n, self.k, halo=2, row_range=row_range)
+        else:
+            stencil5_step_(u, v, self.row0, self.n, self.k, row_range=row_range)
+
     def step(self, overlap: bool = True) -> None:
-        ctx, rows = self.ctx, self.rows
+        """Advances `fuse` time steps (one halo exchange, one kernel launch per row range)."""
+        ctx, rows, d = self.ctx, self.rows, self.halo  # rows within d of a rank edge read the halo
         if not ctx.distributed:
-            stencil5_step_(self.u, self.v, self.row0, self.n, self.k)
-        elif overlap and rows > 2:
+            self._update(self.u, self.v)
+        elif overlap and rows > 2 * d:
             reqs = self._post_exchange()
-            stencil5_step_(self.u, self.v, self.row0, self.n, self.k, row_range=(1, rows - 1))
+            self._update(self.u, self.v, (d, rows - d))
             for r in reqs:
                 r.wait()
-            stencil5_step_(self.u, self.v, self.row0, self.n, self.k, row_range=(0, 1))
-            stencil5_step_(self.u, self.v, self.row0, self.n, self.k, row_range=(rows - 1, rows))
+            self._update(self.u, self.v, (0, d))
+            self._update(self.u, self.v, (rows - d, rows))
         else:
             for r in self._post_exchange():
                 r.wait()
-            stencil5_step_(self.u, self.v, self.row0, self.n, self.k)
+            self._update(self.u, self.v)
         self.u, self.v = self.v, self.u
-        self.steps_done += 1
+        self.steps_done += self.fuse
 
     # ---- checkpoint / resume (SURVEY §5.4): each rank writes its own slab; tensors only (weights_only load)
     def checkpoint(self, prefix: str) -> str:
         path = f"{prefix}.rank{self.ctx.rank}-of-{self.ctx.world}.pt"
-        torch.save({"u": self.u.cpu(), "row0": self.row0, "rows": self.rows, "n": self.n, "cols": self.cols,
+        torch.save({"u": self.interior().cpu(), "row0": self.row0, "rows": self.rows, "n": self.n, "cols": self.cols,
                     "k": self.k, "steps_done": self.steps_done}, path)
         self.ctx.barrier()
         return path
@@ -75,23 +91,26 @@ class StencilSlab:
         st = torch.load(path, map_location="cpu", weights_only=True)
         if (st["row0"], st["rows"], st["n"], st["cols"]) != (self.row0, self.rows, self.n, self.cols):
             raise ValueError(f"checkpoint {path} does not match this decomposition")
-        self.u.copy_(st["u"].to(self.u.device))
+        self.interior().copy_(st["u"].to(self.u.device))  # halos are refreshed by the next exchange
         self.v.copy_(self.u)
         self.k, self.steps_done = st["k"], st["steps_done"]
 
     def run(self, steps: int, overlap: bool = True, graph: bool = False) -> torch.Tensor:
-        """`steps` updates. graph=True (single GPU rank): a HIP graph of two updates (u->v->u) is captured
-        once and replayed, removing per-launch host overhead from the time-stepping loop."""
-        if graph and self.ctx.device.type == "cuda" and not self.ctx.distributed and steps >= 2:
+        """`steps` updates (a multiple of `fuse`). graph=True (single GPU rank): a HIP graph of two launches
+        (u->v->u, 2*fuse updates) is captured once and replayed, removing per-launch host overhead."""
+        f = self.fuse
+        if steps % f:
+            raise ValueError(f"steps must be a multiple of fuse={f}")
+        if graph and self.ctx.device.type == "cuda" and not self.ctx.distributed and steps >= 2 * f:
             fresh = getattr(self, "_g", None) is None or self._g_ptr != (self.u.data_ptr(), self.v.data_ptr())
             g = self._graph()
-            if fresh:  # building the graph ran one eager pair of updates
-                steps -= 2
-            for _ in range(steps // 2):
+            if fresh:  # building the graph ran one eager pair of launches
+                steps -= 2 * f
+            for _ in range(steps // (2 * f)):
                 g.replay()
-            self.steps_done += 2 * (steps // 2)
-            steps %= 2
-        for _ in range(steps):
+            self.steps_done += 2 * f * (steps // (2 * f))
+            steps %= 2 * f
+        for _ in range(steps // f):
             self.step(overlap)
         return self.u
 
@@ -100,19 +119,19 @@ class StencilSlab:
             stream = torch.cuda.Stream()
             stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(stream):  # warm-up outside capture (lazy init of the op)
-                stencil5_step_(self.u, self.v, self.row0, self.n, self.k)
-                stencil5_step_(self.v, self.u, self.row0, self.n, self.k)
+                self._update(self.u, self.v)
+                self._update(self.v, self.u)
             torch.cuda.current_stream().wait_stream(stream)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                stencil5_step_(self.u, self.v, self.row0, self.n, self.k)
-                stencil5_step_(self.v, self.u, self.row0, self.n, self.k)
+                self._update(self.u, self.v)
+                self._update(self.v, self.u)
             self._g, self._g_ptr = g, (self.u.data_ptr(), self.v.data_ptr())
-            self.steps_done += 2  # the warm-up pair advanced the state
+            self.steps_done += 2 * self.fuse  # the warm-up pair advanced the state
         return self._g
 
     def interior(self) -> torch.Tensor:
-        return self.u[1:-1]
+        return self.u[self.halo:self.halo + self.rows]
 
     def gather(self) -> torch.Tensor | None:
         """Full (n, cols) grid on root."""

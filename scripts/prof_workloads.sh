@@ -7,7 +7,7 @@ mkdir -p "$out"
 ws=${@:-"stencil spmv reduce scan sgemm region3d raycast histeq"}
 export TMPDIR=/tmp
 for w in $ws; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/$w" -o "$w" -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/$w" -o "$w" -- \
     python3 -m parallel_c_programs_amd.cli.run_workload "$w" --steps 10 --warmup 2 --no-check > "$out/$w.log" 2>&1 || exit $?
   tail -n 1 "$out/$w.log"
 done

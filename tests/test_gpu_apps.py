@@ -85,8 +85,17 @@ def test_stencil_workload_matches_reference(gpu, ctx):
     w = build_workload("stencil", ctx, n=512)
     for _ in range(5):
         w.step()
-    ref = reference_run(512, 5, device="cpu")
+    ref = reference_run(512, 5 * w.slab.fuse, device="cpu")
     assert torch.equal(w.slab.interior().cpu().view(torch.int16), ref.view(torch.int16))
+
+
+def test_stencil_fused_graph_replay(gpu, ctx):
+    from parallel_c_programs_amd.parallel import StencilSlab, reference_run
+
+    s = StencilSlab(ctx, 256, 1024, fuse=2)
+    s.run(10, graph=True)  # capture warm-up (4 updates) + 1 replay (4) + 1 eager fused step (2)
+    assert s.steps_done == 10
+    assert torch.equal(s.interior().cpu().view(torch.int16), reference_run(256, 10, 1024).view(torch.int16))
 
 
 def test_stencil_hip_graph_replay_matches_eager(gpu, ctx):

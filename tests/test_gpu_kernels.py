@@ -128,6 +128,37 @@ def test_stencil_row_range_split(gpu):
     assert torch.equal(full, part)
 
 
+@pytest.mark.parametrize("shape", [(256, 512), (1000, 1024), (515, 4096), (7, 512)])
+def test_stencil_fused_two_steps_bit_exact(gpu, shape):
+    """Temporal-blocking kernel == two single steps (bf16 bits), random data so every lane/edge path counts."""
+    rows, cols = shape
+    g = torch.Generator().manual_seed(rows)
+    u = (torch.rand(rows + 2, cols, generator=g) * 4 - 2).to(torch.bfloat16)
+    ref = ops.stencil5_reference(ops.stencil5_reference(u, 0, rows), 0, rows)
+    a = u.to(gpu)
+    b = a.clone()
+    ops.stencil5x2_step_(a, b, 0, rows, halo=1)
+    assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16))
+
+
+@pytest.mark.parametrize("global_row0,global_rows", [(0, 300), (40, 340), (40, 300)])
+def test_stencil_fused_halo2_slab_and_row_split(gpu, global_row0, global_rows):
+    """A rank's slab with 2 halo rows (neighbour rows present) and the interior/boundary split used for
+    overlap gives the same bits as the CPU oracle of two steps."""
+    rows, cols = 300 - global_row0 if global_rows == 300 else 300, 1024
+    g = torch.Generator().manual_seed(global_row0 + global_rows)
+    u = (torch.rand(rows + 4, cols, generator=g) * 4 - 2).to(torch.bfloat16)
+    ref = u.clone()
+    ops.stencil5x2_step_(u, ref, global_row0, global_rows, halo=2)  # CPU oracle
+    a = u.to(gpu)
+    full, part = a.clone(), a.clone()
+    ops.stencil5x2_step_(a, full, global_row0, global_rows, halo=2)
+    for rr in [(2, rows - 2), (0, 2), (rows - 2, rows)]:
+        ops.stencil5x2_step_(a, part, global_row0, global_rows, halo=2, row_range=rr)
+    assert torch.equal(full, part)
+    assert torch.equal(full.cpu()[2:-2].view(torch.int16), ref[2:-2].view(torch.int16))
+
+
 def test_spmv_banded_vs_host(gpu):
     m = ops.banded_csr(20000, 41, 20, 10, 20, 5)
     x = ops.create_vector(20000)

@@ -162,8 +162,8 @@ def test_distributed_region_equals_serial(world):
     assert stats["outer_steps"] >= 2  # the region crosses tile borders
 
 
-def _stencil(ctx, q, n, cols, steps, overlap):
-    slab = StencilSlab(ctx, n, cols)
+def _stencil(ctx, q, n, cols, steps, overlap, fuse=1):
+    slab = StencilSlab(ctx, n, cols, fuse=fuse)
     slab.run(steps, overlap)
     full = slab.gather()
     if ctx.is_root:
@@ -174,6 +174,15 @@ def _stencil(ctx, q, n, cols, steps, overlap):
 def test_distributed_stencil_bit_exact(world, overlap):
     n, cols, steps = 64, 48, 7
     res = _collect(world, _stencil, n, cols, steps, overlap)
+    ref = reference_run(n, steps, cols)
+    assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("world,overlap", [(1, True), (2, True), (3, False), (4, True)])
+def test_distributed_stencil_fused_two_steps_bit_exact(world, overlap):
+    """Temporal blocking: 2-row halos, one exchange per two updates, same bits as single steps."""
+    n, cols, steps = 64, 48, 8
+    res = _collect(world, _stencil, n, cols, steps, overlap, 2)
     ref = reference_run(n, steps, cols)
     assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
 
