@@ -108,8 +108,11 @@ int pcmx_raycast_bricked(const unsigned long long* tex, int dim, unsigned char* 
 /* ---------------------------------------------------------------- stencil */
 int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, int ld, int r0, int r1, long long global_row0,
                        long long global_rows, float k, hipStream_t s);
-/* TWO fused updates (temporal blocking, bit-identical to two single steps) over local rows [r0, r1) of a
- * (rows + 2*halo) x ld slab; cols % 512 == 0; rows within 2 of a non-global slab edge need halo >= 2. */
+/* `steps` (2, 3, 4, 6, 8) fused updates (temporal blocking, bit-identical to single steps) over local rows
+ * [r0, r1) of a (rows + 2*halo) x ld slab; cols % 8 == 0; rows within `steps` of a non-global slab edge need
+ * halo >= steps. pcmx_stencil5x2_bf16 = steps 2. */
+int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0, int r1,
+                         long long global_row0, long long global_rows, float k, hipStream_t s);
 int pcmx_stencil5x2_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int r0, int r1,
                          long long global_row0, long long global_rows, float k, hipStream_t s);
 

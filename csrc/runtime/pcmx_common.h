@@ -50,6 +50,16 @@ __device__ __forceinline__ T wave_reduce(T v) {
     return v;
 }
 
+// Whole-wave lane shifts on the DPP path (GFX9 wave_shr:1 / wave_shl:1): a VALU modifier, no LDS round trip
+// like __shfl_up/__shfl_down (ds_bpermute). wave_from_prev: lane l gets lane l-1's value; wave_from_next: lane
+// l gets lane l+1's value. The end lane (0 / 63) receives 0.
+__device__ __forceinline__ float wave_from_prev(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float wave_from_next(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+
 // Inclusive wave scan (Hillis-Steele over 64 lanes).
 __device__ __forceinline__ float wave_inclusive_scan(float v) {
     const int l = lane_id();

@@ -297,17 +297,17 @@ void stencil5_(const at::Tensor& u, at::Tensor out, int64_t r0, int64_t r1, int6
              "stencil5_");
 }
 
-void stencil5x2_(const at::Tensor& u, at::Tensor out, int64_t halo, int64_t r0, int64_t r1, int64_t global_row0,
-                 int64_t global_rows, double k) {
+void stencil5xT_(const at::Tensor& u, at::Tensor out, int64_t halo, int64_t steps, int64_t r0, int64_t r1,
+                 int64_t global_row0, int64_t global_rows, double k) {
     check_gpu(u, "u", at::kBFloat16), check_gpu(out, "out", at::kBFloat16);
     TORCH_CHECK(u.dim() == 2 && u.sizes() == out.sizes() && u.is_contiguous() && out.is_contiguous() && halo >= 1 &&
                     u.size(0) > 2 * halo,
-                "stencil5x2: slabs of shape (rows + 2*halo, cols)");
+                "stencil5xT: slabs of shape (rows + 2*halo, cols)");
     const at::DeviceGuard g(u.device());
     const int rows = (int)(u.size(0) - 2 * halo), cols = (int)u.size(1);
-    check_rc(pcmx_stencil5x2_bf16(u.data_ptr(), out.data_ptr(), rows, cols, cols, (int)halo, (int)r0, (int)r1, global_row0,
-                                  global_rows, (float)k, cur_stream(u)),
-             "stencil5x2_");
+    check_rc(pcmx_stencil5xT_bf16(u.data_ptr(), out.data_ptr(), rows, cols, cols, (int)halo, (int)steps, (int)r0, (int)r1,
+                                  global_row0, global_rows, (float)k, cur_stream(u)),
+             "stencil5xT_");
 }
 
 // ---------------------------------------------------------------- SpMV
@@ -391,7 +391,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
     m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps) -> Tensor");
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
-    m.def("stencil5x2_(Tensor u, Tensor(a!) out, int halo, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
+    m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
     m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x) -> Tensor");
     m.def("pack_edges(Tensor tile) -> Tensor");
@@ -419,7 +419,7 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("brick_pack", brick_pack);
     m.impl("raycast_bricked", raycast_bricked);
     m.impl("stencil5_", stencil5_);
-    m.impl("stencil5x2_", stencil5x2_);
+    m.impl("stencil5xT_", stencil5xT_);
     m.impl("spmv_csr", spmv_csr);
     m.impl("spmv_banded", spmv_banded);
     m.impl("pack_edges", pack_edges);

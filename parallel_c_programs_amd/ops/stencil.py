@@ -49,27 +49,37 @@ def stencil5_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, glo
     return out
 
 
-def stencil5x2_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, global_rows: int | None = None,
-                     k: float = DEFAULT_K, halo: int = 1, row_range: tuple[int, int] | None = None) -> torch.Tensor:
-    """TWO fused updates u -> out (temporal blocking: one HBM read + write per cell per two steps), bit-identical
-    to two stencil5_step_ calls. Slabs are (rows + 2*halo, cols); rows within 2 of a rank boundary need halo 2
-    (the halo rows must hold the neighbour's two boundary rows); GPU path needs cols % 512 == 0."""
+FUSED_STEPS = (2, 3, 4, 6, 8)
+
+
+def stencil5_fused_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, global_rows: int | None = None,
+                         k: float = DEFAULT_K, halo: int = 1, steps: int = 2,
+                         row_range: tuple[int, int] | None = None) -> torch.Tensor:
+    """`steps` fused updates u -> out (temporal blocking: one HBM read + write per cell per `steps` updates),
+    bit-identical to `steps` stencil5_step_ calls. Slabs are (rows + 2*halo, cols); rows within `steps` of a
+    rank boundary need halo >= steps (the halo rows must hold the neighbour's boundary rows)."""
     rows = u.shape[0] - 2 * halo
     global_rows = rows if global_rows is None else global_rows
     r0, r1 = row_range or (0, rows)
     if u.is_cuda:
-        ops().stencil5x2_(u, out, int(halo), int(r0), int(r1), int(global_row0), int(global_rows), float(k))
+        ops().stencil5xT_(u, out, int(halo), int(steps), int(r0), int(r1), int(global_row0), int(global_rows), float(k))
         return out
-    # CPU oracle: two plain steps. With halo 2 the first step also updates local rows -1 and rows (from the
-    # second halo row), which the second step reads as its halo; with halo 1 only global edges are allowed
-    # and the (unused) halo rows simply keep their values.
-    if halo >= 2:
-        s1 = stencil5_reference(u[halo - 2:rows + halo + 2], global_row0 - 1, global_rows, k)[1:-1]
-    else:
-        s1 = stencil5_reference(u, global_row0, global_rows, k)
-    s2 = stencil5_reference(s1, global_row0, global_rows, k)
-    out[halo + r0:halo + r1] = s2[1 + r0:1 + r1]
+    # CPU oracle: plain steps. A slab with h halo rows yields the next level on h-1 halo rows (its outermost
+    # rows go stale); once h == 1 only global edges are allowed and the (unused) halo rows keep their values.
+    cur, h = u, halo
+    for _ in range(steps):
+        nxt = stencil5_reference(cur, global_row0 - (h - 1), global_rows, k)
+        if h > 1:
+            cur, h = nxt[1:-1], h - 1
+        else:
+            cur = nxt
+    out[halo + r0:halo + r1] = cur[h + r0:h + r1]
     return out
+
+
+def stencil5x2_step_(u, out, global_row0=0, global_rows=None, k=DEFAULT_K, halo=1, row_range=None):
+    """Two fused updates (see stencil5_fused_step_)."""
+    return stencil5_fused_step_(u, out, global_row0, global_rows, k, halo, 2, row_range)
 
 
 def init_grid(rows: int, cols: int, global_row0: int = 0, global_rows: int | None = None, device="cpu",

@@ -10,16 +10,16 @@ Overlap: the halo exchange is posted as one grouped RCCL send/recv (RCCL runs it
 the interior rows, which do not read the halo, are computed on the compute stream meanwhile; only the
 boundary rows wait for the halo.
 
-Temporal blocking (fuse=2): the slab keeps TWO halo rows per side, one grouped exchange moves 2 rows per
-neighbour every two updates (half the messages — the halos are latency-bound on xGMI), and one fused kernel
-performs both updates with a single HBM read + write per cell. Results are bit-identical to fuse=1.
+Temporal blocking (fuse=T in 2, 3, 4, 6, 8): the slab keeps T halo rows per side, one grouped exchange moves
+T rows per neighbour every T updates (1/T of the messages — the halos are latency-bound on xGMI), and one
+fused kernel performs the T updates with a single HBM read + write per cell. Bit-identical to fuse=1.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from ..ops.stencil import DEFAULT_K, init_grid, stencil5_step_, stencil5x2_step_
+from ..ops.stencil import DEFAULT_K, FUSED_STEPS, init_grid, stencil5_fused_step_, stencil5_step_
 from .dist import Context
 from .topology import split
 
@@ -29,9 +29,9 @@ class StencilSlab:
 
     def __init__(self, ctx: Context, n: int, cols: int | None = None, k: float = DEFAULT_K, fuse: int = 1):
         self.ctx, self.n, self.cols, self.k = ctx, n, (n if cols is None else cols), k
-        if fuse not in (1, 2):
-            raise ValueError("fuse: 1 or 2 updates per kernel")
-        self.fuse, self.halo = fuse, fuse  # two fused updates read two rows beyond the slab
+        if fuse != 1 and fuse not in FUSED_STEPS:
+            raise ValueError(f"fuse: 1 or one of {FUSED_STEPS} updates per kernel")
+        self.fuse, self.halo = fuse, fuse  # T fused updates read T rows beyond the slab
         self.row0, row1 = split(n, ctx.world, ctx.rank)
         self.rows = row1 - self.row0
         if self.rows < 2 * self.halo:
@@ -54,8 +54,8 @@ class StencilSlab:
 
     def _update(self, u, v, row_range=None):
         """`fuse` updates u -> v over local rows row_range (default all)."""
-        if self.fuse == 2:
-            stencil5x2_step_(u, v, self.row0, self.n, self.k, halo=2, row_range=row_range)
+        if self.fuse > 1:
+            stencil5_fused_step_(u, v, self.row0, self.n, self.k, halo=self.halo, steps=self.fuse, row_range=row_range)
         else:
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=row_range)
 

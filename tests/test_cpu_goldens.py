@@ -136,3 +136,15 @@ def test_t7_vmul_demo():
     i = torch.arange(1024, dtype=torch.float32)
     r = ops.vmul(i + 1, 1.0 / (i + 1))
     assert torch.allclose(r, torch.ones(1024), atol=1e-6)
+
+
+def test_native_extension_loads_without_gpu():
+    """_C.so and libpcmx_hip.so resolve every symbol (a launcher lost in an edit fails here, on CPU)."""
+    import ctypes
+
+    from parallel_c_programs_amd._native import LIB_DIR, ops
+
+    ctypes.CDLL(str(LIB_DIR / "libpcmx_hip.so"), mode=ctypes.RTLD_GLOBAL)
+    o = ops()
+    for name in ("sgemm", "reduce", "scan_out", "stencil5_", "stencil5xT_", "spmv_csr", "region3d_grow_"):
+        assert hasattr(o, name), name

@@ -128,35 +128,40 @@ def test_stencil_row_range_split(gpu):
     assert torch.equal(full, part)
 
 
-@pytest.mark.parametrize("shape", [(256, 512), (1000, 1024), (515, 4096), (7, 512)])
-def test_stencil_fused_two_steps_bit_exact(gpu, shape):
-    """Temporal-blocking kernel == two single steps (bf16 bits), random data so every lane/edge path counts."""
+@pytest.mark.parametrize("steps", [2, 3, 4, 8])
+@pytest.mark.parametrize("shape", [(256, 512), (1000, 1000), (515, 4096), (9, 2000)])
+def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
+    """Temporal-blocking kernel == `steps` single steps (bf16 bits); random data so every lane/strip-overlap
+    path counts; column counts that are not multiples of the 496-column output strip."""
     rows, cols = shape
-    g = torch.Generator().manual_seed(rows)
+    g = torch.Generator().manual_seed(rows + steps)
     u = (torch.rand(rows + 2, cols, generator=g) * 4 - 2).to(torch.bfloat16)
-    ref = ops.stencil5_reference(ops.stencil5_reference(u, 0, rows), 0, rows)
+    ref = u
+    for _ in range(steps):
+        ref = ops.stencil5_reference(ref, 0, rows)
     a = u.to(gpu)
     b = a.clone()
-    ops.stencil5x2_step_(a, b, 0, rows, halo=1)
+    ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps)
     assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16))
 
 
+@pytest.mark.parametrize("steps", [2, 4])
 @pytest.mark.parametrize("global_row0,global_rows", [(0, 300), (40, 340), (40, 300)])
-def test_stencil_fused_halo2_slab_and_row_split(gpu, global_row0, global_rows):
-    """A rank's slab with 2 halo rows (neighbour rows present) and the interior/boundary split used for
-    overlap gives the same bits as the CPU oracle of two steps."""
+def test_stencil_fused_deep_halo_slab_and_row_split(gpu, global_row0, global_rows, steps):
+    """A rank's slab with `steps` halo rows (neighbour rows present) and the interior/boundary split used for
+    overlap gives the same bits as the CPU oracle."""
     rows, cols = 300 - global_row0 if global_rows == 300 else 300, 1024
     g = torch.Generator().manual_seed(global_row0 + global_rows)
-    u = (torch.rand(rows + 4, cols, generator=g) * 4 - 2).to(torch.bfloat16)
+    u = (torch.rand(rows + 2 * steps, cols, generator=g) * 4 - 2).to(torch.bfloat16)
     ref = u.clone()
-    ops.stencil5x2_step_(u, ref, global_row0, global_rows, halo=2)  # CPU oracle
+    ops.stencil5_fused_step_(u, ref, global_row0, global_rows, halo=steps, steps=steps)  # CPU oracle
     a = u.to(gpu)
     full, part = a.clone(), a.clone()
-    ops.stencil5x2_step_(a, full, global_row0, global_rows, halo=2)
-    for rr in [(2, rows - 2), (0, 2), (rows - 2, rows)]:
-        ops.stencil5x2_step_(a, part, global_row0, global_rows, halo=2, row_range=rr)
+    ops.stencil5_fused_step_(a, full, global_row0, global_rows, halo=steps, steps=steps)
+    for rr in [(steps, rows - steps), (0, steps), (rows - steps, rows)]:
+        ops.stencil5_fused_step_(a, part, global_row0, global_rows, halo=steps, steps=steps, row_range=rr)
     assert torch.equal(full, part)
-    assert torch.equal(full.cpu()[2:-2].view(torch.int16), ref[2:-2].view(torch.int16))
+    assert torch.equal(full.cpu()[steps:-steps].view(torch.int16), ref[steps:-steps].view(torch.int16))
 
 
 def test_spmv_banded_vs_host(gpu):

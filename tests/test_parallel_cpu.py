@@ -178,11 +178,12 @@ def test_distributed_stencil_bit_exact(world, overlap):
     assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
 
 
-@pytest.mark.parametrize("world,overlap", [(1, True), (2, True), (3, False), (4, True)])
-def test_distributed_stencil_fused_two_steps_bit_exact(world, overlap):
-    """Temporal blocking: 2-row halos, one exchange per two updates, same bits as single steps."""
-    n, cols, steps = 64, 48, 8
-    res = _collect(world, _stencil, n, cols, steps, overlap, 2)
+@pytest.mark.parametrize("world,overlap,fuse", [(1, True, 2), (2, True, 2), (3, False, 2), (4, True, 2), (2, True, 4),
+                                                (3, True, 3)])
+def test_distributed_stencil_fused_steps_bit_exact(world, overlap, fuse):
+    """Temporal blocking: `fuse`-row halos, one exchange per `fuse` updates, same bits as single steps."""
+    n, cols, steps = 64, 48, 12
+    res = _collect(world, _stencil, n, cols, steps, overlap, fuse)
     ref = reference_run(n, steps, cols)
     assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
 
