@@ -7,9 +7,9 @@
 //    iterates Gauss-Seidel sweeps until nothing changes inside the tile (`__syncthreads_or`), so one
 //    launch advances the front across a whole tile instead of one cell (the naive kernel of
 //    raycast.cu:534 needs one launch per BFS level).
-//  * Active-tile worklist: a tile only runs if it or a face neighbour changed in the previous launch
-//    (act_in -> act_out, double-buffered), so late launches touch only the frontier. Inactive
-//    workgroups exit before reading memory.
+//  * Active-tile worklist: a tile only runs if a face neighbour changed in the previous launch. 2-D:
+//    act_in -> act_out flags over the tile grid. 3-D (65k tiles at 512^3): a compacted device-built list
+//    walked by a persistent grid, so a launch costs the frontier, not a full-volume dispatch.
 //  * Halo cells are read-only inputs. That makes the same kernel the compute step of the distributed
 //    version: a rank's halo holds its neighbours' boundary after an RCCL exchange (parallel/region2d.py).
 //  * Region state is 0/1 (a cell never leaves the region), so races between tiles are benign and the
@@ -85,19 +85,31 @@ __global__ __launch_bounds__(kThreads2) void region2d_tile_kernel(const unsigned
 
 // ----------------------------------------------------------------------------------------------- 3-D
 // Tile interior 32(x) x 8(y) x 8(z); one thread per (x,y) column of the tile walks 8 z-slices.
+// Work is a COMPACTED tile list: launch e processes list[e%2] (count[e%3]) with a persistent grid and
+// appends the tiles to visit next (changed tiles and their face neighbours) to list[(e+1)%2], deduplicated
+// by stamping mark[tile] = e+1 with an atomic exchange. A 512^3 grow touches ~1-2k of the 65k tiles per
+// launch, so a launch costs what the frontier costs, not a full-volume dispatch. The first list holds the
+// tiles that contain any region voxel (one scan of the region). Counters rotate over 3 slots: launch e
+// zeroes slot (e+2)%3, the output slot of launch e+1, so no memset sits between launches.
 constexpr int kTX = 32, kTY = 8, kTZ = 8;
 constexpr int kThreads3 = kTX * kTY;
+constexpr int kListGrid = 2048;  // persistent grid of the list kernel (8 workgroups per CU)
 
-__global__ __launch_bounds__(kThreads3) void region3d_tile_kernel(const unsigned char* __restrict__ data,
-                                                                 unsigned char* __restrict__ region, int dim, int thr,
-                                                                 const int* __restrict__ act_in,
-                                                                 int* __restrict__ act_out, int* __restrict__ flag) {
-    const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    const int nbx = gridDim.x, nby = gridDim.y, nbz = gridDim.z;
-    const long long tid = ((long long)bz * nby + by) * nbx + bx;
-    if (act_in && act_in[tid] == 0) return;
-    __shared__ unsigned char sd[kTZ + 2][kTY + 2][kTX + 2];
-    __shared__ unsigned char sr[kTZ + 2][kTY + 2][kTX + 2];
+struct Grow3dWs {
+    int flag;
+    int count[3];
+    // followed by: int mark[ntiles]; int list[2][ntiles]
+};
+
+__device__ __forceinline__ void push_tile(int t, int stamp, int* __restrict__ mark, int* __restrict__ list,
+                                          int* __restrict__ count) {
+    if (atomicExch(&mark[t], stamp) != stamp) list[atomicAdd(count, 1)] = t;
+}
+
+// Grows one tile to its local fixpoint; returns (block-uniform) whether any voxel of the tile changed.
+__device__ bool grow_tile3d(const unsigned char* __restrict__ data, unsigned char* __restrict__ region, int dim, int thr,
+                            int bx, int by, int bz, unsigned char (*sd)[kTY + 2][kTX + 2],
+                            unsigned char (*sr)[kTY + 2][kTX + 2]) {
     const int x0 = bx * kTX - 1, y0 = by * kTY - 1, z0 = bz * kTZ - 1;
     const size_t plane = (size_t)dim * dim;
     constexpr int kE = (kTZ + 2) * (kTY + 2) * (kTX + 2);
@@ -140,15 +152,63 @@ __global__ __launch_bounds__(kThreads3) void region3d_tile_kernel(const unsigned
         for (int lz = 1; lz <= kTZ; ++lz)
             if (mine & (1u << lz)) region[(size_t)(z0 + lz) * plane + (size_t)(y0 + ly) * dim + x0 + lx] = 1;
     }
-    if (any_block && threadIdx.x == 0) {
-        *flag = 1;
-        act_out[tid] = 1;
-        if (bx > 0) act_out[tid - 1] = 1;
-        if (bx + 1 < nbx) act_out[tid + 1] = 1;
-        if (by > 0) act_out[tid - nbx] = 1;
-        if (by + 1 < nby) act_out[tid + nbx] = 1;
-        if (bz > 0) act_out[tid - (long long)nbx * nby] = 1;
-        if (bz + 1 < nbz) act_out[tid + (long long)nbx * nby] = 1;
+    return any_block;
+}
+
+__global__ __launch_bounds__(kThreads3) void region3d_list_kernel(const unsigned char* __restrict__ data,
+                                                                 unsigned char* __restrict__ region, int dim, int thr,
+                                                                 int nbx, int nby, int nbz, int epoch,
+                                                                 Grow3dWs* __restrict__ ws, int* __restrict__ mark,
+                                                                 int* __restrict__ lists, int ntiles) {
+    __shared__ unsigned char sd[kTZ + 2][kTY + 2][kTX + 2];
+    __shared__ unsigned char sr[kTZ + 2][kTY + 2][kTX + 2];
+    const int* list_in = lists + (epoch & 1) * ntiles;
+    int* list_out = lists + ((epoch + 1) & 1) * ntiles;
+    int* count_out = &ws->count[(epoch + 1) % 3];
+    if (blockIdx.x == 0 && threadIdx.x == 0) ws->count[(epoch + 2) % 3] = 0;
+    const int n = __hip_atomic_load(&ws->count[epoch % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+        const int t = list_in[idx];
+        const int bx = t % nbx, by = (t / nbx) % nby, bz = t / (nbx * nby);
+        const bool changed = grow_tile3d(data, region, dim, thr, bx, by, bz, sd, sr);
+        // a changed tile reached its local fixpoint; its 6 face neighbours see new halo cells next launch
+        // (the tile itself is re-queued only if a neighbour changes in turn)
+        if (changed && threadIdx.x < 7) {
+            const int d = threadIdx.x;
+            if (d == 0) {
+                ws->flag = 1;
+            } else {
+                const int nx = bx + (d == 1) - (d == 2), ny = by + (d == 3) - (d == 4), nz = bz + (d == 5) - (d == 6);
+                if (nx >= 0 && ny >= 0 && nz >= 0 && nx < nbx && ny < nby && nz < nbz)
+                    push_tile((nz * nby + ny) * nbx + nx, epoch + 1, mark, list_out, count_out);
+            }
+        }
+        __syncthreads();  // LDS tile buffers are reused by the next tile of this workgroup
+    }
+}
+
+// First work list: every tile holding a region voxel (16 B per thread loads of the region).
+__global__ __launch_bounds__(kThreads3) void region3d_seed_tiles_kernel(const unsigned char* __restrict__ region, int dim,
+                                                                       int nbx, int nby, Grow3dWs* __restrict__ ws,
+                                                                       int* __restrict__ mark, int* __restrict__ list0) {
+    // one workgroup per (y-row of tiles, z-slab of tiles): 8 x 8 voxel rows of the full x extent
+    const int by = blockIdx.x % nby, bz = blockIdx.x / nby;
+    const size_t plane = (size_t)dim * dim;
+    __shared__ int hit[64];
+    if (threadIdx.x < 64) hit[threadIdx.x] = 0;
+    __syncthreads();
+    const int vecs_per_row = dim / 16;  // dim % 16 == 0 on this path
+    for (int i = threadIdx.x; i < kTY * kTZ * vecs_per_row; i += kThreads3) {
+        const int v = i % vecs_per_row, yz = i / vecs_per_row;
+        const int y = by * kTY + yz % kTY, z = bz * kTZ + yz / kTY;
+        if (y >= dim || z >= dim) continue;
+        const pcmx::i32x4 w = *reinterpret_cast<const pcmx::i32x4*>(region + (size_t)z * plane + (size_t)y * dim + v * 16);
+        if ((w.x | w.y | w.z | w.w) != 0) hit[(v * 16) / kTX] = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x < nbx && hit[threadIdx.x]) {
+        const int t = (bz * nby + by) * nbx + threadIdx.x;
+        push_tile(t, 0, mark, list0, &ws->count[0]);
     }
 }
 
@@ -226,18 +286,43 @@ extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* regio
 
 extern "C" long long pcmx_region3d_workspace_bytes(int dim) {
     const long long nt = (long long)((dim + kTX - 1) / kTX) * ((dim + kTY - 1) / kTY) * ((dim + kTZ - 1) / kTZ);
-    return 16 + 2 * nt * 4;
+    return (long long)sizeof(Grow3dWs) + 3 * nt * 4;
 }
 
+// Grows `region` (0 = outside, nonzero = inside) to the 6-connected fixpoint. Host syncs once per `batch`
+// launches (a changed-flag read back); launches run on the device-built tile lists in between.
 extern "C" int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char* region, int dim, int thr, void* ws,
                                         int batch, int max_launches, hipStream_t s, int* launches_out) {
     if (dim <= 0 || !ws) return -1;
-    dim3 grid((dim + kTX - 1) / kTX, (dim + kTY - 1) / kTY, (dim + kTZ - 1) / kTZ);
-    const long long nt = (long long)grid.x * grid.y * grid.z;
-    auto launch = [&](const int* ain, int* aout, int* flag) {
-        region3d_tile_kernel<<<grid, kThreads3, 0, s>>>(data, region, dim, thr, ain, aout, flag);
-    };
-    return run_active_loop(launch, nt, ws, batch < 1 ? 8 : batch, max_launches, s, launches_out);
+    if (dim % 16 || (((uintptr_t)region) & 15)) return -1;  // seed scan reads 16-B vectors
+    const int nbx = (dim + kTX - 1) / kTX, nby = (dim + kTY - 1) / kTY, nbz = (dim + kTZ - 1) / kTZ;
+    if (nbx > 64) return -1;  // seed scan keeps one hit flag per x-tile in a 64-entry LDS array
+    const long long nt = (long long)nbx * nby * nbz;
+    if (nt > 0x3fffffff) return -1;
+    Grow3dWs* w = reinterpret_cast<Grow3dWs*>(ws);
+    int* mark = reinterpret_cast<int*>(w + 1);
+    int* lists = mark + nt;
+    // marks = -1 (no epoch), counters = 0, then the seed tiles (epoch 0) go to list 0
+    PCMX_HIP_RET(hipMemsetAsync(w, 0, sizeof(Grow3dWs), s));
+    PCMX_HIP_RET(hipMemsetAsync(mark, 0xff, (size_t)nt * 4, s));
+    region3d_seed_tiles_kernel<<<nby * nbz, kThreads3, 0, s>>>(region, dim, nbx, nby, w, mark, lists);
+    PCMX_HIP_RET(hipGetLastError());
+    const int b = batch < 1 ? 8 : batch;
+    int launches = 0;
+    while (launches < max_launches) {
+        PCMX_HIP_RET(hipMemsetAsync(&w->flag, 0, sizeof(int), s));
+        for (int i = 0; i < b && launches < max_launches; ++i, ++launches) {
+            region3d_list_kernel<<<kListGrid, kThreads3, 0, s>>>(data, region, dim, thr, nbx, nby, nbz, launches, w, mark,
+                                                               lists, (int)nt);
+            PCMX_HIP_RET(hipGetLastError());
+        }
+        int h = 0;
+        PCMX_HIP_RET(hipMemcpyAsync(&h, &w->flag, sizeof(int), hipMemcpyDeviceToHost, s));
+        PCMX_HIP_RET(hipStreamSynchronize(s));
+        if (!h) break;
+    }
+    if (launches_out) *launches_out = launches;
+    return 0;
 }
 
 extern "C" int pcmx_region3d_grow_naive(const unsigned char* data, unsigned char* region, int dim, int thr, int* flag_ws,
