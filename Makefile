@@ -40,4 +40,4 @@ run-raycast: all                     # 5-cuda-region-growing/Makefile
 run-raycast-opencl: all              # 6-opencl-region-growing/Makefile (IMAGE_DIM 64, naive grow, global caster)
 	bin/raycast --image-dim 64 --global --naive
 run-vmul: all                        # 6-opencl-region-growing/multiply_opencl.c
-	$(PY) -m parallel_c_programs_amd.cli.run_vmul
+	bin/vmul

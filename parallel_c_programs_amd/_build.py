@@ -153,6 +153,7 @@ BIN_TOOLS = {
     "device_info": ("bin/device_info_main.cpp", "hip"),
     "region": ("bin/region_main.cpp", "hip"),
     "mpi_ring": ("bin/mpi_ring_main.cpp", "hip"),
+    "vmul": ("bin/vmul_main.cpp", "hip"),
     "pcmx_launch": ("bin/launch_main.c", "c"),
 }
 

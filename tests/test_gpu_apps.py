@@ -156,3 +156,44 @@ def test_matrix_multiply_dispatches_to_mfma_backend(gpu):
     assert np.abs(out - ref).max() / np.abs(ref).max() < 1e-5
     for m in (a, b, c):
         lib.free_matrix(m)
+
+
+def _bin(name):
+    from conftest import ROOT
+
+    return str(ROOT / "bin" / name)
+
+
+def test_native_vmul_table(gpu):
+    import subprocess
+
+    r = subprocess.run([_bin("vmul")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    i = lines.index("Host\tDevice")
+    assert lines[i + 1:i + 11] == ["1.00\t1.00"] * 10
+    assert any("gfx950" in ln for ln in lines[:i])
+
+
+def test_native_raycast_opencl_variant_matches_ops(gpu, tmp_path):
+    """bin/raycast --image-dim 64 --global --naive (the OpenCL program) == the torch-op pipeline, bit for bit."""
+    import subprocess
+
+    r = subprocess.run([_bin("raycast"), "--image-dim", "64", "--global", "--naive"], capture_output=True, text=True,
+                       timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    img = bmp.read(tmp_path / "out.bmp")
+    vol = ops.create_volume(512, device=gpu, seed=0)
+    reg, _ = ops.region3d(vol, threshold=1, method="naive")
+    want = ops.raycast(vol, (reg != 0).to(torch.uint8), 64, method="global").cpu().numpy()
+    assert np.array_equal(img, want)
+
+
+def test_native_raycast_cuda_program(gpu, tmp_path):
+    import subprocess
+
+    r = subprocess.run([_bin("raycast")], capture_output=True, text=True, timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "Grow time:" in r.stdout and "Raycast time: " in r.stdout and r.stdout.count("Time : ") == 2
+    img = bmp.read(tmp_path / "out.bmp")
+    assert img.shape == (512, 512) and int((img == 255).sum()) > 0
