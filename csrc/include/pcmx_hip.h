@@ -120,6 +120,18 @@ int pcmx_stencil5x2_bf16(const void* u, void* out, int rows, int cols, int ld, i
 long long pcmx_spmv_csr_plan(const long long* row_ptr_host, int n_rows, void* items_host, long long max_items);
 int pcmx_spmv_csr(const long long* row_ptr, const int* col, const float* val, const float* x, float* y, int n_rows,
                   const void* items, long long n_items, hipStream_t s);
+/* XCD-sliced CSR (ops/sparse.py SlicedCSR): n_slices = 8 * phases <= PCMX_SPMV_MAX_SLICES; per nonzero col, val
+ * and lrow (u16 row offset inside its item); per slice nnz-balanced items (a later piece of a split long row
+ * has row1 == row0). Slice s runs on the blocks b with b % 8 == s % 8 (one XCD), writes ypart[s][0, n_rows);
+ * a combine pass sums the partials into y and a fix-up adds extra[fix[k].item] to y[fix[k].row].
+ * slice_nz0 / slice_item0 are HOST arrays (n_slices and n_slices + 1 entries). */
+#define PCMX_SPMV_MAX_SLICES 32
+int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x, float* ypart,
+                     float* extra, float* y, int n_rows, int n_cols, int n_slices, const long long* slice_nz0,
+                     const long long* slice_item0, const void* items, const void* fix, int n_fix, hipStream_t s);
+/* lab knob of the sliced kernel: bit 0 = skip the x gathers; mode >> 8 (if nonzero) = resident blocks per CU.
+ * Returns the previous setting. */
+int pcmx_spmv_set_mode(int mode);
 int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                      const float* x, float* y, hipStream_t s);
 

@@ -4,11 +4,19 @@
 // CSR (any sparsity, power-law safe): CSR-adaptive with nnz-balanced work items. An analysis pass
 // (pcmx_spmv_csr_plan, once per matrix) cuts the rows into items of <= kItemNnz nonzeros: runs of short
 // rows are packed into one item, a long row is split into several items. One wave per item:
-//   * multi-row item: the wave streams the item's values/columns coalesced (16 B per lane), multiplies by
-//     the gathered x, parks the products in LDS, then reduces rows with L = 64/rows lanes per row;
+//   * multi-row item: the wave streams the item's values/columns coalesced, multiplies by the gathered x,
+//     parks the products in LDS, then reduces rows with L = 64/rows lanes per row;
 //   * long-row piece: straight wave reduction, one float atomic per piece into y (y zeroed first).
 // Every wave does about the same number of nonzeros whatever the degree distribution, so the heavy rows
 // of a power-law graph do not produce a tail.
+//
+// XCD-sliced CSR (SlicedCSR in ops/sparse.py): the plain kernel's x gathers miss the 4-MiB per-XCD L2 ~85%
+// of the time at 1e7 columns (x = 40 MB) and run at the Infinity-Cache gather rate (~60 G gathers/s
+// measured chip-wide by scripts/gather_lab.hip, vs ~270 G/s when each XCD gathers from its own <= 4 MiB).
+// So the columns are cut into S = 8 * phases slices (a small, hot head of columns is dealt by rows instead,
+// so every XCD keeps its own copy of it); workgroups are dealt round-robin over the 8 XCDs, so block b runs
+// slice (b % 8) + 8 * phase and all of a slice's gathers stay inside ONE L2. Each slice writes a partial-y
+// row, a combine pass sums the S partials, a fix-up adds the later pieces of split long rows.
 //
 // Banded (implicit column indices): one wave per row; the 5 bands are contiguous slices of x and of the
 // value array, so all loads are unit-stride and no column index is ever read.
@@ -25,19 +33,23 @@ struct Item {
     long long nz0, nz1;    // nonzeros [nz0, nz1)
 };
 
-constexpr int kItemRows = 1024;           // rows per multi-row item (bounds the row-pointer LDS stage)
-constexpr int kPerLane = kItemNnz / kWave;  // nonzeros per lane in phase 1
+constexpr int kItemRows = 1023;           // rows per multi-row item (bounds the row-pointer LDS stage)
+constexpr int kRpPerLane = (kItemRows + 1 + 63) / 64;  // row pointers per lane (kItemRows + 1 per item)
+constexpr int kPerLane = kItemNnz / kWave;  // nonzeros per lane
+constexpr int kMaxSlices = PCMX_SPMV_MAX_SLICES;
+int g_persist_blocks = 2;  // sliced kernel: resident blocks (of 4 waves) per CU (170 VGPRs -> 2 waves/SIMD)
+int g_spmv_mode = 0;       // lab knob (pcmx_spmv_set_mode): 1 = skip the x gathers
 
-// One wave per item. Phase 1 issues every column/value load of the item up front (kPerLane coalesced
-// 256-B wave loads each), then all x gathers, so a lane keeps 2 x kPerLane loads in flight instead of a
-// dependent load chain. Products are parked in LDS with the item's row pointers; phase 2 reduces rows
-// with L lanes per row out of LDS only.
+// ------------------------------------------------------------------------------------------ plain CSR
+// One wave per item. All column/value loads of the item AND its row pointers are issued up front, then all
+// x gathers, so a lane keeps ~3 x kPerLane loads in flight instead of a dependent chain. Products are parked
+// in LDS with the row pointers; the row reduction (L lanes per row) then reads LDS only.
 __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_csr_items_kernel(
     const long long* __restrict__ row_ptr, const int* __restrict__ col, const float* __restrict__ val,
     const float* __restrict__ x, float* __restrict__ y, const Item* __restrict__ items, long long n_items) {
     __shared__ float prod[kWavesPerBlock][kItemNnz];
     __shared__ int rps[kWavesPerBlock][kItemRows + 1];
-    const int lane = pcmx::lane_id(), w = threadIdx.x / kWave;
+    const int w = threadIdx.x / kWave, lane = pcmx::lane_id();
     const long long it = (long long)blockIdx.x * kWavesPerBlock + w;
     if (it >= n_items) return;
     const Item item = items[it];
@@ -58,19 +70,28 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_csr_items_kernel(
         for (int j = 0; j < kPerLane; ++j) acc += vj[j] * x[cj[j]];
         acc = pcmx::wave_reduce<float, 0>(acc);
         if (lane == 0) {
-            const bool whole = nz0 == row_ptr[item.row0] && item.nz1 == row_ptr[item.row0 + 1];
-            if (whole)
+            if (nz0 == row_ptr[item.row0] && item.nz1 == row_ptr[item.row0 + 1])
                 y[item.row0] = acc;
             else
                 atomicAdd(&y[item.row0], acc);
         }
         return;
     }
+    long long rj[kRpPerLane];
+#pragma unroll
+    for (int j = 0; j < kRpPerLane; ++j) {
+        const int i = j * kWave + lane;
+        rj[j] = i <= nrows ? __builtin_nontemporal_load(row_ptr + item.row0 + i) : 0;
+    }
     float* pr = prod[w];
     int* rp = rps[w];
 #pragma unroll
     for (int j = 0; j < kPerLane; ++j) pr[j * kWave + lane] = vj[j] * x[cj[j]];
-    for (int i = lane; i <= nrows; i += kWave) rp[i] = (int)(row_ptr[item.row0 + i] - nz0);
+#pragma unroll
+    for (int j = 0; j < kRpPerLane; ++j) {
+        const int i = j * kWave + lane;
+        if (i <= nrows) rp[i] = (int)(rj[j] - nz0);
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // L lanes per row: about avg-row-length / 4 lanes, power of two, at most 64 / (rows per pass)
@@ -85,6 +106,177 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_csr_items_kernel(
         for (int off = L >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
         if (sub == 0) y[item.row0 + r] = acc;
     }
+}
+
+// ------------------------------------------------------------------------------------------ XCD-sliced CSR
+// Layout per slice: col/val of its nonzeros (slice-major, row order kept), lrow = the u16 row offset of each
+// nonzero inside its item, and nnz-balanced items (a later piece of a split long row has row1 == row0).
+// A slice averages ~1 nonzero per row, so rows are not reduced from row pointers: the wave scatters its
+// products with LDS float adds (ds_add_f32) into the item's rows. One wave owns its LDS rows and its adds
+// execute in program/lane order, so the sums are reproducible run to run.
+//
+// Persistent waves with a one-item software pipeline: a wave issues item k's gathers as soon as its columns
+// are in registers, then item k+1's stream loads, and only then waits for the gathers, so the next item's
+// HBM latency hides behind the current item's gathers and LDS work (measured: one item per wave 1.07 ms,
+// pipelined 0.99 ms at 8 slices). Every load and store of the loop is a buffer instruction whose descriptor
+// covers exactly the item's bytes: lanes past the end read 0 / drop their store in hardware, so no memory
+// instruction sits under a branch and the compiler's vmcnt bookkeeping stays exact across the loop.
+struct SliceMeta {
+    long long nz0[kMaxSlices];    // first nonzero of slice s in the slice-major col/val/lrow
+    long long item0[kMaxSlices + 1];
+};
+
+struct StreamRegs {
+    int c[kPerLane];
+    float v[kPerLane];
+    unsigned short r[kPerLane];
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void load_item_stream(const int* __restrict__ col, const float* __restrict__ val,
+                                                 const unsigned short* __restrict__ lrow, const Item& it, StreamRegs& q,
+                                                 int lane) {
+    const unsigned n = (unsigned)(it.nz1 - it.nz0);
+    const auto rc = rsrc(col + it.nz0, n * 4), rv = rsrc(val + it.nz0, n * 4), rr = rsrc(lrow + it.nz0, n * 2);
+#pragma unroll
+    for (int j = 0; j < kPerLane; ++j) {  // aux 2 = nt: streamed once
+        const unsigned i = j * kWave + lane;
+        q.c[j] = __builtin_amdgcn_raw_buffer_load_b32(rc, i * 4, 0, 2);
+        q.v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, i * 4, 0, 2));
+    }
+#pragma unroll
+    for (int j = 0; j < kPerLane; ++j) q.r[j] = __builtin_amdgcn_raw_buffer_load_b16(rr, (j * kWave + lane) * 2, 0, 2);
+}
+
+struct SlicedCtx {
+    const int* col;
+    const float* val;
+    const unsigned short* lrow;
+    __amdgpu_buffer_rsrc_t rx;
+    const Item* items;
+    float* yp;
+    float* extra;
+    float* yw;
+    long long i1, stride;
+    int lane;
+};
+
+// One pipeline step: gathers of the current item, stream loads of the next item, then the current item's
+// LDS scatter and stores. Called alternately with the two register sets swapped (a register copy would make
+// the compiler wait for the prefetch).
+template <int kMode>
+__device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, const Item& cur, const StreamRegs& q,
+                                            Item& nitem, StreamRegs& nq) {
+    const int lane = k.lane;
+    float g[kPerLane];
+#pragma unroll
+    for (int j = 0; j < kPerLane; ++j)
+        g[j] = (kMode & 1) ? __int_as_float(q.c[j])
+                           : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(k.rx, q.c[j] * 4, 0, 0));
+    const long long nxt = it + k.stride;
+    const bool more = nxt < k.i1;
+    nitem = k.items[more ? nxt : it];
+    load_item_stream(k.col, k.val, k.lrow, nitem, nq, lane);  // (a harmless re-read of the last item at the end)
+    const int n = (int)(cur.nz1 - cur.nz0);
+    const int nrows = cur.row1 - cur.row0;
+    float* dst;
+    int nstore;
+    if (nrows <= 1) {  // whole short row or a piece of a long row (later piece: row1 == row0 -> extra[it])
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) acc += q.v[j] * g[j];
+        acc = pcmx::wave_reduce<float, 0>(acc);
+        if (lane == 0) k.yw[0] = acc;
+        dst = nrows == 1 ? k.yp + cur.row0 : k.extra + it;
+        nstore = 1;
+    } else {
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const int i = j * kWave + lane;
+            if (i < nrows) k.yw[i] = 0.f;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const int i = j * kWave + lane;
+            if (i < n) atomicAdd(&k.yw[q.r[j]], q.v[j] * g[j]);
+        }
+        dst = k.yp + cur.row0;
+        nstore = nrows;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const auto ry = rsrc(dst, (unsigned)nstore * 4);
+#pragma unroll
+    for (int j = 0; j < kPerLane; ++j) {
+        const int i = j * kWave + lane;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(k.yw[i]), ry, i * 4, 0, 2);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // next item's zeroing after these LDS reads
+    it = nxt;
+    return more;
+}
+
+template <int kMode>
+__global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
+    const unsigned short* __restrict__ lrow, const int* __restrict__ col, const float* __restrict__ val,
+    const float* __restrict__ x, int n_cols, float* __restrict__ ypart, float* __restrict__ extra,
+    const Item* __restrict__ items, SliceMeta meta, int n_rows, int blocks_per_slice) {
+    __shared__ float yl[kWavesPerBlock][kItemRows + 1];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int b = blockIdx.x;
+    const int phase = b / (8 * blocks_per_slice);
+    const int s = phase * 8 + (b & 7);
+    SlicedCtx k;
+    k.i1 = meta.item0[s + 1];
+    k.stride = (long long)blocks_per_slice * kWavesPerBlock;
+    long long it = meta.item0[s] + (long long)((b >> 3) % blocks_per_slice) * kWavesPerBlock + w;
+    if (it >= k.i1) return;
+    const long long base = meta.nz0[s];
+    k.col = col + base, k.val = val + base, k.lrow = lrow + base;
+    k.rx = rsrc(x, (unsigned)n_cols * 4);
+    k.items = items, k.extra = extra, k.yp = ypart + (size_t)s * n_rows, k.yw = yl[w];
+    k.lane = pcmx::lane_id();
+    Item ia = items[it], ib;
+    StreamRegs qa, qb;
+    load_item_stream(k.col, k.val, k.lrow, ia, qa, k.lane);
+    while (sliced_step<kMode>(k, it, ia, qa, ib, qb) && sliced_step<kMode>(k, it, ib, qb, ia, qa)) {
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restrict__ ypart, float* __restrict__ y,
+                                                           int n_rows) {
+    using pcmx::f32x4;
+    const int n4 = n_rows / 4;
+    if (n_rows % 4 == 0) {  // partial rows are 16-B aligned
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+            f32x4 acc = pcmx::ld_nt(reinterpret_cast<const f32x4*>(ypart) + i);
+#pragma unroll
+            for (int s = 1; s < S; ++s)
+                acc += pcmx::ld_nt(reinterpret_cast<const f32x4*>(ypart + (size_t)s * n_rows) + i);
+            reinterpret_cast<f32x4*>(y)[i] = acc;
+        }
+        return;
+    }
+    for (int r = blockIdx.x * 256 + threadIdx.x; r < n_rows; r += gridDim.x * 256) {
+        float acc = 0.f;
+#pragma unroll
+        for (int s = 0; s < S; ++s) acc += ypart[(size_t)s * n_rows + r];
+        y[r] = acc;
+    }
+}
+
+// later pieces of split long rows: fix[k] = {item index, row}
+__global__ __launch_bounds__(256) void spmv_fixup_kernel(const float* __restrict__ extra, const int2* __restrict__ fix,
+                                                         int n_fix, float* __restrict__ y) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < n_fix) atomicAdd(&y[fix[k].y], extra[fix[k].x]);
 }
 
 // one wave per row of the banded matrix
@@ -153,6 +345,58 @@ extern "C" int pcmx_spmv_csr(const long long* row_ptr, const int* col, const flo
     spmv_csr_items_kernel<<<(unsigned)blocks, kWavesPerBlock * kWave, 0, s>>>(row_ptr, col, val, x, y,
                                                                                reinterpret_cast<const Item*>(items), n_items);
     return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x,
+                                float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
+                                const long long* slice_nz0, const long long* slice_item0, const void* items,
+                                const void* fix, int n_fix, hipStream_t s) {
+    if (n_rows <= 0) return 0;
+    if (n_slices <= 0 || n_slices % 8 || n_slices > kMaxSlices) return (int)hipErrorInvalidValue;
+    SliceMeta meta{};
+    long long most = 0;
+    for (int k = 0; k < n_slices; ++k) {
+        meta.nz0[k] = slice_nz0[k];
+        meta.item0[k] = slice_item0[k];
+        if (slice_item0[k + 1] < slice_item0[k]) return (int)hipErrorInvalidValue;
+        most = slice_item0[k + 1] - slice_item0[k] > most ? slice_item0[k + 1] - slice_item0[k] : most;
+    }
+    meta.item0[n_slices] = slice_item0[n_slices];
+    if (most > 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        const long long need = (most + kWavesPerBlock - 1) / kWavesPerBlock;
+        const long long per = (long long)(cus / 8) * g_persist_blocks;  // resident blocks per XCD
+        const int bp = (int)(need < per ? need : per);
+        const unsigned nb = (unsigned)(bp * n_slices);
+        if (g_spmv_mode & 1)
+            spmv_sliced_kernel<1><<<nb, kWavesPerBlock * kWave, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra,
+                                                                        reinterpret_cast<const Item*>(items), meta, n_rows, bp);
+        else
+            spmv_sliced_kernel<0><<<nb, kWavesPerBlock * kWave, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra,
+                                                                        reinterpret_cast<const Item*>(items), meta, n_rows, bp);
+    }
+    const long long want = (n_rows / 4 + 255) / 256;
+    const int cb = want > 2048 ? 2048 : (want < 1 ? 1 : (int)want);
+    switch (n_slices) {
+        case 8: spmv_combine_kernel<8><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
+        case 16: spmv_combine_kernel<16><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
+        case 24: spmv_combine_kernel<24><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
+        case 32: spmv_combine_kernel<32><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    if (n_fix > 0)
+        spmv_fixup_kernel<<<(n_fix + 255) / 256, 256, 0, s>>>(extra, reinterpret_cast<const int2*>(fix), n_fix, y);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_spmv_set_mode(int mode) {
+    const int old = g_spmv_mode | (g_persist_blocks << 8);
+    g_spmv_mode = mode & 0xff;
+    if (mode >> 8) g_persist_blocks = mode >> 8;
+    return old;
 }
 
 extern "C" int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,

@@ -324,6 +324,35 @@ at::Tensor spmv_csr(const at::Tensor& row_ptr, const at::Tensor& col, const at::
     return y;
 }
 
+// XCD-sliced CSR (see spmv.hip): meta is a CPU int64 tensor [2 * n_slices + 1] = slice nz0[n_slices] ++
+// slice item0[n_slices + 1]; ypart [n_slices * n_rows] and extra [n_items] are caller-owned scratch.
+at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::Tensor& val, const at::Tensor& x,
+                       const at::Tensor& items, const at::Tensor& fix, const at::Tensor& meta, at::Tensor ypart,
+                       at::Tensor extra, int64_t n_rows) {
+    check_gpu(lrow, "lrow", at::kShort), check_gpu(col, "col", at::kInt), check_gpu(val, "val", at::kFloat);
+    check_gpu(x, "x", at::kFloat), check_gpu(items, "items", at::kLong), check_gpu(fix, "fix", at::kInt);
+    check_gpu(ypart, "ypart", at::kFloat), check_gpu(extra, "extra", at::kFloat);
+    TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous(), "spmv_sliced: CPU int64 meta");
+    const int64_t S = (meta.numel() - 1) / 2;
+    TORCH_CHECK(S >= 8 && S % 8 == 0 && S <= PCMX_SPMV_MAX_SLICES, "spmv_sliced: 8, 16, 24 or 32 slices");
+    TORCH_CHECK(ypart.numel() >= S * n_rows && lrow.numel() == col.numel() && val.numel() == col.numel(),
+                "spmv_sliced: ypart / lrow / val shape");
+    TORCH_CHECK(x.numel() < (int64_t(1) << 30), "spmv_sliced: x must be < 2^30 elements (32-bit buffer offsets)");
+    const int64_t* m = meta.data_ptr<int64_t>();
+    TORCH_CHECK(m[S] >= 0 && m[2 * S] <= items.size(0) && extra.numel() >= items.size(0), "spmv_sliced: items/extra shape");
+    TORCH_CHECK(fix.dim() == 2 && fix.size(1) == 2, "spmv_sliced: fix [k, 2]");
+    for (int64_t k = 0; k < S; ++k)
+        TORCH_CHECK(m[k] >= 0 && m[k] <= col.numel() && m[S + k] <= m[S + k + 1], "spmv_sliced: meta");
+    const at::DeviceGuard g(val.device());
+    auto y = at::empty({n_rows}, val.options());
+    check_rc(pcmx_spmv_sliced(reinterpret_cast<const unsigned short*>(lrow.data_ptr<int16_t>()), col.data_ptr<int>(),
+                              val.data_ptr<float>(), x.data_ptr<float>(), ypart.data_ptr<float>(), extra.data_ptr<float>(),
+                              y.data_ptr<float>(), (int)n_rows, (int)x.numel(), (int)S, (const long long*)m,
+                              (const long long*)m + S, items.data_ptr(), fix.data_ptr(), (int)fix.size(0), cur_stream(val)),
+             "spmv_sliced");
+    return y;
+}
+
 at::Tensor spmv_banded(const at::Tensor& vals, const at::Tensor& row_off, int64_t n, int64_t a, int64_t b, int64_t c,
                        int64_t d, int64_t e, const at::Tensor& x) {
     check_gpu(vals, "vals", at::kFloat), check_gpu(row_off, "row_off", at::kLong), check_gpu(x, "x", at::kFloat);
@@ -393,6 +422,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
+    m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows) -> Tensor");
     m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x) -> Tensor");
     m.def("pack_edges(Tensor tile) -> Tensor");
     m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask) -> ()");
@@ -421,6 +451,7 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("stencil5_", stencil5_);
     m.impl("stencil5xT_", stencil5xT_);
     m.impl("spmv_csr", spmv_csr);
+    m.impl("spmv_sliced", spmv_sliced);
     m.impl("spmv_banded", spmv_banded);
     m.impl("pack_edges", pack_edges);
     m.impl("unpack_halo_", unpack_halo_);
@@ -430,6 +461,7 @@ PYBIND11_MODULE(_C, mod) {
     mod.doc() = "pcmx MI355X kernels (ops live under torch.ops.pcmx)";
     mod.def("device_count", []() { return pcmx_device_count(); });
     mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr");
+    mod.def("spmv_set_mode", [](int mode) { return pcmx_spmv_set_mode(mode); }, "sliced SpMV lab knob (0 = normal)");
     mod.def("sgemm_set_tuning", [](int order, int diag) { return pcmx_sgemm_set_tuning(order, diag); });
     mod.def("scan_set_rows", [](int rows) { return pcmx_scan_set_rows(rows); }, "scan tile shape: f32x4 rows per lane (16 = 8 waves, 8 = 16 waves)");
 }

@@ -146,11 +146,15 @@ class Stencil(Workload):
 class SpMV(Workload):
     """Power-law CSR SpMV (nnz-balanced row blocks) + all-gather of y: x <- A x."""
 
-    def __init__(self, ctx, n_rows=10_000_000, nnz=100_000_000, alpha=2.5, **_):
+    def __init__(self, ctx, n_rows=10_000_000, nnz=100_000_000, alpha=2.5, slices=16, head=0.0625,
+                 balance=0.0, **_):
         from ..parallel.spmv import DistributedSpMV
 
-        super().__init__(ctx, {"n_rows": n_rows, "nnz": nnz}, "spmv", "GFLOP/s")
-        self.d = DistributedSpMV.powerlaw(ctx, n_rows, nnz, alpha)
+        slices = int(slices) if ctx.device.type == "cuda" else 0
+        super().__init__(ctx, {"n_rows": n_rows, "nnz": nnz, "slices": slices, "head": head},
+                         "spmv", "GFLOP/s")
+        self.d = DistributedSpMV.powerlaw(ctx, n_rows, nnz, alpha, slices=slices, head=float(head),
+                                          balance=float(balance))
         self.x = torch.empty(n_rows, device=ctx.device)
         ops.rand_uniform_(self.x, 5, 0.0, 1.0)
         self.y = None

@@ -3,7 +3,7 @@ from .gemm import sgemm, sgemm_naive_host, sgemm_out, sgemm_simt
 from .halo import pack_edges, unpack_halo_
 from .image import (SEED_3D, Camera, apply_region_mask, corner_seeds, create_volume, default_camera, histeq, pad1,
                     raycast, region2d, region2d_grow_padded_, region3d)
-from .sparse import CSR, banded_csr, create_vector, powerlaw_csr, spmv, spmv_banded
+from .sparse import CSR, SlicedCSR, banded_csr, create_vector, powerlaw_csr, spmv, spmv_banded
 from .stencil import init_grid, stencil5_reference, stencil5_step_, stencil5x2_step_, stencil5_fused_step_
 from .vector import OP_CODES, axpy_, dot, fill_, rand_uniform_, reduce, scan, vadd, vmul
 
@@ -13,6 +13,6 @@ __all__ = [
     "histeq", "region2d", "region2d_grow_padded_", "region3d", "corner_seeds", "pad1", "apply_region_mask",
     "create_volume", "raycast", "default_camera", "Camera", "SEED_3D",
     "stencil5_step_", "stencil5x2_step_", "stencil5_fused_step_", "stencil5_reference", "init_grid",
-    "CSR", "banded_csr", "create_vector", "powerlaw_csr", "spmv", "spmv_banded",
+    "CSR", "SlicedCSR", "banded_csr", "create_vector", "powerlaw_csr", "spmv", "spmv_banded",
     "pack_edges", "unpack_halo_",
 ]

@@ -50,6 +50,116 @@ class CSR:
         return d
 
 
+class SlicedCSR:
+    """XCD-sliced CSR for SpMV on MI355X (csrc/kernels/spmv.hip: spmv_sliced_kernel).
+
+    The columns are cut into ``n_slices`` (8 x phases) ranges of about equal nnz; slice s keeps its nonzeros
+    contiguous (slice-major copy of col/val, row order kept), the u16 row offset of every nonzero inside its
+    work item (``lrow``) and its own nnz-balanced items. The kernel deals slice s to the workgroups that share
+    one XCD, so each 4-MiB L2 only holds one slice's part of x. ``head``: the lowest-index columns holding that
+    fraction of the nonzeros (the hottest of a power-law graph) are dealt to the slices by row blocks instead,
+    so every XCD keeps its own copy of them. Same product as the plain CSR kernel (fp32 sums in a different,
+    fixed order). Built once per matrix on the matrix's device (torch ops; the item cuts use the host planner).
+    """
+
+    def __init__(self, m: CSR, n_slices: int = 16, head: float = 0.0625, balance: float = 0.0):
+        from .. import _C  # noqa: F401  (pybind module carries the planner)
+
+        if n_slices % 8 or not 8 <= n_slices <= 32:
+            raise ValueError("n_slices must be 8, 16, 24 or 32")
+        dev = m.val.device
+        n, S, nnz = m.n_rows, n_slices, m.nnz
+        self.n_rows, self.n_cols, self.n_slices, self.nnz = n, m.n_cols, S, nnz
+        col = m.col.to(dev)
+        hist = torch.bincount(col, minlength=m.n_cols).double()
+        H = int(torch.searchsorted(hist.cumsum(0), torch.tensor([head * nnz], device=dev, dtype=torch.float64))) \
+            if head > 0 else 0
+        self.head_cols = H
+        # slice bounds over the tail: equal quantiles of a per-column cost = nnz in the column + balance * mean
+        # nnz per column (balance 0: equal nnz per slice, the measured best)
+        w = hist + balance * nnz / max(1, m.n_cols)
+        w[:H] = 0
+        cum = w.cumsum(0)
+        tgt = torch.arange(1, S, device=dev, dtype=torch.float64) * (float(cum[-1]) / S)
+        bounds = torch.searchsorted(cum, tgt, right=True).to(torch.int32)
+        self.bounds = bounds.cpu()
+        sid = torch.bucketize(col, bounds, right=True)  # slice of every nonzero (int64)
+        deg = (m.row_ptr[1:] - m.row_ptr[:-1]).to(dev)
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), deg)
+        if H > 0:  # head nonzeros: by row blocks of equal head nnz
+            inh = col < H
+            hrows = rows[inh]
+            hcum = torch.bincount(hrows, minlength=n).cumsum(0).double()
+            rcut = torch.searchsorted(hcum, torch.arange(1, S, device=dev, dtype=torch.float64) * (float(hcum[-1]) / S),
+                                      right=True)
+            sid[inh] = torch.bucketize(hrows, rcut, right=True)
+            del inh, hrows, hcum
+        order = torch.sort(sid, stable=True).indices
+        self.col = col[order].contiguous()
+        self.val = m.val.to(dev)[order].contiguous()
+        counts = torch.bincount(sid * n + rows, minlength=S * n).view(S, n)
+        del order, rows, sid, col
+        slice_nnz = counts.sum(1).cpu()
+        if int(slice_nnz.max()) >= 2 ** 31:
+            raise ValueError("a slice holds >= 2^31 nonzeros: use more slices")
+        nz0 = torch.zeros(S, dtype=torch.int64)
+        nz0[1:] = slice_nnz.cumsum(0)[:-1]
+        items, fix, item0 = [], [], [0]
+        self.lrow = torch.empty(nnz, dtype=torch.int16, device=dev)
+        for k in range(S):
+            rp = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            rp[1:] = counts[k].cumsum(0)
+            rpc = rp.cpu()
+            it = _C.spmv_csr_plan(rpc)
+            r0, r1 = it[:, 0] & 0xFFFFFFFF, it[:, 0] >> 32
+            # a later piece of a split long row: a single-row item not starting at the row's first nonzero;
+            # encoded as an empty row range (row1 == row0), its sum goes to extra[] and is fixed up into y
+            idx = torch.nonzero(((r1 - r0) == 1) & (it[:, 1] != rpc[r0])).flatten()
+            fix.append(torch.stack([idx + item0[-1], r0[idx]], 1))
+            it[idx, 0] = r0[idx] | (r0[idx] << 32)
+            items.append(it)
+            item0.append(item0[-1] + it.shape[0])
+            nzk = int(rpc[-1])
+            if nzk:  # row offset of every nonzero inside its item (< kItemRows = 1023; 0 for single-row items)
+                itd = it.to(dev)
+                row_of = torch.repeat_interleave(torch.arange(n, device=dev), counts[k])
+                item_of = torch.repeat_interleave(torch.arange(itd.shape[0], device=dev), itd[:, 2] - itd[:, 1])
+                off = (row_of - (itd[:, 0] & 0xFFFFFFFF)[item_of]).clamp_(min=0)
+                self.lrow[int(nz0[k]):int(nz0[k]) + nzk] = off.to(torch.int16)
+                del itd, row_of, item_of, off
+        del counts
+        self.items = torch.cat(items).to(dev)
+        self.fix = torch.cat(fix).to(torch.int32).contiguous().to(dev)
+        self.meta = torch.cat([nz0, torch.tensor(item0, dtype=torch.int64)]).contiguous()
+        self.ypart = torch.empty(S * n, dtype=torch.float32, device=dev)
+        self.extra = torch.empty(max(1, item0[-1]), dtype=torch.float32, device=dev)
+
+    def spmv(self, x: torch.Tensor) -> torch.Tensor:
+        return ops().spmv_sliced(self.lrow, self.col, self.val, x, self.items, self.fix, self.meta, self.ypart,
+                                 self.extra, self.n_rows)
+
+    def rows(self) -> torch.Tensor:
+        """Row of every stored nonzero, rebuilt from the items and lrow (the layout the kernel reads)."""
+        it = self.items
+        r0 = it[:, 0] & 0xFFFFFFFF
+        S = self.n_slices
+        out = torch.empty(self.nnz, dtype=torch.int64, device=it.device)
+        for k in range(S):
+            a, b = int(self.meta[S + k]), int(self.meta[S + k + 1])
+            base = int(self.meta[k])
+            itk = it[a:b]
+            item_of = torch.repeat_interleave(torch.arange(b - a, device=it.device), itk[:, 2] - itk[:, 1])
+            nzk = int(item_of.numel())
+            out[base:base + nzk] = r0[a:b][item_of] + self.lrow[base:base + nzk].long()
+        return out
+
+    def reference(self, x: torch.Tensor) -> torch.Tensor:
+        """fp64 product straight from the sliced layout (tests the layout on any device)."""
+        y = torch.zeros(self.n_rows, dtype=torch.float64, device=x.device)
+        y.index_add_(0, self.rows().to(x.device), self.val.double().to(x.device) * x.double()[self.col.long()])
+        return y
+
+
 class _CSRStruct(ctypes.Structure):
     _fields_ = [("n_row_ptr", ctypes.c_int), ("row_ptr", ctypes.POINTER(ctypes.c_int)),
                 ("col_ind", ctypes.POINTER(ctypes.c_int)), ("n_values", ctypes.c_int),

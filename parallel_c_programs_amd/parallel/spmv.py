@@ -13,7 +13,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ..ops.sparse import CSR, powerlaw_csr_rows, powerlaw_row_ptr, spmv
+from ..ops.sparse import CSR, SlicedCSR, powerlaw_csr_rows, powerlaw_row_ptr, spmv
 from .dist import Context
 
 
@@ -31,30 +31,39 @@ def nnz_balanced_cuts(row_ptr: torch.Tensor, parts: int) -> list[int]:
 
 
 class DistributedSpMV:
-    def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int]):
+    def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
+                 head: float = 0.0625, balance: float = 0.0):
         self.ctx, self.cuts, self.local = ctx, cuts, local.to(ctx.device)
+        self.sliced = None
         self.n = row_ptr.numel() - 1
         self.row0, self.row1 = cuts[ctx.rank], cuts[ctx.rank + 1]
         self.block = max(cuts[i + 1] - cuts[i] for i in range(ctx.world))
         if ctx.device.type == "cuda":
-            self.local.plan()
+            if slices:  # XCD-sliced layout (ops.SlicedCSR); the plain CSR copy is then dropped
+                self.sliced = SlicedCSR(self.local, slices, head, balance)
+                self.local = CSR(self.local.row_ptr[-1:], self.local.col[:0], self.local.val[:0], self.local.n_cols)
+            else:
+                self.local.plan()
         idx = torch.cat([torch.arange(cuts[r], cuts[r + 1]) - cuts[r] + r * self.block for r in range(ctx.world)])
         self.compact = idx.to(ctx.device)
         self.gathered = torch.empty(ctx.world * self.block, dtype=torch.float32, device=ctx.device)
         self.ybuf = torch.zeros(self.block, dtype=torch.float32, device=ctx.device)
 
     @staticmethod
-    def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1) -> "DistributedSpMV":
+    def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
+                 slices: int = 0, head: float = 0.0625, balance: float = 0.0) -> "DistributedSpMV":
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)
-        return DistributedSpMV(ctx, rp, local, cuts)
+        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance)
 
     @property
     def local_nnz(self) -> int:
-        return self.local.nnz
+        return self.sliced.nnz if self.sliced is not None else self.local.nnz
 
     def multiply_local(self, x: torch.Tensor) -> torch.Tensor:
+        if self.sliced is not None:
+            return self.sliced.spmv(x)
         return spmv(self.local, x)
 
     def allgather(self, y_local: torch.Tensor) -> torch.Tensor:

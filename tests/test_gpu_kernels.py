@@ -199,6 +199,44 @@ def test_spmv_long_rows(gpu):
     assert (out - ref).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("slices,head", [(8, 0.0), (16, 0.0625), (24, 0.0), (32, 0.2)])
+def test_spmv_sliced_powerlaw_vs_fp64(gpu, slices, head):
+    m = ops.powerlaw_csr(30000, 600_000, alpha=2.2, seed=5)
+    x = torch.rand(30000, dtype=torch.float32)
+    ref = ops.SlicedCSR(m, slices, head=head).reference(x)  # layout oracle (CPU)
+    rows = torch.repeat_interleave(torch.arange(m.n_rows), m.row_ptr[1:] - m.row_ptr[:-1])
+    want = torch.zeros(m.n_rows, dtype=torch.float64).index_add_(0, rows, m.val.double() * x.double()[m.col.long()])
+    absrow = torch.zeros(m.n_rows, dtype=torch.float64).index_add_(0, rows, (m.val.double() * x.double()[m.col.long()]).abs())
+    assert torch.allclose(ref, want, rtol=0, atol=1e-9)
+    s = ops.SlicedCSR(m.to(gpu), slices, head=head)
+    out = s.spmv(x.to(gpu)).cpu().double()
+    assert torch.equal(out, s.spmv(x.to(gpu)).cpu().double())  # reproducible
+    # fp32 accumulation: error bounded by a few ulps of the row's absolute sum
+    assert ((out - want).abs() / (absrow + 1e-3)).max().item() < 1e-5
+    plain = ops.spmv(m.to(gpu), x.to(gpu)).cpu().double()
+    assert ((out - plain).abs() / (absrow + 1e-3)).max().item() < 1e-5
+
+
+def test_spmv_sliced_long_rows_and_unsorted_columns(gpu):
+    # rows long enough to split into several items INSIDE one slice (fix-up path), empty rows, unsorted columns
+    n = 64
+    lens = torch.tensor([0, 40000, 3, 0, 17000, 1, 9000] + [5] * (n - 7))
+    rp = torch.zeros(n + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(lens, 0)
+    nnz = int(rp[-1])
+    g = torch.Generator().manual_seed(7)
+    col = torch.randint(0, 5000, (nnz,), dtype=torch.int32, generator=g)
+    val = torch.rand(nnz, generator=g) - 0.5
+    m = ops.CSR(rp, col, val, 5000)
+    x = torch.rand(5000, generator=g)
+    ref = m.dense().double() @ x.double()
+    s = ops.SlicedCSR(m.to(gpu), 8, head=0.1)
+    assert s.fix.shape[0] > 0
+    for _ in range(2):  # partials / extras are reused scratch: a second call must not accumulate
+        out = s.spmv(x.to(gpu)).cpu().double()
+        assert (out - ref).abs().max().item() < 1e-3
+
+
 @pytest.mark.parametrize("dtype", [torch.uint8, torch.bfloat16, torch.float32])
 def test_halo_pack_unpack(gpu, dtype):
     H, W = 37, 53

@@ -1,0 +1,49 @@
+"""CPU checks of the XCD-sliced SpMV layout (ops.SlicedCSR): the layout the gfx950 kernel reads must hold
+exactly the matrix's nonzeros, each with its row, whatever the slice count, head fraction or row lengths."""
+import pytest
+import torch
+
+from parallel_c_programs_amd import ops
+
+
+def _rows(m):
+    return torch.repeat_interleave(torch.arange(m.n_rows), m.row_ptr[1:] - m.row_ptr[:-1])
+
+
+def _fp64(m, x):
+    return torch.zeros(m.n_rows, dtype=torch.float64).index_add_(0, _rows(m), m.val.double() * x.double()[m.col.long()])
+
+
+@pytest.mark.parametrize("slices,head", [(8, 0.0), (16, 0.0625), (24, 0.3), (32, 0.0)])
+def test_sliced_layout_is_a_permutation_of_the_matrix(slices, head):
+    m = ops.powerlaw_csr(20000, 300_000, alpha=2.2, seed=9)
+    s = ops.SlicedCSR(m, slices, head=head)
+    key_a = torch.sort(_rows(m) * m.n_cols + m.col.long()).values
+    key_b = torch.sort(s.rows() * m.n_cols + s.col.long()).values
+    assert torch.equal(key_a, key_b)
+    x = torch.rand(m.n_cols)
+    assert torch.allclose(s.reference(x), _fp64(m, x), rtol=0, atol=1e-9)
+    assert s.lrow.min() >= 0 and s.lrow.max() < 1023
+
+
+def test_sliced_items_split_long_rows_and_cover_every_row():
+    n = 40
+    lens = torch.tensor([0, 30000, 2, 0, 5000] + [3] * (n - 5))
+    rp = torch.zeros(n + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(lens, 0)
+    g = torch.Generator().manual_seed(1)
+    col = torch.randint(0, 3000, (int(rp[-1]),), dtype=torch.int32, generator=g)
+    m = ops.CSR(rp, col, torch.rand(int(rp[-1]), generator=g), 3000)
+    s = ops.SlicedCSR(m, 8, head=0.0)
+    assert s.fix.shape[0] > 0 and set(s.fix[:, 1].tolist()) <= {1, 4}
+    it = s.items
+    r0, r1 = it[:, 0] & 0xFFFFFFFF, it[:, 0] >> 32
+    assert bool(((it[:, 2] - it[:, 1]) <= 1024).all()) and bool(((r1 - r0) <= 1023).all())
+    for k in range(8):  # every slice's items tile [0, n_rows) (later pieces are empty ranges)
+        a, b = int(s.meta[8 + k]), int(s.meta[9 + k])
+        covered = torch.zeros(n, dtype=torch.int64)
+        for i in range(a, b):
+            covered[int(r0[i]):int(r1[i])] += 1
+        assert bool((covered == 1).all())
+    x = torch.rand(3000, generator=g)
+    assert torch.allclose(s.reference(x), _fp64(m, x), rtol=0, atol=1e-9)
