@@ -127,13 +127,34 @@ def main():
     scan_gbps = None
     if not args.no_scan:
         y = torch.empty_like(x)
+        before = torch.zeros(1, device=dev)
 
         def scan_step():
-            native_ops().scan_out(x, y, False, None)
+            # global prefix sum over the rank-ordered concatenation: N > 1 reduce-then-scan (local HBM reduce,
+            # RCCL all-gather of the N totals, single-pass scan seeded with the lower ranks' sum)
+            if dist is None:
+                native_ops().scan_out(x, y, False, None)
+                return
+            tot = ops.reduce(x, "sum").reshape(1)
+            tots = torch.empty(world, device=dev)
+            dist.all_gather_into_tensor(tots, tot)
+            before.copy_(tots[:rank].sum().reshape(1))
+            native_ops().scan_out(x, y, False, before)
 
         t_scan = timed(scan_step, max(2, args.steps // 2), 1)
         scan_gbps = world * 8.0 * rn * max(2, args.steps // 2) / t_scan / 1e9
         del y
+
+    # vector all-reduce bandwidth over RCCL/xGMI (N > 1): 256 MiB of f32 per rank, ring bus bandwidth
+    ar_busbw = None
+    if dist is not None:
+        del x
+        torch.cuda.empty_cache()
+        v = torch.ones(64 << 20, device=dev)
+        ar_steps = max(3, args.steps // 2)
+        t_ar = timed(lambda: dist.all_reduce(v), ar_steps, 1)
+        ar_busbw = v.numel() * 4 * 2 * (world - 1) / world * ar_steps / t_ar / 1e9
+        del v
 
     if rank == 0:
         out = {
@@ -163,6 +184,7 @@ def main():
             "reduce_elements_per_gpu": rn,
             "reduce_rel_dev_from_expectation": red_rel,
             "scan_gbps": None if scan_gbps is None else round(scan_gbps, 1),
+            "allreduce_256MiB_busbw_gbps": None if ar_busbw is None else round(ar_busbw, 1),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
