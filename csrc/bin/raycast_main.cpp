@@ -93,8 +93,8 @@ int main(int argc, char** argv) {
     float cam12[12];
     for (int i = 0; i < 3; ++i)
         cam12[i] = cam.camera[i], cam12[3 + i] = cam.forward[i], cam12[6 + i] = cam.right[i], cam12[9 + i] = cam.up[i];
-    unsigned long long* tex = nullptr;
-    if (!global) CHECK(hipMalloc(&tex, nvox * sizeof(unsigned long long)));
+    void* tex = nullptr;  // 16-byte texels (pcmx_brick_pack)
+    if (!global) CHECK(hipMalloc(&tex, nvox * 16));
     t0 = pcmx_wtime();
     if (global) {
         CHECK(pcmx_raycast_global(data, region, dim, image, image_dim, cam12, cam.pixel_width, cam.step_size,

@@ -100,9 +100,11 @@ int pcmx_volume_gen_u8(unsigned char* data, int dim, unsigned seed, hipStream_t 
 int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
                         int image_dim, const float* cam12, float pixel_width, float step, int max_steps, int f64_color,
                         hipStream_t s);
-int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, unsigned long long* tex,
-                    hipStream_t s);
-int pcmx_raycast_bricked(const unsigned long long* tex, int dim, unsigned char* image, int image_dim,
+/* texture path: 16-byte texel per voxel = 2x2x2 footprint of data and region (dim <= 2048) */
+int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, void* tex, hipStream_t s);
+/* texture ray caster: steps per prefetch batch (1, 4 = default, 8, 16); returns the previous value */
+int pcmx_raycast_set_batch(int steps);
+int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* image, int image_dim,
                          const float* cam12, float pixel_width, float step, int max_steps, hipStream_t s);
 
 /* ---------------------------------------------------------------- stencil */

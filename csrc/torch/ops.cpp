@@ -264,9 +264,12 @@ at::Tensor raycast_global(const at::Tensor& data, const at::Tensor& region, int6
 at::Tensor brick_pack(const at::Tensor& data, const at::Tensor& region) {
     check_u8_gpu(data, "data"), check_u8_gpu(region, "region");
     const at::DeviceGuard g(data.device());
-    auto tex = at::empty(data.sizes(), data.options().dtype(at::kLong));
-    check_rc(pcmx_brick_pack(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0),
-                             reinterpret_cast<unsigned long long*>(tex.data_ptr<int64_t>()), cur_stream(data)),
+    TORCH_CHECK(data.dim() == 3 && data.sizes() == region.sizes() && data.size(0) == data.size(1) &&
+                    data.size(0) == data.size(2) && data.size(0) <= 2048 && data.is_contiguous() && region.is_contiguous(),
+                "brick_pack: contiguous cubic volumes, dim <= 2048");
+    auto tex = at::empty({data.size(0), data.size(1), data.size(2), 2}, data.options().dtype(at::kLong));  // 16 B texels
+    check_rc(pcmx_brick_pack(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0), tex.data_ptr(),
+                             cur_stream(data)),
              "brick_pack");
     return tex;
 }
@@ -274,10 +277,11 @@ at::Tensor brick_pack(const at::Tensor& data, const at::Tensor& region) {
 at::Tensor raycast_bricked(const at::Tensor& tex, int64_t image_dim, at::ArrayRef<double> cam12, double pixel_width,
                            double step, int64_t max_steps) {
     check_gpu(tex, "tex", at::kLong);
+    TORCH_CHECK(tex.dim() == 4 && tex.size(3) == 2 && tex.is_contiguous(), "raycast_bricked: tex from brick_pack");
     const at::DeviceGuard g(tex.device());
     auto img = at::empty({image_dim, image_dim}, tex.options().dtype(at::kByte));
     auto c = cam_vec(cam12);
-    check_rc(pcmx_raycast_bricked(reinterpret_cast<const unsigned long long*>(tex.data_ptr<int64_t>()), (int)tex.size(0),
+    check_rc(pcmx_raycast_bricked(tex.data_ptr(), (int)tex.size(0),
                                   img.data_ptr<uint8_t>(), (int)image_dim, c.data(), (float)pixel_width, (float)step,
                                   (int)max_steps, cur_stream(tex)),
              "raycast_bricked");
@@ -461,6 +465,7 @@ PYBIND11_MODULE(_C, mod) {
     mod.doc() = "pcmx MI355X kernels (ops live under torch.ops.pcmx)";
     mod.def("device_count", []() { return pcmx_device_count(); });
     mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr");
+    mod.def("raycast_set_batch", [](int steps) { return pcmx_raycast_set_batch(steps); }, "texture ray caster prefetch batch");
     mod.def("spmv_set_mode", [](int mode) { return pcmx_spmv_set_mode(mode); }, "sliced SpMV lab knob (0 = normal)");
     mod.def("sgemm_set_tuning", [](int order, int diag) { return pcmx_sgemm_set_tuning(order, diag); });
     mod.def("scan_set_rows", [](int rows) { return pcmx_scan_set_rows(rows); }, "scan tile shape: f32x4 rows per lane (16 = 8 waves, 8 = 16 waves)");

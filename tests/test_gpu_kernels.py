@@ -100,6 +100,45 @@ def test_raycast_texture_close(gpu):
     assert abs(a.mean().item() - b.mean().item()) < 3.0
 
 
+@pytest.mark.parametrize("dim", [20, 21, 64])
+def test_brick_pack_texels(gpu, dim):
+    # 16-byte texel = 2x2x2 footprint of data then of region (0/1), edge-clamped; vector (dim % 4 == 0) and
+    # scalar pack kernels against a plain torch gather
+    g = torch.Generator().manual_seed(dim)
+    d = torch.randint(0, 256, (dim, dim, dim), dtype=torch.uint8, generator=g)
+    r = (torch.rand(dim, dim, dim, generator=g) < 0.3).to(torch.uint8) * 7
+    from parallel_c_programs_amd._native import ops as native
+
+    tex = native().brick_pack(d.to(gpu), r.to(gpu)).cpu().view(torch.uint8).view(dim, dim, dim, 16)
+    i = torch.arange(dim)
+    i1 = (i + 1).clamp(max=dim - 1)
+    want = torch.empty(dim, dim, dim, 16, dtype=torch.uint8)
+    for w, (vol, zz) in enumerate([(d, i), (d, i1), ((r != 0).to(torch.uint8), i), ((r != 0).to(torch.uint8), i1)]):
+        for b, (yy, xx) in enumerate([(i, i), (i, i1), (i1, i), (i1, i1)]):
+            want[..., 4 * w + b] = vol[zz][:, yy][:, :, xx]
+    assert torch.equal(tex, want)
+
+
+def test_raycast_texture_batches_identical(gpu):
+    # the prefetch-batched march must give the image of the one-step-at-a-time march, bit for bit
+    from parallel_c_programs_amd import _C
+
+    vol = ops.create_volume(512, device=gpu, seed=0)
+    reg, _ = ops.region3d(vol, threshold=1)
+    reg = (reg != 0).to(torch.uint8)
+    imgs = []
+    old = _C.raycast_set_batch(1)
+    try:
+        for b in (1, 4, 8, 16):
+            _C.raycast_set_batch(b)
+            imgs.append(ops.raycast(vol, reg, 96, method="texture"))
+    finally:
+        _C.raycast_set_batch(old)
+    assert int(imgs[0].sum()) > 0
+    for im in imgs[1:]:
+        assert torch.equal(im, imgs[0])
+
+
 @pytest.mark.parametrize("shape", [(256, 512), (1000, 1024), (515, 4096)])
 def test_stencil_bit_exact(gpu, shape):
     rows, cols = shape
