@@ -94,7 +94,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 3; ++i)
         cam12[i] = cam.camera[i], cam12[3 + i] = cam.forward[i], cam12[6 + i] = cam.right[i], cam12[9 + i] = cam.up[i];
     void* tex = nullptr;  // 16-byte texels (pcmx_brick_pack)
-    if (!global) CHECK(hipMalloc(&tex, nvox * 16));
+    if (!global) CHECK(hipMalloc(&tex, nvox * 16 + 16));
     t0 = pcmx_wtime();
     if (global) {
         CHECK(pcmx_raycast_global(data, region, dim, image, image_dim, cam12, cam.pixel_width, cam.step_size,

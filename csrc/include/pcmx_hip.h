@@ -100,7 +100,9 @@ int pcmx_volume_gen_u8(unsigned char* data, int dim, unsigned seed, hipStream_t 
 int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
                         int image_dim, const float* cam12, float pixel_width, float step, int max_steps, int f64_color,
                         hipStream_t s);
-/* texture path: 16-byte texel per voxel = 2x2x2 footprint of data and region (dim <= 2048) */
+/* texture path: tex holds dim^3 * 16 + 16 bytes: per-voxel texels with the 2x2x2 footprint of data and region
+ * (8-byte texels when every data value < 128, else 16-byte; the format flag is stored behind the texels),
+ * dim <= 2048 */
 int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, void* tex, hipStream_t s);
 /* texture ray caster: steps per prefetch batch (1, 4 = default, 8, 16); returns the previous value */
 int pcmx_raycast_set_batch(int steps);

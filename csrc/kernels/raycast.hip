@@ -6,13 +6,15 @@
 //    of value_at, floor/ceil corner selection, f64 colour update of the C build, no FMA contraction).
 //    mode CUDA: the same with the f32 colour update of the CUDA kernel.
 //  * raycast_bricked: the reference's hardware-texture path re-designed for CDNA (gfx950 exposes no
-//    image/texture sampling to HIP): the volume is pre-packed into 8-byte texels holding the 2x2 (x,y)
-//    footprint of data AND region, so one trilinear sample of both volumes costs two 8-byte loads
-//    (z and z+1) instead of 16 byte loads; texel-centre addressing, clamp-to-edge and 8-bit fixed-point
-//    weights emulate cudaFilterModeLinear + cudaReadModeNormalizedFloat.
-//  * Both casters march positions by repeated f32 adds exactly like the reference, but skip sampling
+//    image/texture sampling to HIP): the volume is pre-packed into texels holding the whole 2x2x2 footprint
+//    of data AND region (8 bytes with the region in bit 7 when the data is < 128, else 16 bytes), so one
+//    trilinear sample of both volumes is ONE load instead of 16 byte loads; texel-centre addressing,
+//    clamp-to-edge and 8-bit fixed-point weights emulate cudaFilterModeLinear + cudaReadModeNormalizedFloat.
+//    Rays are clipped analytically to the volume and only the steps inside are visited (prefetched in
+//    batches). 512^2 image of the 512^3 reference volume: 3.18 -> 1.66 ms per frame including the pack.
+//  * raycast_global marches positions by repeated f32 adds exactly like the reference, but skips sampling
 //    while the ray is outside the volume's bounding box (the adds still run, so positions are unchanged)
-//    and stop once the ray has left it (a convex box cannot be re-entered): identical images, far fewer
+//    and stops once the ray has left it (a convex box cannot be re-entered): identical images, far fewer
 //    loads for rays that miss or exit early.
 //  * 16x16 pixel workgroups (4 wave64s of 16x4 pixels): neighbouring rays share cache lines.
 #include "pcmx_common.h"
@@ -131,35 +133,60 @@ __global__ __launch_bounds__(256) void raycast_ref_kernel(const unsigned char* _
 #pragma clang fp contract(on)
 
 // ---------------------------------------------------------------------------------- texture path
-// One 16-byte texel per voxel (x,y,z) holds the whole 2x2x2 trilinear footprint of data AND region:
-//   .x = data  (x,y,z)  (x+1,y,z)  (x,y+1,z)  (x+1,y+1,z)      .y = data at plane z+1 (same order)
-//   .z = region(x,y,z) ...                                      .w = region at plane z+1
-// (neighbours clamped to the volume edge), so one sample of both volumes is ONE 16-B load per lane. The
-// march is bound by the L2 lane-request rate (~2.6e8 samples per 512^2 image), so halving the requests per
-// sample (8-byte texels took two loads, planes z and z+1) is what counts.
+// Texel formats (chosen on the device, no host round trip: brick_pack first scans the data for a byte >= 128
+// and records the answer in a flag stored behind the texels, which every later kernel reads):
+//  * narrow (every data value < 128, e.g. the reference volume, values <= 50): 8 bytes per voxel holding the
+//    whole 2x2x2 trilinear footprint, region folded into bit 7 of each data byte:
+//      .x = [d|r<<7] at (x,y,z) (x+1,y,z) (x,y+1,z) (x+1,y+1,z)      .y = the same at plane z+1
+//  * wide (any value >= 128): 16 bytes per voxel, .x/.y = data at planes z/z+1, .z/.w = region (0/1).
+// Neighbours are clamped to the volume edge. One sample of both volumes is ONE load per lane: the march is
+// bound by the L2 lane-request rate (~2.6e8 samples per 512^2 image), and the pack by its texel writes.
+__global__ __launch_bounds__(256) void data_hibit_kernel(const unsigned char* __restrict__ data, size_t n,
+                                                        int* __restrict__ flag) {
+    size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    int hit = 0;
+    for (; i < n; i += (size_t)gridDim.x * 256 * 16) {
+        if (i + 16 <= n && ((reinterpret_cast<size_t>(data) + i) % 16) == 0) {
+            const uint4 v = *reinterpret_cast<const uint4*>(data + i);
+            hit |= ((v.x | v.y | v.z | v.w) & 0x80808080u) != 0;
+        } else {
+            for (size_t j = i; j < n && j < i + 16; ++j) hit |= data[j] >= 128;
+        }
+    }
+    if (__syncthreads_or(hit) && threadIdx.x == 0) atomicOr(flag, 1);
+}
+
+__device__ __forceinline__ unsigned rbit(unsigned char v) { return v != 0; }
+
 __global__ __launch_bounds__(256) void brick_pack_kernel(const unsigned char* __restrict__ data,
                                                         const unsigned char* __restrict__ region, int dim,
-                                                        uint4* __restrict__ tex) {
+                                                        void* __restrict__ tex, const int* __restrict__ wide_flag) {
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
     if (x >= dim) return;
+    const bool wide = *wide_flag != 0;
     const int x1 = min(x + 1, dim - 1), y1 = min(y + 1, dim - 1), z1 = min(z + 1, dim - 1);
-    const size_t P = (size_t)dim * dim;
+    const size_t P = (size_t)dim * dim, v = (size_t)z * P + (size_t)y * dim + x;
     unsigned w[4];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const size_t zz = (size_t)(q ? z1 : z) * P;
         const size_t r0 = zz + (size_t)y * dim, r1 = zz + (size_t)y1 * dim;
-        w[q] = (unsigned)data[r0 + x] | ((unsigned)data[r0 + x1] << 8) | ((unsigned)data[r1 + x] << 16) |
-               ((unsigned)data[r1 + x1] << 24);
-        w[2 + q] = (unsigned)(region[r0 + x] != 0) | ((unsigned)(region[r0 + x1] != 0) << 8) |
-                   ((unsigned)(region[r1 + x] != 0) << 16) | ((unsigned)(region[r1 + x1] != 0) << 24);
+        const unsigned d = (unsigned)data[r0 + x] | ((unsigned)data[r0 + x1] << 8) | ((unsigned)data[r1 + x] << 16) |
+                           ((unsigned)data[r1 + x1] << 24);
+        const unsigned r = rbit(region[r0 + x]) | (rbit(region[r0 + x1]) << 8) | (rbit(region[r1 + x]) << 16) |
+                           (rbit(region[r1 + x1]) << 24);
+        w[q] = wide ? d : (d | (r << 7));
+        w[2 + q] = r;
     }
-    tex[(size_t)z * P + (size_t)y * dim + x] = make_uint4(w[0], w[1], w[2], w[3]);
+    if (wide)
+        reinterpret_cast<uint4*>(tex)[v] = make_uint4(w[0], w[1], w[2], w[3]);
+    else
+        reinterpret_cast<uint2*>(tex)[v] = make_uint2(w[0], w[1]);
 }
 
 // 4 voxels per thread (dim % 4 == 0): each of the 8 source rows is read as one aligned u32 (+ the next byte);
-// the 4 texels go through LDS so the stores leave fully coalesced (consecutive lanes, consecutive 16 B): the
-// pack is bound by its 16 B/voxel of writes.
+// the 4 texels go through LDS so the stores leave fully coalesced (consecutive lanes, consecutive texels).
+// (4 rows per thread, re-using the shared source rows, measured slower: 64 KB of LDS halves occupancy.)
 __device__ __forceinline__ unsigned row5(const unsigned char* __restrict__ p, int x, int dim, unsigned& next) {
     next = p[min(x + 4, dim - 1)];
     return *reinterpret_cast<const unsigned*>(p + x);
@@ -174,8 +201,9 @@ __device__ __forceinline__ unsigned pair(unsigned a, unsigned an, unsigned b, un
 
 __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* __restrict__ data,
                                                          const unsigned char* __restrict__ region, int dim,
-                                                         uint4* __restrict__ tex) {
+                                                         void* __restrict__ tex, const int* __restrict__ wide_flag) {
     const int x = min((blockIdx.x * 256 + (int)threadIdx.x) * 4, dim - 4), y = blockIdx.y, z = blockIdx.z;
+    const bool wide = *wide_flag != 0;
     const int y1 = min(y + 1, dim - 1), z1 = min(z + 1, dim - 1);
     const size_t P = (size_t)dim * dim;
     const size_t rows[4] = {(size_t)z * P + (size_t)y * dim, (size_t)z * P + (size_t)y1 * dim,
@@ -191,17 +219,31 @@ __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* _
         rn[q] = rn[q] ? 1u : 0u;
     }
     __shared__ uint4 stage[1024];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        stage[threadIdx.x * 4 + i] = make_uint4(pair(d[0], dn[0], d[1], dn[1], i), pair(d[2], dn[2], d[3], dn[3], i),
-                                                pair(r[0], rn[0], r[1], rn[1], i), pair(r[2], rn[2], r[3], rn[3], i));
-    __syncthreads();
     const int xb = blockIdx.x * 1024;  // first voxel of this block's row segment
-    uint4* out = tex + rows[0];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int j = i * 256 + threadIdx.x;
-        if (xb + j < dim) out[xb + j] = stage[j];
+        const unsigned r0 = pair(r[0], rn[0], r[1], rn[1], i), r1 = pair(r[2], rn[2], r[3], rn[3], i);
+        const unsigned d0 = pair(d[0], dn[0], d[1], dn[1], i), d1 = pair(d[2], dn[2], d[3], dn[3], i);
+        if (wide)
+            stage[threadIdx.x * 4 + i] = make_uint4(d0, d1, r0, r1);
+        else
+            reinterpret_cast<uint2*>(stage)[threadIdx.x * 4 + i] = make_uint2(d0 | (r0 << 7), d1 | (r1 << 7));
+    }
+    __syncthreads();
+    if (wide) {
+        uint4* out = reinterpret_cast<uint4*>(tex) + rows[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = i * 256 + threadIdx.x;
+            if (xb + j < dim) out[xb + j] = stage[j];
+        }
+    } else {
+        uint2* out = reinterpret_cast<uint2*>(tex) + rows[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = i * 256 + threadIdx.x;
+            if (xb + j < dim) out[xb + j] = reinterpret_cast<const uint2*>(stage)[j];
+        }
     }
 }
 
@@ -223,9 +265,9 @@ __device__ __forceinline__ float q8(float f) { return rintf(f * 256.f) * (1.f / 
 // per batch (2*D texel loads in flight) and consumed in order with the reference's termination tests (stop at
 // colour >= 255, stop when the ray leaves the convex box). Positions differ from the reference's repeated
 // f32 adds by rounding only (~1e-3 voxel), below the 8-bit weight quantum of the emulated texture filter.
-template <int D>
-__global__ __launch_bounds__(256) void raycast_tex_kernel(const uint4* __restrict__ tex, int dim,
-                                                         unsigned char* __restrict__ image, int image_dim, Cam c) {
+template <int D, bool WIDE>
+__device__ __forceinline__ void raycast_tex_march(const void* __restrict__ texv, int dim,
+                                                  unsigned char* __restrict__ image, int image_dim, const Cam& c) {
     const int px = blockIdx.x * 16 + (threadIdx.x & 15);  // (8x8-pixel waves measured no faster)
     const int py = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (px >= image_dim || py >= image_dim) return;
@@ -259,7 +301,7 @@ __global__ __launch_bounds__(256) void raycast_tex_kernel(const uint4* __restric
         const int k1 = min(c.max_steps, (int)ceilf(k_hi) + 1);
         bool entered = false, active = true;
         for (int i = k0; active && i <= k1 && color < 255.f; i += D) {
-            uint4 t[D];
+            uint4 t[D];  // data z, data z+1, region z, region z+1 (4 corners each)
             float ax[D], ay[D], az[D];
             bool inb[D];
 #pragma unroll
@@ -277,7 +319,12 @@ __global__ __launch_bounds__(256) void raycast_tex_kernel(const uint4* __restric
                 x0 = min(x0, dim - 1), y0 = min(y0, dim - 1), z0 = min(z0, dim - 1);
                 const unsigned o = (unsigned)y0 * (unsigned)dim + (unsigned)x0;  // < 2^32 for dim <= 2048
                 // unconditional, always in-bounds load (no masked-load branch); unused when !inb
-                t[k] = tex[(size_t)z0 * P + o];
+                if constexpr (WIDE) {
+                    t[k] = reinterpret_cast<const uint4*>(texv)[(size_t)z0 * P + o];
+                } else {
+                    const uint2 q = reinterpret_cast<const uint2*>(texv)[(size_t)z0 * P + o];
+                    t[k] = make_uint4(q.x & 0x7f7f7f7fu, q.y & 0x7f7f7f7fu, (q.x >> 7) & 0x01010101u, (q.y >> 7) & 0x01010101u);
+                }
             }
 #pragma unroll
             for (int k = 0; k < D; ++k) {
@@ -297,6 +344,15 @@ __global__ __launch_bounds__(256) void raycast_tex_kernel(const uint4* __restric
         }
     }
     image[py * image_dim + px] = (unsigned char)(color > 255.f ? 255.f : color);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void raycast_tex_kernel(const void* __restrict__ tex, const int* __restrict__ wide,
+                                                         int dim, unsigned char* __restrict__ image, int image_dim, Cam c) {
+    if (*wide)
+        raycast_tex_march<D, true>(tex, dim, image, image_dim, c);
+    else
+        raycast_tex_march<D, false>(tex, dim, image, image_dim, c);
 }
 
 int g_tex_batch = 4;  // steps per prefetch batch (pcmx_raycast_set_batch; measured best of 1/4/8/16)
@@ -339,10 +395,14 @@ extern "C" int pcmx_raycast_global(const unsigned char* data, const unsigned cha
 extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, void* tex,
                                hipStream_t s) {
     if (dim <= 0 || dim > 2048) return -1;
+    const size_t nvox = (size_t)dim * dim * dim;
+    int* wide = reinterpret_cast<int*>(reinterpret_cast<char*>(tex) + nvox * 16);  // format flag behind the texels
+    PCMX_HIP_RET(hipMemsetAsync(wide, 0, sizeof(int), s));
+    data_hibit_kernel<<<1024, 256, 0, s>>>(data, nvox, wide);
     if (dim % 4 == 0 && (reinterpret_cast<size_t>(data) | reinterpret_cast<size_t>(region)) % 4 == 0)
-        brick_pack4_kernel<<<dim3((dim / 4 + 255) / 256, dim, dim), 256, 0, s>>>(data, region, dim, reinterpret_cast<uint4*>(tex));
+        brick_pack4_kernel<<<dim3((dim / 4 + 255) / 256, dim, dim), 256, 0, s>>>(data, region, dim, tex, wide);
     else
-        brick_pack_kernel<<<dim3((dim + 255) / 256, dim, dim), 256, 0, s>>>(data, region, dim, reinterpret_cast<uint4*>(tex));
+        brick_pack_kernel<<<dim3((dim + 255) / 256, dim, dim), 256, 0, s>>>(data, region, dim, tex, wide);
     return (int)hipGetLastError();
 }
 
@@ -351,12 +411,12 @@ extern "C" int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* ima
     if (dim <= 1 || dim > 2048 || image_dim <= 0) return -1;
     const Cam c = make_cam(cam12, pixel_width, step, max_steps);
     dim3 grid((image_dim + 15) / 16, (image_dim + 15) / 16);
-    const uint4* t4 = reinterpret_cast<const uint4*>(tex);
+    const int* wide = reinterpret_cast<const int*>(reinterpret_cast<const char*>(tex) + (size_t)dim * dim * dim * 16);
     switch (g_tex_batch) {
-        case 1: raycast_tex_kernel<1><<<grid, 256, 0, s>>>(t4, dim, image, image_dim, c); break;
-        case 16: raycast_tex_kernel<16><<<grid, 256, 0, s>>>(t4, dim, image, image_dim, c); break;
-        case 8: raycast_tex_kernel<8><<<grid, 256, 0, s>>>(t4, dim, image, image_dim, c); break;
-        default: raycast_tex_kernel<4><<<grid, 256, 0, s>>>(t4, dim, image, image_dim, c); break;
+        case 1: raycast_tex_kernel<1><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
+        case 16: raycast_tex_kernel<16><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
+        case 8: raycast_tex_kernel<8><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
+        default: raycast_tex_kernel<4><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
     }
     return (int)hipGetLastError();
 }

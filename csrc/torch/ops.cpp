@@ -2,6 +2,7 @@
 // GPU tensors dispatch here (DispatchKey "CUDA" is the HIP device on ROCm builds of PyTorch); kernels
 // run on the current torch HIP stream so they compose with torch.distributed (RCCL) streams and hipGraph
 // capture. Workspaces come from the torch caching allocator (no hipMalloc on the launch path).
+#include <cmath>
 #include <torch/extension.h>
 #include <torch/library.h>
 #include <c10/hip/HIPStream.h>
@@ -267,7 +268,7 @@ at::Tensor brick_pack(const at::Tensor& data, const at::Tensor& region) {
     TORCH_CHECK(data.dim() == 3 && data.sizes() == region.sizes() && data.size(0) == data.size(1) &&
                     data.size(0) == data.size(2) && data.size(0) <= 2048 && data.is_contiguous() && region.is_contiguous(),
                 "brick_pack: contiguous cubic volumes, dim <= 2048");
-    auto tex = at::empty({data.size(0), data.size(1), data.size(2), 2}, data.options().dtype(at::kLong));  // 16 B texels
+    auto tex = at::empty({data.numel() * 2 + 2}, data.options().dtype(at::kLong));  // texels + format flag
     check_rc(pcmx_brick_pack(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0), tex.data_ptr(),
                              cur_stream(data)),
              "brick_pack");
@@ -277,11 +278,14 @@ at::Tensor brick_pack(const at::Tensor& data, const at::Tensor& region) {
 at::Tensor raycast_bricked(const at::Tensor& tex, int64_t image_dim, at::ArrayRef<double> cam12, double pixel_width,
                            double step, int64_t max_steps) {
     check_gpu(tex, "tex", at::kLong);
-    TORCH_CHECK(tex.dim() == 4 && tex.size(3) == 2 && tex.is_contiguous(), "raycast_bricked: tex from brick_pack");
+    TORCH_CHECK(tex.dim() == 1 && tex.numel() >= 18 && tex.is_contiguous(), "raycast_bricked: tex from brick_pack");
+    const int64_t nvox = (tex.numel() - 2) / 2;
+    int64_t dim = (int64_t)std::llround(std::cbrt((double)nvox));
+    TORCH_CHECK(dim * dim * dim == nvox, "raycast_bricked: tex from brick_pack of a cubic volume");
     const at::DeviceGuard g(tex.device());
     auto img = at::empty({image_dim, image_dim}, tex.options().dtype(at::kByte));
     auto c = cam_vec(cam12);
-    check_rc(pcmx_raycast_bricked(tex.data_ptr(), (int)tex.size(0),
+    check_rc(pcmx_raycast_bricked(tex.data_ptr(), (int)dim,
                                   img.data_ptr<uint8_t>(), (int)image_dim, c.data(), (float)pixel_width, (float)step,
                                   (int)max_steps, cur_stream(tex)),
              "raycast_bricked");

@@ -12,6 +12,7 @@ from parallel_c_programs_amd.ops.image import default_camera  # noqa: E402
 vol = ops.create_volume(512, device="cuda", seed=0)
 reg, _ = ops.region3d(vol, threshold=1)
 tex = native().brick_pack(vol, (reg != 0).to(torch.uint8))
+
 cam = default_camera(512)
 
 
@@ -31,6 +32,9 @@ def timeit(fn, reps=10):
     return e0.elapsed_time(e1) / reps
 
 
+regb = (reg != 0).to(torch.uint8)
+print(f"brick_pack (narrow 8-B texels): {timeit(lambda: native().brick_pack(vol, regb)):.3f} ms")
+print(f"brick_pack (wide 16-B texels, data | 128): {timeit(lambda: native().brick_pack(vol | 128, regb)):.3f} ms")
 for ms in (1000, 2000, 3000, 4000, 5000):
     print(f"max_steps {ms}: {timeit(lambda: run(ms)):.3f} ms")
 

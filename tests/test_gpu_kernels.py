@@ -101,22 +101,34 @@ def test_raycast_texture_close(gpu):
 
 
 @pytest.mark.parametrize("dim", [20, 21, 64])
-def test_brick_pack_texels(gpu, dim):
-    # 16-byte texel = 2x2x2 footprint of data then of region (0/1), edge-clamped; vector (dim % 4 == 0) and
-    # scalar pack kernels against a plain torch gather
-    g = torch.Generator().manual_seed(dim)
-    d = torch.randint(0, 256, (dim, dim, dim), dtype=torch.uint8, generator=g)
+@pytest.mark.parametrize("hi", [128, 256])
+def test_brick_pack_texels(gpu, dim, hi):
+    # texel = 2x2x2 footprint of data then region, edge-clamped; narrow 8-B texels (region in bit 7) when every
+    # data value < 128, else 16-B texels; vector (dim % 4 == 0) and scalar pack kernels vs a plain torch gather
+    g = torch.Generator().manual_seed(dim + hi)
+    d = torch.randint(0, hi, (dim, dim, dim), dtype=torch.uint8, generator=g)
     r = (torch.rand(dim, dim, dim, generator=g) < 0.3).to(torch.uint8) * 7
     from parallel_c_programs_amd._native import ops as native
 
-    tex = native().brick_pack(d.to(gpu), r.to(gpu)).cpu().view(torch.uint8).view(dim, dim, dim, 16)
+    tex = native().brick_pack(d.to(gpu), r.to(gpu)).cpu()
+    n = dim ** 3
+    assert tex.numel() == 2 * n + 2
+    wide = int(tex[2 * n].item() & 0xFFFFFFFF)
+    assert wide == (1 if hi > 128 else 0)
     i = torch.arange(dim)
     i1 = (i + 1).clamp(max=dim - 1)
-    want = torch.empty(dim, dim, dim, 16, dtype=torch.uint8)
-    for w, (vol, zz) in enumerate([(d, i), (d, i1), ((r != 0).to(torch.uint8), i), ((r != 0).to(torch.uint8), i1)]):
-        for b, (yy, xx) in enumerate([(i, i), (i, i1), (i1, i), (i1, i1)]):
-            want[..., 4 * w + b] = vol[zz][:, yy][:, :, xx]
-    assert torch.equal(tex, want)
+    rb = (r != 0).to(torch.uint8)
+
+    def corners(vol, zz):
+        return torch.stack([vol[zz][:, yy][:, :, xx] for yy, xx in [(i, i), (i, i1), (i1, i), (i1, i1)]], -1)
+
+    if wide:
+        got = tex[:2 * n].view(torch.uint8).view(dim, dim, dim, 16)
+        want = torch.cat([corners(d, i), corners(d, i1), corners(rb, i), corners(rb, i1)], -1)
+    else:
+        got = tex[:n].view(torch.uint8).view(dim, dim, dim, 8)
+        want = torch.cat([corners(d, i) | (corners(rb, i) << 7), corners(d, i1) | (corners(rb, i1) << 7)], -1)
+    assert torch.equal(got, want)
 
 
 def test_raycast_texture_batches_identical(gpu):
