@@ -63,6 +63,19 @@ def test_region3d_small(gpu, method):
     assert n >= 1
 
 
+@pytest.mark.parametrize("dim,thr,levels", [(96, 1, 2), (128, 1, 3), (64, 3, 8), (128, 2, 5)])
+def test_region3d_tiled_random_maze(gpu, dim, thr, levels):
+    # random low-entropy volumes (long snaking similar paths), partial x-tiles (96), seeds on tile faces /
+    # volume edges (a seed on a face of a tile that cannot grow), several thresholds: the bit-parallel tiled
+    # grow equals the serial flood fill
+    g = torch.Generator().manual_seed(dim * 10 + thr)
+    vol = (torch.randint(0, levels, (dim, dim, dim), generator=g) * 3).to(torch.uint8)
+    for seed in [(0, 0, 0), (63, 8, 16), (dim - 1, dim - 1, dim - 1), (32, 7, 8), (min(64, dim - 1), 15, 7)]:
+        ref, _ = ops.region3d(vol, seed=seed, threshold=thr)
+        reg, n = ops.region3d(vol.to(gpu), seed=seed, threshold=thr, method="tiled")
+        assert torch.equal((reg.cpu() != 0).to(torch.uint8), ref), seed
+
+
 def test_region3d_reference_box(gpu):
     # T2: the region from seed (50,300,300) is exactly the 99x149x149 box (2,197,899 voxels)
     vol = ops.create_volume(512, device=gpu, seed=0)
