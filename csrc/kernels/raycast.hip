@@ -218,32 +218,27 @@ __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* _
                ((r[q] & 0xff000000) ? 0x1000000u : 0u);
         rn[q] = rn[q] ? 1u : 0u;
     }
-    __shared__ uint4 stage[1024];
+    // texel j lives in slot j + j/16: the 16-B slots written by lanes t, t+4, ... (texels 4t+i) then fall on
+    // distinct LDS banks, and the coalesced read-back (texels j, j+1, ...) stays contiguous
+    __shared__ uint4 stage[1024 + 64];
     const int xb = blockIdx.x * 1024;  // first voxel of this block's row segment
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const unsigned r0 = pair(r[0], rn[0], r[1], rn[1], i), r1 = pair(r[2], rn[2], r[3], rn[3], i);
         const unsigned d0 = pair(d[0], dn[0], d[1], dn[1], i), d1 = pair(d[2], dn[2], d[3], dn[3], i);
-        if (wide)
-            stage[threadIdx.x * 4 + i] = make_uint4(d0, d1, r0, r1);
-        else
-            reinterpret_cast<uint2*>(stage)[threadIdx.x * 4 + i] = make_uint2(d0 | (r0 << 7), d1 | (r1 << 7));
+        const int j = threadIdx.x * 4 + i;
+        stage[j + (j >> 4)] = wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
     }
     __syncthreads();
-    if (wide) {
-        uint4* out = reinterpret_cast<uint4*>(tex) + rows[0];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int j = i * 256 + threadIdx.x;
-            if (xb + j < dim) out[xb + j] = stage[j];
-        }
-    } else {
-        uint2* out = reinterpret_cast<uint2*>(tex) + rows[0];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int j = i * 256 + threadIdx.x;
-            if (xb + j < dim) out[xb + j] = reinterpret_cast<const uint2*>(stage)[j];
-        }
+    for (int i = 0; i < 4; ++i) {
+        const int j = i * 256 + threadIdx.x;
+        if (xb + j >= dim) continue;
+        const uint4 t = stage[j + (j >> 4)];
+        if (wide)
+            reinterpret_cast<uint4*>(tex)[rows[0] + xb + j] = t;
+        else
+            reinterpret_cast<uint2*>(tex)[rows[0] + xb + j] = make_uint2(t.x, t.y);
     }
 }
 
