@@ -79,9 +79,10 @@ int pcmx_sgemm_f32_simt(const float* A, const float* B, float* C, int M, int N, 
 int pcmx_sgemm_set_tuning(int tile_order, int k0_diag);
 
 /* ---------------------------------------------------------------- histogram equalisation */
-/* out = tf[img] (bit-identical to the serial reference); hist_ws: 256 u32 (also receives the histogram) */
-int pcmx_histeq_u8(const unsigned char* img, unsigned char* out, long long npix, unsigned* hist_ws, int force_multiblock,
-                   hipStream_t s);
+/* out = tf[img] (bit-identical to the serial reference). ws: pcmx_histeq_workspace_bytes(), 16-B aligned, ZEROED
+ * before the first call and left zeroed by every call (self-cleaning ticket); one call in flight per workspace. */
+long long pcmx_histeq_workspace_bytes(void);
+int pcmx_histeq_u8(const unsigned char* img, unsigned char* out, long long npix, void* ws, hipStream_t s);
 
 /* ---------------------------------------------------------------- region growing */
 long long pcmx_region2d_workspace_bytes(int H, int W);

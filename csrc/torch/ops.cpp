@@ -3,6 +3,8 @@
 // run on the current torch HIP stream so they compose with torch.distributed (RCCL) streams and hipGraph
 // capture. Workspaces come from the torch caching allocator (no hipMalloc on the launch path).
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <torch/extension.h>
 #include <torch/library.h>
 #include <c10/hip/HIPStream.h>
@@ -185,14 +187,26 @@ void check_u8_gpu(const at::Tensor& t, const char* name) {
 }
 
 // ---------------------------------------------------------------- histogram equalisation
-at::Tensor histeq(const at::Tensor& img, bool force_multiblock) {
+// The multi-block histeq keeps its histogram + ticket in a workspace that every call leaves zeroed, so it is
+// allocated (and zeroed) once per (device, stream): no memset launch per call, and calls on different streams
+// never share one.
+at::Tensor& histeq_workspace(const at::Tensor& like, hipStream_t s) {
+    static std::mutex mu;
+    static auto* cache = new std::map<std::pair<int, hipStream_t>, at::Tensor>();  // never destroyed: no frees at exit
+    std::lock_guard<std::mutex> lock(mu);
+    auto& ws = (*cache)[{like.device().index(), s}];
+    if (!ws.defined()) ws = at::zeros({pcmx_histeq_workspace_bytes()}, like.options().dtype(at::kByte));
+    return ws;
+}
+
+at::Tensor histeq(const at::Tensor& img) {
     check_u8_gpu(img, "img");
     const at::DeviceGuard g(img.device());
     auto ic = aligned_contig(img);
     auto out = at::empty_like(ic);
-    auto hist = at::empty({256}, img.options().dtype(at::kInt));
-    check_rc(pcmx_histeq_u8(ic.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), ic.numel(),
-                            reinterpret_cast<unsigned*>(hist.data_ptr<int>()), force_multiblock ? 1 : 0, cur_stream(img)),
+    const hipStream_t s = cur_stream(img);
+    auto& ws = histeq_workspace(ic, s);
+    check_rc(pcmx_histeq_u8(ic.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), ic.numel(), ws.data_ptr(), s),
              "histeq");
     return out;
 }
@@ -420,7 +434,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("sgemm_out(Tensor a, Tensor b, Tensor(a!) c, float alpha=1., float beta=0., int variant=-1) -> Tensor(a!)");
     m.def("sgemm_simt(Tensor a, Tensor b) -> Tensor");
     m.def("device_info(int device=0) -> ()", device_info);
-    m.def("histeq(Tensor img, bool force_multiblock=False) -> Tensor");
+    m.def("histeq(Tensor img) -> Tensor");
     m.def("region2d_grow_(Tensor(a!) region, Tensor img, int thr, int batch=4, int max_launches=100000) -> int");
     m.def("region3d_grow_(Tensor(a!) region, Tensor data, int thr, bool tiled=True, int batch=8, int max_launches=1000000) -> int");
     m.def("volume_gen_(Tensor(a!) data, int seed) -> Tensor(a!)");

@@ -22,13 +22,16 @@ from .._native import cpu_lib, ops
 def histeq(img: torch.Tensor, method: str = "auto", n_threads: int = 4) -> torch.Tensor:
     """Equalise an 8-bit image (bit-identical to the serial reference on every path).
 
-    method (CPU only): "serial" | "omp" | "pthreads"; GPU: "auto" (fused single launch for small images)
-    or "multiblock".
+    method (CPU only): "serial" | "omp" | "pthreads". GPU tensors always run the two-launch gfx950 path
+    (per-lane LDS counters + bank-replicated LUT map, csrc/kernels/histeq.hip); "auto" / "multiblock" are
+    accepted for GPU tensors.
     """
     if img.dtype != torch.uint8:
         raise TypeError("histeq: uint8 image expected")
     if img.is_cuda:
-        return ops().histeq(img.contiguous(), method == "multiblock").view(img.shape)
+        if method not in ("auto", "multiblock"):
+            raise ValueError(f"histeq: method {method!r} is CPU-only")
+        return ops().histeq(img.contiguous()).view(img.shape)
     src = img.contiguous()
     out = torch.empty_like(src)
     lib = cpu_lib()

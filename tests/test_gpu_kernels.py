@@ -26,6 +26,24 @@ def test_histeq_large_random(gpu):
     assert torch.equal(ops.histeq(img.to(gpu), "multiblock").cpu(), ref)
 
 
+@pytest.mark.parametrize("shape,hi", [((1, 7), 256), ((17, 3), 5), ((512, 512), 1), ((1023, 1021), 3),
+                                      ((4096, 4096), 256)])
+def test_histeq_tails_and_skew(gpu, shape, hi):
+    """npix % 16 tails, one-block grids, single-bin images (every pixel on one per-lane counter) and repeated
+    calls on the self-cleaning workspace, on the default and a side stream."""
+    g = torch.Generator().manual_seed(shape[0] * 7 + hi)
+    img = torch.randint(0, hi, shape, dtype=torch.uint8, generator=g) + (255 - hi if hi < 200 else 0)
+    ref = ops.histeq(img, "serial")
+    gi = img.to(gpu)
+    for _ in range(3):
+        assert torch.equal(ops.histeq(gi).cpu(), ref)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        out = ops.histeq(gi)
+    s.synchronize()
+    assert torch.equal(out.cpu(), ref)
+
+
 def test_region2d_golden(gpu, assets):
     img = torch.from_numpy(bmp.read(assets / "pic1.bmp").copy())
     gold = torch.from_numpy(bmp.read(assets / "region_pic1_golden.bmp").copy())
