@@ -616,7 +616,9 @@ int launch1w(const float* A, const float* B, float* Cm, int M, int N, int K, int
 
 
 // ---------------------------------------------------------------------------------------------------
-// Production kernel (variant 7): one wave per SIMD, register-staged, every LDS access 16 B wide.
+// Register-staged kernels: variant 7 (4 waves, one per SIMD) and the production variant 16 (CfgRS8: 8 waves,
+// two per SIMD, wave tile 64x128, 128 accumulators in VGPRs — the second wave per SIMD issues MFMAs while the
+// other waits at the per-stage barrier; +1.1% at 8192^3, 148.1 -> 149.8 TFLOPS). Every LDS access 16 B wide.
 //  * 256x256x32 tile, 4 waves as 2x2, each wave 128x128 = 4x4 tiles of v_mfma_f32_32x32x2_f32
 //    (256 accumulators in AGPRs).
 //  * Staging: buffer_load_dwordx4 (one SRD per operand, 32-bit voffset + scalar soffset: 2 VGPRs of
@@ -629,15 +631,16 @@ int launch1w(const float* A, const float* B, float* Cm, int M, int N, int K, int
 //    and the epilogue stores 16 B per lane (512 contiguous bytes per row).
 //  * 32 ds_read_b128 + 16 ds_write_b128 + 16 buffer loads per 256 MFMAs per wave, each non-MFMA
 //    instruction pinned between MFMA groups (sched_barrier) so it issues in the MFMA shadow.
-struct CfgRS {
-    static constexpr int BM = 256, BN = 256, BK = 32, WM = 2, WN = 2;
+template <int WM_, int WN_>
+struct CfgRSW {
+    static constexpr int BM = 256, BN = 256, BK = 32, WM = WM_, WN = WN_;
     static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
     static constexpr int kWaveM = BM / WM, kWaveN = BN / WN;
     static constexpr int MT = kWaveM / 32, NT = kWaveN / 32;
     static constexpr int kAFloats = BM * BK, kBFloats = BK * BN;
     static constexpr int kStage = kAFloats + kBFloats;
-    static constexpr int kAPW = BM / 8 / kWaves;   // A pieces (8 rows x 128 B) per wave: 8
-    static constexpr int kBPW = BK / kWaves;       // B pieces (one 1-KiB k-row) per wave: 8
+    static constexpr int kAPW = BM / 8 / kWaves;   // A pieces (8 rows x 128 B) per wave: 8 (4 waves) / 4 (8 waves)
+    static constexpr int kBPW = BK / kWaves;       // B pieces (one 1-KiB k-row) per wave: 8 / 4
     // padded-A layout (PADA): rows of BK+4 floats (144 B): 8 consecutive rows of a ds_read_b128 group hit
     // disjoint 16-B bank slots (144r mod 256 = 0,144,32,176,...), so the k-chunk enters the address as a
     // compile-time constant (ds_read offset field) instead of an XOR with a lane-dependent swizzle.
@@ -646,14 +649,15 @@ struct CfgRS {
     static constexpr int kStagePad = kAFloatsPad + kBFloats;
     static_assert(NT == 4, "interleaved-column B read assumes 4 N-tiles per wave");
 };
+using CfgRS = CfgRSW<2, 2>;   // production: 4 waves (1 per SIMD), wave tile 128x128 (256 accumulators)
+using CfgRS8 = CfgRSW<4, 2>;  // 8 waves (2 per SIMD), wave tile 64x128 (128 accumulators)
 
-template <bool BETA, int SCHED, bool PADA = false>
-__global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const float* __restrict__ A,
+template <bool BETA, int SCHED, bool PADA = false, class C = CfgRS>
+__global__ __launch_bounds__(C::kThreads, 1) void sgemm_rs_kernel(const float* __restrict__ A,
                                                                      const float* __restrict__ B,
                                                                      float* __restrict__ Cmat, int M, int N, int K,
                                                                      int lda, int ldb, int ldc, float alpha,
                                                                      float beta) {
-    using C = CfgRS;
     typedef __attribute__((address_space(3))) pcmx::f32x4 lds_f4;
     constexpr int kSt = PADA ? C::kStagePad : C::kStage;      // floats per LDS stage
     constexpr int kAF = PADA ? C::kAFloatsPad : C::kAFloats;  // floats of the A part of a stage
@@ -736,7 +740,7 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
 #pragma unroll
                 for (int j = 0; j < C::NT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[s][j], acc[i][j], 0, 0, 0);
-                if (i & 1) filler(s * 2 + (i >> 1));
+                filler(s * C::MT + i);
             }
     };
     auto none = [](int) {};
@@ -760,14 +764,19 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
 
     pcmx::f32x4 fa0[C::MT], fa1[C::MT], fb0[4], fb1[4];
     read(lds, 0, fa0, fb0);
+    if constexpr (SCHED == 3) {  // the loop is entered with no LDS op pending (see the end of stage())
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     auto stage = [&](int t, auto write_c, auto load_c) {
         constexpr bool WRITE = decltype(write_c)::value;  // registers hold stage t+1
         constexpr bool LOAD = decltype(load_c)::value;    // stage t+2 exists
         lds_float* cur = lds + (t & 1) * kSt;
         lds_float* nxt = lds + ((t + 1) & 1) * kSt;
         const int k2 = (t + 2) * C::BK;
-        // SCHED 0: pieces 0..15 after every 8 MFMAs of chunks 0-1 (pinned); 1: one piece per 16 MFMAs over
-        // all 4 chunks (pinned); 2: as 0 without sched_barrier pinning.
+        // SCHED 0: the stage's pieces spread over chunks 0-1, each pinned between MFMA groups; 2: as 0 without
+        // sched_barrier pinning; 3: as 0 plus pinned LDS reads and explicit stage-boundary waits (below).
         auto fill = [&](int qq) __attribute__((always_inline)) {
             auto body = [&] {
                 lwrite(qq, nxt);
@@ -775,25 +784,43 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
             };
             if constexpr (SCHED == 2) body(); else pin(body);
         };
+        // filler(slot) runs after every NT MFMAs (slot = s * MT + i, 4 * MT slots per chunk); the stage's
+        // P = kAPW + kBPW pieces are spread evenly over chunks 0-1. (Spreading them over all 4 chunks, a former
+        // SCHED 1, is a race: chunk 3 runs after the barrier while other waves already read `nxt`.)
         auto chunk_filler = [&](int chunk) __attribute__((always_inline)) {
             return [&, chunk](int slot) __attribute__((always_inline)) {
                 if constexpr (!WRITE) return;
-                if constexpr (SCHED == 1) {
-                    if (slot & 1) fill(chunk * 4 + (slot >> 1));
-                } else {
-                    if (chunk < 2) fill(chunk * 8 + slot);
-                }
+                constexpr int P = C::kAPW + C::kBPW, kSlots = 4 * C::MT;
+                constexpr int kChunks = 2, kPer = P / kChunks, kEvery = kSlots / kPer;
+                static_assert(P % kChunks == 0 && kSlots % kPer == 0, "even piece spread");
+                if (chunk < kChunks && (slot + 1) % kEvery == 0) fill(chunk * kPer + slot / kEvery);
             };
         };
-        read(cur, 1, fa1, fb1);
+        // SCHED 3: every chunk's LDS reads pinned where they are written (the scheduler otherwise sinks the
+        // chunk-3 B reads next to the barrier, whose lgkmcnt(0) then exposes their latency every stage)
+        auto rd = [&](const lds_float* st, int kc, pcmx::f32x4(&a)[C::MT], pcmx::f32x4(&b)[4]) __attribute__((always_inline)) {
+            if constexpr (SCHED == 3) pin([&] { read(st, kc, a, b); }); else read(st, kc, a, b);
+        };
+        rd(cur, 1, fa1, fb1);
         mma(fa0, fb0, chunk_filler(0));
-        read(cur, 2, fa0, fb0);
+        rd(cur, 2, fa0, fb0);
         mma(fa1, fb1, chunk_filler(1));
-        read(cur, 3, fa1, fb1);
+        rd(cur, 3, fa1, fb1);
         mma(fa0, fb0, chunk_filler(2));
+        // SCHED 3: chunk 2's MFMAs stay above the barrier (they would sink below it and leave the barrier
+        // waiting on the chunk-3 reads just issued) ...
+        if constexpr (SCHED == 3) __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
-        if constexpr (WRITE) read(nxt, 0, fa0, fb0);
+        if constexpr (WRITE) rd(nxt, 0, fa0, fb0);
         mma(fa1, fb1, chunk_filler(3));
+        // ... and the stage ends with no LDS read pending (the next-stage reads completed under chunk 3's 64
+        // MFMAs), so the waitcnt pass need not guess across the loop back-edge (it emitted lgkmcnt(0) right
+        // after the next stage's first reads)
+        if constexpr (SCHED == 3) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
+            __builtin_amdgcn_sched_barrier(0);
+        }
     };
     int t = 0;
     for (; t + 2 < nk; ++t) stage(t, std::true_type{}, std::true_type{});
@@ -813,19 +840,18 @@ __global__ __launch_bounds__(CfgRS::kThreads, 1) void sgemm_rs_kernel(const floa
         }
 }
 
-template <int SCHED, bool PADA = false>
+template <int SCHED, bool PADA = false, class C = CfgRS>
 int launch_rs(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
               float beta, hipStream_t s) {
-    using C = CfgRS;
     if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
     if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return -1;
     // 32-bit buffer offsets: the block's A rows and the whole B panel must stay below 2 GiB
     if ((long long)C::BM * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31)) return -1;
     const int grid = (M / C::BM) * (N / C::BN);
     if (beta != 0.f)
-        sgemm_rs_kernel<true, SCHED, PADA><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_rs_kernel<true, SCHED, PADA, C><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     else
-        sgemm_rs_kernel<false, SCHED, PADA><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_rs_kernel<false, SCHED, PADA, C><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     return (int)hipGetLastError();
 }
 
@@ -1248,8 +1274,11 @@ extern "C" int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, 
         case 5: return launch1w<false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 7: return launch_rs<0>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 10: return launch_rs<2>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 14: return launch_rs<3>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 15: return launch_rs<3, false, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 16: return launch_rs<0, false, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 18: return launch_rs<2, false, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 11: return launch_rs<0, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 12: return launch_rs<1, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 8: return launch_rs16(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 13: return launch_rs16i(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         default: return -1;
@@ -1258,11 +1287,11 @@ extern "C" int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, 
 
 extern "C" int pcmx_sgemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
                               float alpha, float beta, hipStream_t s) {
-    // 256x256 tiles (register-staged, one wave per SIMD) when the grid fills the 256 CUs; otherwise the
-    // 128x128 two-waves-per-SIMD kernel (4x more tiles).
+    // 256x256 tiles (register-staged, 8 waves = two per SIMD, variant 16) when the grid fills the 256 CUs;
+    // otherwise the 128x128 two-waves-per-SIMD kernel (4x more tiles).
     const bool big_ok = (M % 256 == 0) && (N % 256 == 0) && (long long)(M / 256) * (N / 256) >= 192;
     if (big_ok) {
-        const int rc = pcmx_sgemm_f32_variant(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 7, s);
+        const int rc = pcmx_sgemm_f32_variant(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 16, s);
         if (rc != -1) return rc;  // -1: offsets exceed the 32-bit buffer range -> fall back
     }
     if (M % 256 == 0 && N % 256 == 0 && big_ok)

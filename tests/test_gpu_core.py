@@ -84,7 +84,7 @@ def test_scan_integer_exact(gpu):
     assert torch.equal(out.long(), torch.cumsum(x.long(), 0))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 10])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 8, 10, 11, 13, 14, 15, 16, 18])
 def test_sgemm_identity_asymmetric(gpu, variant):
     # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
     n = 256
@@ -94,6 +94,17 @@ def test_sgemm_identity_asymmetric(gpu, variant):
     assert torch.equal(c, b)
     c2 = ops.sgemm(b, a, variant=variant)
     assert torch.equal(c2, b)
+
+
+@pytest.mark.parametrize("variant", [7, 14, 15, 16, 18])
+def test_sgemm_register_staged_multitile_vs_fp64(gpu, variant):
+    # several tiles in both directions and 2+ LDS stages of prefetch: M != N != K
+    g = torch.Generator(device=gpu).manual_seed(variant)
+    a = torch.rand(768, 1280, device=gpu, generator=g) * 2 - 1
+    b = torch.rand(1280, 512, device=gpu, generator=g) * 2 - 1
+    c = ops.sgemm(a, b, variant=variant)
+    ref = a.double() @ b.double()
+    assert ((c.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
 @pytest.mark.parametrize("shape", [(256, 256, 256), (512, 768, 1024), (1024, 1024, 2048), (100, 70, 33), (1000, 1000, 1000)])
