@@ -5,13 +5,14 @@
 // MI355X design
 //  * Tiled local fixpoint, so one launch advances the front across a whole tile instead of one cell (the
 //    naive kernel of raycast.cu:534 needs one launch per BFS level: 249 launches, 61 ms at 512^3).
-//    2-D: a workgroup stages its tile plus a 1-cell halo in LDS and iterates Gauss-Seidel sweeps
-//    (`__syncthreads_or`). 3-D: BIT-PARALLEL one-wave tiles of 64x8x8 — a lane holds one 64-voxel row as
+//    2-D: BIT-PARALLEL one-wave 64x64 tiles (a lane holds a 64-pixel row word; Kogge-Stone closures along
+//    rows and, by shuffles, along columns), 4x4 tiles per workgroup exchanging borders through LDS. 3-D:
+//    BIT-PARALLEL one-wave tiles of 64x8x8 — a lane holds one 64-voxel row as
 //    a 64-bit mask, similarity to the x / y / z neighbours as link masks, and a sweep is a few 64-bit ops
 //    plus cross-lane shuffles (a front crosses a whole row per sweep; no LDS, no barriers): 0.73 ms per
 //    512^3 grow (the 32x8x8 LDS-tile version took 1.47 ms).
 //  * Active-tile worklist: a tile only runs if a face neighbour changed in the previous launch. 2-D:
-//    act_in -> act_out flags over the tile grid. 3-D (32k tiles at 512^3): a compacted device-built list
+//    act_in -> act_out flags over the block grid (self-cleaning, no memset between launches). 3-D (32k tiles at 512^3): a compacted device-built list
 //    walked by a persistent grid, so a launch costs the frontier, not a full-volume dispatch.
 //  * Halo cells are read-only inputs. That makes the same kernel the compute step of the distributed
 //    version: a rank's halo holds its neighbours' boundary after an RCCL exchange (parallel/region2d.py).
@@ -23,66 +24,172 @@
 namespace {
 
 // ----------------------------------------------------------------------------------------------- 2-D
-constexpr int kT2 = 64;            // tile interior edge
-constexpr int kE2 = kT2 + 2;       // with halo
-constexpr int kThreads2 = 256;
+// Bit-parallel: the padded (H+2) x (W+2) grid is held as 64-bit words (row y, word x = columns 64x..64x+63):
+// rb = region bits, hl = "pixel c is similar to c+1" links, vl = "pixel (y,c) is similar to (y+1,c)" links
+// (built once per grow by region2d_bits_prep_kernel). A wave owns a 64-row x 1-word tile (lane = row); a
+// 16-wave workgroup owns a 4 x 4 block of tiles (256 x 256 pixels) whose words it keeps in LDS. A sweep is a
+// Kogge-Stone closure along the row (6 shift/and steps each way: a front crosses any horizontal run in one
+// sweep) and along the column across lanes (6 shuffle steps each way), repeated to the tile fixpoint (wave
+// ballot, no barrier), then tiles exchange borders through LDS until the block is stable (one barrier per
+// round). Blocks exchange borders between launches; a block runs only if a neighbour's border changed.
+// Halo cells (row 0 / H+1, column 0 / W+1) are read-only seeds: nothing propagates INTO or THROUGH them.
+constexpr int kB2 = 4;                   // tiles per block edge
+constexpr int kWaves2 = kB2 * kB2;       // one wave per tile
+constexpr int kThreads2 = kWaves2 * 64;  // 1024
 
-// Arrays are padded: interior rows/cols 1..H / 1..W, pitch `ld` >= W+2.
-__global__ __launch_bounds__(kThreads2) void region2d_tile_kernel(const unsigned char* __restrict__ img,
-                                                                 unsigned char* __restrict__ region, int H, int W,
-                                                                 int ld, int thr, const int* __restrict__ act_in,
+typedef unsigned long long u64;
+
+__device__ __forceinline__ u64 shfl_up64(u64 v, int k) {
+    const int l = pcmx::lane_id();
+    const u64 t = __shfl_up(v, (unsigned)k, 64);
+    return l >= k ? t : 0ull;
+}
+__device__ __forceinline__ u64 shfl_down64(u64 v, int k) {
+    const int l = pcmx::lane_id();
+    const u64 t = __shfl_down(v, (unsigned)k, 64);
+    return l + k < 64 ? t : 0ull;
+}
+
+// interior bits of word x in row y: columns 1..W of rows 1..H
+__device__ __forceinline__ u64 interior_mask(int y, int x, int H, int W) {
+    if (y < 1 || y > H) return 0ull;
+    const int c0 = 64 * x, lo = c0 < 1 ? 1 - c0 : 0, hi = W - c0;  // bits lo..hi
+    if (hi < lo) return 0ull;
+    const u64 upto = hi >= 63 ? ~0ull : ((1ull << (hi + 1)) - 1);
+    return upto & (~0ull << lo);
+}
+
+// One wave per (row y, word x): lane = column bit. Builds rb/hl/vl with ballots.
+__global__ __launch_bounds__(256) void region2d_bits_prep_kernel(const unsigned char* __restrict__ img,
+                                                                const unsigned char* __restrict__ region, int R, int C,
+                                                                int ld, int nw, int thr, u64* __restrict__ rb,
+                                                                u64* __restrict__ hl, u64* __restrict__ vl) {
+    const long long wid = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (wid >= (long long)R * nw) return;
+    const int y = (int)(wid / nw), x = (int)(wid % nw);
+    const int c = 64 * x + pcmx::lane_id();
+    bool r = false, h = false, v = false;
+    if (c < C) {
+        const int a = img[(size_t)y * ld + c];
+        r = region[(size_t)y * ld + c] != 0;
+        if (c + 1 < C) h = abs(a - (int)img[(size_t)y * ld + c + 1]) < thr;
+        if (y + 1 < R) v = abs(a - (int)img[(size_t)(y + 1) * ld + c]) < thr;
+    }
+    const u64 br = __ballot(r), bh = __ballot(h), bv = __ballot(v);
+    if (pcmx::lane_id() == 0) rb[wid] = br, hl[wid] = bh, vl[wid] = bv;
+}
+
+// New interior bits back to the byte region (only 0 -> 1 writes).
+__global__ __launch_bounds__(256) void region2d_bits_store_kernel(unsigned char* __restrict__ region, int H, int W,
+                                                                 int ld, int nw, const u64* __restrict__ rb) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)H * W) return;
+    const int y = 1 + (int)(i / W), c = 1 + (int)(i % W);
+    if ((rb[(size_t)y * nw + (c >> 6)] >> (c & 63)) & 1ull) {
+        unsigned char* p = region + (size_t)y * ld + c;
+        if (!*p) *p = 1;
+    }
+}
+
+__global__ __launch_bounds__(kThreads2) void region2d_bits_kernel(u64* __restrict__ rb, const u64* __restrict__ hl,
+                                                                 const u64* __restrict__ vl, int R, int H, int W,
+                                                                 int nw, int* __restrict__ act_in,
                                                                  int* __restrict__ act_out, int* __restrict__ flag) {
-    const int tx = blockIdx.x, ty = blockIdx.y;
-    const int ntx = gridDim.x, nty = gridDim.y;
-    if (act_in && act_in[ty * ntx + tx] == 0) return;
-    __shared__ unsigned char simg[kE2][kE2 + 2];
-    __shared__ unsigned char sreg[kE2][kE2 + 2];
-    const int x0 = tx * kT2, y0 = ty * kT2;  // padded coords of the halo corner
-    for (int i = threadIdx.x; i < kE2 * kE2; i += kThreads2) {
-        const int ly = i / kE2, lx = i % kE2;
-        const int gy = y0 + ly, gx = x0 + lx;
-        const bool ok = gy <= H + 1 && gx <= W + 1;
-        simg[ly][lx] = ok ? img[(size_t)gy * ld + gx] : 0;
-        sreg[ly][lx] = ok ? region[(size_t)gy * ld + gx] : 0;
+    const int nbx = gridDim.x, bxi = blockIdx.x, byi = blockIdx.y, bid = byi * nbx + bxi;
+    if (act_in[bid] == 0) return;
+    __shared__ u64 sr[kB2 * 64][kB2];  // the block's region words, [row][word]
+    __shared__ int any_change;
+    const int lane = pcmx::lane_id(), wave = threadIdx.x >> 6;
+    const int wy = wave / kB2, wx = wave % kB2;
+    const int y = (byi * kB2 + wy) * 64 + lane, x = bxi * kB2 + wx;
+    const int ly = wy * 64 + lane;
+    const bool valid = y < R && x < nw;
+    const size_t at = (size_t)y * nw + x;
+    const u64 im = valid ? interior_mask(y, x, H, W) : 0ull;
+    const u64 h = valid ? hl[at] : 0ull;
+    const u64 v = valid ? vl[at] : 0ull;                                  // row y <-> y+1
+    u64 vup = shfl_up64(v, 1);                                              // row y-1 <-> y
+    if (lane == 0 && valid && y > 0) vup = vl[at - nw];
+    const u64 hleft = (valid && x > 0) ? hl[at - 1] : 0ull;                 // bit 63: column 64x-1 <-> 64x
+    // receive masks (only interior cells receive)
+    const u64 E = (h << 1) & im;                                            // x <- x-1
+    const u64 Wm = h & im;                                                  // x <- x+1 (bit 63: from next word)
+    const u64 D = vup & im;                                                 // from the row above
+    const u64 U = v & im;                                                   // from the row below
+    const bool in_l = (hleft >> 63) & im & 1ull, in_r = (h >> 63) & (im >> 63) & 1ull;
+    // words outside the block (fixed during this launch): left/right neighbours per row, rows above/below
+    const bool bl = wx == 0, br = wx == kB2 - 1, bt = wy == 0, bb = wy == kB2 - 1;
+    const u64 ext_l = (bl && valid && x > 0) ? rb[at - 1] : 0ull;
+    const u64 ext_r = (br && valid && x + 1 < nw) ? rb[at + 1] : 0ull;
+    const u64 ext_t = (bt && lane == 0 && valid && y > 0) ? rb[at - nw] : 0ull;
+    const u64 ext_b = (bb && lane == 63 && x < nw && y + 1 < R) ? rb[at + nw] : 0ull;
+    const u64 r0 = valid ? rb[at] : 0ull;
+    u64 r = r0;
+    sr[ly][wx] = r;
+    __syncthreads();
+    for (;;) {
+        // seeds from the 4 neighbour tiles (LDS inside the block, launch-start values outside)
+        const u64 nl = bl ? ext_l : sr[ly][wx - 1];
+        const u64 nr = br ? ext_r : sr[ly][wx + 1];
+        u64 nt = 0ull, nb = 0ull;
+        if (lane == 0) nt = bt ? ext_t : sr[ly - 1][wx];
+        if (lane == 63) nb = bb ? ext_b : sr[ly + 1][wx];
+        u64 g = r | (in_l && (nl >> 63) ? 1ull : 0ull) | (in_r && (nr & 1ull) ? (1ull << 63) : 0ull) | (nt & D) | (nb & U);
+        const u64 start = r;
+        for (;;) {
+            const u64 before = g;
+            u64 p = E;  // along the row, towards higher bits
+            g |= (g << 1) & p, p &= p << 1;
+            g |= (g << 2) & p, p &= p << 2;
+            g |= (g << 4) & p, p &= p << 4;
+            g |= (g << 8) & p, p &= p << 8;
+            g |= (g << 16) & p, p &= p << 16;
+            g |= (g << 32) & p;
+            p = Wm & ~(1ull << 63);  // towards lower bits (bit 63's link leads out of the word)
+            g |= (g >> 1) & p, p &= p >> 1;
+            g |= (g >> 2) & p, p &= p >> 2;
+            g |= (g >> 4) & p, p &= p >> 4;
+            g |= (g >> 8) & p, p &= p >> 8;
+            g |= (g >> 16) & p, p &= p >> 16;
+            g |= (g >> 32) & p;
+            p = D;  // down the column (across lanes)
+#pragma unroll
+            for (int k = 1; k < 64; k <<= 1) {
+                g |= shfl_up64(g, k) & p;
+                p &= shfl_up64(p, k);
+            }
+            p = U;  // up the column
+#pragma unroll
+            for (int k = 1; k < 64; k <<= 1) {
+                g |= shfl_down64(g, k) & p;
+                p &= shfl_down64(p, k);
+            }
+            if (!__any(g != before)) break;
+        }
+        r = g;
+        const int changed = r != start;
+        __syncthreads();  // everyone has read the neighbours' words of this round
+        sr[ly][wx] = r;
+        if (!__syncthreads_or(changed)) break;
+    }
+    // publish: changed words, then activate the neighbour blocks whose shared border changed
+    const u64 diff = r ^ r0;
+    if (valid && diff) rb[at] = r;
+    const bool cl = bl && __any(diff & 1ull), cr = br && __any(diff >> 63), ct = bt && __any(lane == 0 && diff),
+               cb = bb && __any(lane == 63 && diff), cany = __any(diff != 0ull);
+    if (threadIdx.x == 0) any_change = 0;
+    __syncthreads();
+    if (lane == 0) {
+        if (cany) atomicOr(&any_change, 1);
+        if (cl && bxi > 0) act_out[bid - 1] = 1;
+        if (cr && bxi + 1 < nbx) act_out[bid + 1] = 1;
+        if (ct && byi > 0) act_out[bid - nbx] = 1;
+        if (cb && byi + 1 < (int)gridDim.y) act_out[bid + nbx] = 1;
     }
     __syncthreads();
-    const int lx = 1 + (threadIdx.x & 63);
-    const int rowgrp = threadIdx.x >> 6;  // 4 row groups, 16 rows each
-    const bool col_in = x0 + lx <= W;
-    unsigned long long mine = 0;  // bit k: this thread set row 1 + rowgrp + 4k
-    bool any_block = false;
-    while (true) {
-        int changed = 0;
-#pragma unroll
-        for (int k = 0; k < kT2 / 4; ++k) {
-            const int ly = 1 + rowgrp + 4 * k;
-            if (!col_in || y0 + ly > H || sreg[ly][lx]) continue;
-            const int v = simg[ly][lx];
-            const bool grow = (sreg[ly - 1][lx] && abs(v - (int)simg[ly - 1][lx]) < thr) ||
-                              (sreg[ly + 1][lx] && abs(v - (int)simg[ly + 1][lx]) < thr) ||
-                              (sreg[ly][lx - 1] && abs(v - (int)simg[ly][lx - 1]) < thr) ||
-                              (sreg[ly][lx + 1] && abs(v - (int)simg[ly][lx + 1]) < thr);
-            if (grow) {
-                sreg[ly][lx] = 1;
-                mine |= 1ull << k;
-                changed = 1;
-            }
-        }
-        if (!__syncthreads_or(changed)) break;
-        any_block = true;
-    }
-    if (mine) {
-#pragma unroll
-        for (int k = 0; k < kT2 / 4; ++k)
-            if (mine & (1ull << k)) region[(size_t)(y0 + 1 + rowgrp + 4 * k) * ld + x0 + lx] = 1;
-    }
-    if (any_block && threadIdx.x == 0) {
-        *flag = 1;
-        act_out[ty * ntx + tx] = 1;
-        if (tx > 0) act_out[ty * ntx + tx - 1] = 1;
-        if (tx + 1 < ntx) act_out[ty * ntx + tx + 1] = 1;
-        if (ty > 0) act_out[(ty - 1) * ntx + tx] = 1;
-        if (ty + 1 < nty) act_out[(ty + 1) * ntx + tx] = 1;
+    if (threadIdx.x == 0) {
+        act_in[bid] = 0;  // self-cleaning: this array is the next-but-one launch's act_out
+        if (any_change) *flag = 1;  // (the block itself is at its fixpoint: only neighbours re-activate it)
     }
 }
 
@@ -360,24 +467,50 @@ __global__ __launch_bounds__(256) void region3d_step_kernel(const unsigned char*
     }
 }
 
-struct ActWs {
-    int flag;
-    int pad[3];
-};
+}  // namespace
 
-// Runs tile launches until a batch of `batch` launches changes nothing. Blocks the host once per batch.
-template <class Launch>
-int run_active_loop(Launch launch, long long ntiles, void* ws, int batch, int max_launches, hipStream_t s,
-                    int* launches_out) {
+namespace {
+struct Region2dGeom {
+    int R, C, nw, nbx, nby;
+    long long words, nblocks;
+};
+Region2dGeom region2d_geom(int H, int W) {
+    Region2dGeom g;
+    g.R = H + 2, g.C = W + 2, g.nw = (g.C + 63) / 64;
+    g.nbx = (g.nw + kB2 - 1) / kB2, g.nby = ((g.R + 63) / 64 + kB2 - 1) / kB2;
+    g.words = (long long)g.R * g.nw, g.nblocks = (long long)g.nbx * g.nby;
+    return g;
+}
+}  // namespace
+
+extern "C" long long pcmx_region2d_workspace_bytes(int H, int W) {
+    const Region2dGeom g = region2d_geom(H, W);
+    return 64 + ((2 * g.nblocks * 4 + 7) / 8) * 8 + 3 * g.words * 8;
+}
+
+// ws: [flag | act0 | act1 | rb | hl | vl]. Host reads the changed flag once per `batch` launches.
+extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* region, int H, int W, int ld, int thr,
+                                  void* ws, int batch, int max_launches, hipStream_t s, int* launches_out) {
+    if (H <= 0 || W <= 0 || ld < W + 2 || !ws || ((uintptr_t)ws & 7)) return -1;
+    const Region2dGeom g = region2d_geom(H, W);
     int* flag = reinterpret_cast<int*>(ws);
-    int* act[2] = {flag + 4, flag + 4 + ntiles};
-    PCMX_HIP_RET(hipMemsetAsync(act[0], 0xff, ntiles * sizeof(int), s));  // every tile active at first
+    int* act[2] = {flag + 16, flag + 16 + g.nblocks};
+    u64* rb = reinterpret_cast<u64*>((char*)ws + 64 + ((2 * g.nblocks * 4 + 7) / 8) * 8);
+    u64* hl = rb + g.words;
+    u64* vl = hl + g.words;
+    const long long prep_threads = g.words * 64;
+    region2d_bits_prep_kernel<<<(unsigned)((prep_threads + 255) / 256), 256, 0, s>>>(img, region, g.R, g.C, ld, g.nw,
+                                                                                    thr, rb, hl, vl);
+    PCMX_HIP_RET(hipGetLastError());
+    PCMX_HIP_RET(hipMemsetAsync(act[0], 0x01, g.nblocks * sizeof(int), s));  // every block runs first (nonzero)
+    PCMX_HIP_RET(hipMemsetAsync(act[1], 0, g.nblocks * sizeof(int), s));
+    const dim3 grid(g.nbx, g.nby);
+    if (batch < 1) batch = 4;
     int launches = 0, cur = 0;
     while (launches < max_launches) {
         PCMX_HIP_RET(hipMemsetAsync(flag, 0, sizeof(int), s));
         for (int b = 0; b < batch && launches < max_launches; ++b, ++launches) {
-            PCMX_HIP_RET(hipMemsetAsync(act[cur ^ 1], 0, ntiles * sizeof(int), s));
-            launch(act[cur], act[cur ^ 1], flag);
+            region2d_bits_kernel<<<grid, kThreads2, 0, s>>>(rb, hl, vl, g.R, H, W, g.nw, act[cur], act[cur ^ 1], flag);
             PCMX_HIP_RET(hipGetLastError());
             cur ^= 1;
         }
@@ -386,25 +519,10 @@ int run_active_loop(Launch launch, long long ntiles, void* ws, int batch, int ma
         PCMX_HIP_RET(hipStreamSynchronize(s));
         if (!h) break;
     }
+    region2d_bits_store_kernel<<<(unsigned)(((long long)H * W + 255) / 256), 256, 0, s>>>(region, H, W, ld, g.nw, rb);
+    PCMX_HIP_RET(hipGetLastError());
     if (launches_out) *launches_out = launches;
     return 0;
-}
-}  // namespace
-
-extern "C" long long pcmx_region2d_workspace_bytes(int H, int W) {
-    const long long nt = (long long)((W + kT2 - 1) / kT2) * ((H + kT2 - 1) / kT2);
-    return 16 + 2 * nt * 4;
-}
-
-extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* region, int H, int W, int ld, int thr,
-                                  void* ws, int batch, int max_launches, hipStream_t s, int* launches_out) {
-    if (H <= 0 || W <= 0 || ld < W + 2 || !ws) return -1;
-    dim3 grid((W + kT2 - 1) / kT2, (H + kT2 - 1) / kT2);
-    const long long nt = (long long)grid.x * grid.y;
-    auto launch = [&](const int* ain, int* aout, int* flag) {
-        region2d_tile_kernel<<<grid, kThreads2, 0, s>>>(img, region, H, W, ld, thr, ain, aout, flag);
-    };
-    return run_active_loop(launch, nt, ws, batch < 1 ? 4 : batch, max_launches, s, launches_out);
 }
 
 extern "C" long long pcmx_region3d_workspace_bytes(int dim) {

@@ -218,8 +218,39 @@ class Histeq(Workload):
         return float(self.img.numel())
 
 
+class Region2D(Workload):
+    """The reference's MPI region-growing app on one device: corner-seeded 4-connected flood fill with
+    |a-b| < 2 over pic1.bmp (ref 2-mpi-region-growing/region.c:493-533, 582-604). side > 512 tiles pic1 to
+    side x side (longer propagation paths, more tiles); a step regrows from the seeds."""
+
+    def __init__(self, ctx, side=512, **_):
+        super().__init__(ctx, {"side": side}, "region2d", "Mpix/s")
+        from pathlib import Path
+
+        from ..utils import bmp
+
+        pic = torch.from_numpy(bmp.read(Path(__file__).resolve().parents[2] / "assets" / "pic1.bmp").copy())
+        reps = max(1, -(-side // pic.shape[0]))
+        self.img = pic.repeat(reps, reps)[:side, :side].contiguous().to(ctx.device)
+        self.side = side
+
+    def step(self):
+        self.region = ops.region2d(self.img)
+
+    def work_per_step(self):
+        return float(self.img.numel())
+
+    def scale(self):
+        return 1e6
+
+    def check(self):
+        if self.side != 512:
+            return {"region_pixels": int(self.region.sum())}
+        return {"region_pixels": int(self.region.sum()), "golden_pixels": 64420}
+
+
 WORKLOADS = {"sgemm": Sgemm, "reduce": Reduce, "scan": Scan, "stencil": Stencil, "spmv": SpMV,
-             "region3d": Region3D, "raycast": Raycast, "histeq": Histeq}
+             "region3d": Region3D, "raycast": Raycast, "histeq": Histeq, "region2d": Region2D}
 
 
 def build_workload(name: str, ctx: Context, **cfg) -> Workload:
