@@ -72,7 +72,8 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ in, long lon
 template <int R, int W>
 __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float* __restrict__ out, long long n, long long tile,
                                             f32x4 (&v)[R], long long next, f32x4 (&vn)[R], long long ntiles, int exclusive,
-                                            float init, ScanWs* ws, float* s_wave_tot, float* s_prefix) {
+                                            float init, ScanWs* ws, float* s_wave_tot, float* s_prefix,
+                                            unsigned* s_next) {
     unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
     const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
     // ---- in-wave scan: per row, lane-local prefix, then a wave scan of the lane totals
@@ -103,6 +104,12 @@ __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float*
                            __HIP_MEMORY_SCOPE_AGENT);
     // ---- the next tile's loads go out now and overlap the look-back below
     if (next < ntiles) load_tile<R, W>(in, n, next, vn);
+    // ---- the ticket for the tile after `next` is taken HERE, before this tile's stores: vmcnt retires in
+    //      order, so an atomic issued after the 16 stores (the previous schedule) made wave 0 - and through the
+    //      next barrier the whole block - wait for the stores to complete on every tile. Issued before the
+    //      look-back, its return is covered by the poll's wait; published by the barrier below.
+    unsigned ticket = 0u;
+    if (threadIdx.x == 0) ticket = atomicAdd(&ws->ticket, 1u);
 
     // ---- wave 0: decoupled look-back over the predecessors' {flag, value} granules
     if (wave == 0) {
@@ -143,6 +150,7 @@ __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float*
         }
         if (lane == 0) *s_prefix = init + prefix;
     }
+    if (threadIdx.x == 0) *s_next = ticket;
     __syncthreads();
     const float off = *s_prefix + wexcl;
 
@@ -182,23 +190,23 @@ __global__ __launch_bounds__(W * kWave) void scan_persistent_kernel(const float*
     __shared__ unsigned s_tile[2];
     const float init = init_dev ? *init_dev : 0.f;
     f32x4 va[R], vb[R];
-    if (threadIdx.x == 0) s_tile[0] = atomicAdd(&ws->ticket, 1u);
+    if (threadIdx.x == 0) {
+        s_tile[0] = atomicAdd(&ws->ticket, 1u);
+        s_tile[1] = atomicAdd(&ws->ticket, 1u);
+    }
     __syncthreads();
-    long long ta = s_tile[0];
+    long long ta = s_tile[0], tb = s_tile[1];
     if (ta >= ntiles) return;
     load_tile<R, W>(in, n, ta, va);
-    // unrolled by two so both register buffers are statically named (every exit is block-uniform)
+    // unrolled by two so both register buffers are statically named (every exit is block-uniform); each
+    // finish_tile takes the ticket two tiles ahead and publishes it in s_tile[slot] by its last barrier
     while (true) {
-        if (threadIdx.x == 0) s_tile[1] = atomicAdd(&ws->ticket, 1u);
-        __syncthreads();
-        const long long tb = s_tile[1];
-        finish_tile<R, W>(in, out, n, ta, va, tb, vb, ntiles, exclusive, init, ws, s_wave_tot[0], &s_prefix[0]);
+        finish_tile<R, W>(in, out, n, ta, va, tb, vb, ntiles, exclusive, init, ws, s_wave_tot[0], &s_prefix[0], &s_tile[0]);
         if (tb >= ntiles) break;
-        if (threadIdx.x == 0) s_tile[0] = atomicAdd(&ws->ticket, 1u);
-        __syncthreads();
         ta = s_tile[0];
-        finish_tile<R, W>(in, out, n, tb, vb, ta, va, ntiles, exclusive, init, ws, s_wave_tot[1], &s_prefix[1]);
+        finish_tile<R, W>(in, out, n, tb, vb, ta, va, ntiles, exclusive, init, ws, s_wave_tot[1], &s_prefix[1], &s_tile[1]);
         if (ta >= ntiles) break;
+        tb = s_tile[1];
     }
 }
 
