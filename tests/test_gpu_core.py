@@ -70,6 +70,22 @@ def test_scan(gpu, n, exclusive):
     assert (out.double() - ref).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_scan_many_tiles_per_block(gpu, exclusive):
+    # ~1221 128-KiB tiles over <= 256 persistent blocks: every block walks several tickets (taken two tiles
+    # ahead), and the last tile is partial with a straddling f32x4 row
+    n = 40_000_007
+    x = torch.randint(0, 4, (n,), device=gpu).float()
+    ref = torch.cumsum(x.long(), 0)
+    if exclusive:
+        ref = torch.cat([ref.new_zeros(1), ref[:-1]])
+    out = ops.scan(x, exclusive=exclusive)
+    # integer inputs: exact while partial sums stay below 2^24, then f32 rounding of the carried prefix
+    err = (out.double() - ref.double()).abs() / ref.double().clamp_min(1.0)
+    assert err.max().item() < 2e-5  # <= ~1 rounding of the carried prefix per tile hop
+    assert torch.equal(out[: 1 << 20].long(), ref[: 1 << 20])
+
+
 def test_scan_with_device_init(gpu):
     x = torch.ones(50_000, device=gpu)
     init = torch.tensor([10.0], device=gpu)
