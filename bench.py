@@ -1,16 +1,26 @@
 #!/usr/bin/env python3
-"""Headline benchmark: "TFLOPS SGEMM 8192^2 + GB/s reduce 1e9 f32, at 1/2/4/8 MI355X" (BASELINE.json).
+"""Headline benchmark: "TFLOPS SGEMM 8192^2 + GB/s reduce 1e9 f32, at 1/2/4/8 MI355X" (BASELINE.json), plus
+every other BASELINE.json north-star config measured at the same N in the same job.
 
-One process per GPU (torchrun / torch.distributed.run, RCCL over xGMI for N>1), weak scaling: every rank
-owns its own 8192x8192 fp32 operands and its own 1e9-element f32 array (4 GB, HBM-resident, generated on
-device). A timed SGEMM step is one C = A @ B on the gfx950 MFMA kernel (exact fp32); a timed reduce step
-is the local HBM-bound reduction kernel followed by an RCCL all-reduce of the partial, so every rank ends
-the step holding the global sum of N x 1e9 values.
+One process per GPU (torchrun / torch.distributed.run, RCCL over xGMI for N > 1). Sections, each with its
+own correctness check, all timed the same way (W untimed warm-up steps, then EXACTLY K timed steps bracketed
+by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harness.py):
 
-Contract (driver): `python bench.py --gpus N --steps K --warmup W`; W untimed warm-up steps, then EXACTLY K
-timed steps bracketed by barrier + torch.cuda.synchronize() on both sides; the max over ranks is reported;
-rank 0 prints ONE JSON line. `value` = whole-job SGEMM TFLOPS (sum over GPUs); the reduce/scan numbers are
-extra fields of the same line.
+  sgemm    (value) 8192^3 fp32 C = A @ B per GPU on the MFMA kernel, weak scaling; fp64 spot check; the
+           hipBLASLt torch.matmul of the same operands is timed alongside for reference
+  reduce   global sum, local HBM reduce + one-scalar RCCL all-reduce: weak (1e9 f32 per GPU) and strong
+           (1e9 f32 in total, 1e9/N per GPU); fp64 check
+  scan     global inclusive prefix sum over the rank-ordered concatenation (reduce-then-scan): weak and
+           strong like reduce; fp64 check of the first 2^20 outputs of every rank incl. its rank offset
+  stencil  16384^2 bf16 5-point stencil, strong scaling: row slabs, 4 fused updates per kernel and one 4-row
+           halo exchange per neighbour overlapped with the interior update; bit-exact check of the same
+           distributed path against the single-step oracle
+  spmv     power-law CSR, 1e8 nnz / 1e7 rows, strong scaling: nnz-balanced row blocks, XCD-sliced kernel,
+           chunked all-gather of y overlapped with the product; fp64 check of every rank's rows
+  (N > 1)  256 MiB RCCL all-reduce bus bandwidth
+
+rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra
+fields of the same line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
 """
 from __future__ import annotations
 
@@ -18,178 +28,167 @@ import argparse
 import json
 import os
 import sys
-import time
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "TFLOPS SGEMM 8192^2 + GB/s reduce 1e9 f32, at 1/2/4/8 MI355X"
+SECTIONS = ("sgemm", "reduce", "scan", "stencil", "spmv")
 
 
-def parse():
-    ap = argparse.ArgumentParser(description=__doc__)
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=8192, help="SGEMM M=N=K")
-    ap.add_argument("--reduce-n", type=float, default=1e9, help="f32 elements reduced per GPU per step")
-    ap.add_argument("--no-scan", action="store_true", help="skip the extra prefix-scan measurement")
+    ap.add_argument("--reduce-n", type=float, default=1e9, help="f32 elements (per GPU weak, in total strong)")
+    ap.add_argument("--stencil-n", type=int, default=16384)
+    ap.add_argument("--stencil-fuse", type=int, default=4)
+    ap.add_argument("--spmv-rows", type=float, default=1e7)
+    ap.add_argument("--spmv-nnz", type=float, default=1e8)
+    ap.add_argument("--spmv-chunks", type=int, default=0, help="all-gather pipeline depth (0: 1 at N=1, else 4)")
+    ap.add_argument("--sections", default=",".join(SECTIONS), help="comma list out of " + ",".join(SECTIONS))
     ap.add_argument("--no-ref", action="store_true", help="skip the torch.matmul (hipBLASLt) reference timing")
-    return ap.parse_args()
+    ap.add_argument("--small", action="store_true", help="tiny sizes (CPU/gloo rehearsal)")
+    ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")
+    a = ap.parse_args(argv)
+    if a.small:
+        a.size, a.reduce_n, a.stencil_n, a.spmv_rows, a.spmv_nnz = 256, 1e5, 256, 2e4, 2e5
+    return a
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def _r(v, nd=4):
+    return None if v is None else round(float(v), nd)
+
+
+def main(argv=None):
+    args = parse(argv)
+    from parallel_c_programs_amd import ops
+    from parallel_c_programs_amd.models import workloads as W
+    from parallel_c_programs_amd.parallel import finalize, init
+    from parallel_c_programs_amd.utils.harness import timed
+
+    ctx = init(device=args.device)
+    world, rank, dev = ctx.world, ctx.rank, ctx.device
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # noqa: F811
+    if dev.type == "cuda":
+        from parallel_c_programs_amd._native import ops as native_ops
 
-        dist.init_process_group("nccl", device_id=dev)
+        native_ops()  # the HIP extension must load: no silent fallback on a GPU box
+    sections = [s for s in args.sections.split(",") if s]
+    K, Wm = args.steps, args.warmup
+    out = {}
 
-    from parallel_c_programs_amd import ops
-    from parallel_c_programs_amd._native import ops as native_ops
+    def free():
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
 
-    native_ops()  # the HIP extension must load: no silent fallback on a GPU box
+    def log(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def timed(step_fn, steps, warmup):
-        for _ in range(warmup):
-            step_fn()
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step_fn()
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        if dist is not None:
-            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        return dt.item()
-
+    # ---- SGEMM (headline value): weak scaling, 8192^3 per GPU
     n = args.size
-    a = torch.empty(n, n, device=dev)
-    b = torch.empty(n, n, device=dev)
-    ops.rand_uniform_(a, 1000 + rank, -1.0, 1.0)
-    ops.rand_uniform_(b, 2000 + rank, -1.0, 1.0)
-    c = torch.empty(n, n, device=dev)
+    tflops = ms_gemm = None
+    if "sgemm" in sections:
+        g = W.Sgemm(ctx, n=n)
+        t = timed(ctx, g.step, K, Wm)
+        rep = g.report(t, K)
+        tflops, ms_gemm = rep["value"], rep["ms_per_step"]
+        out["sgemm_tflops_per_gpu"] = _r(tflops / world, 3)
+        out["sgemm_max_rel_err_vs_fp64"] = ctx.max_over_ranks(g.check()["max_rel_err_vs_fp64"])
+        if not args.no_ref and dev.type == "cuda":
+            kr = max(3, K // 2)
+            t_ref = timed(ctx, lambda: torch.matmul(g.a, g.b, out=g.c), kr, 1)
+            out["hipblaslt_torch_matmul_tflops"] = _r(world * g.work_per_step() * kr / t_ref / 1e12, 3)
+        del g
+        free()
+        log(f"sgemm {tflops:.1f} TFLOPS")
 
-    def gemm_step():
-        ops.sgemm_out(a, b, c)
-
-    t_gemm = timed(gemm_step, args.steps, args.warmup)
-    flop = 2.0 * n * n * n
-    ms_gemm = 1e3 * t_gemm / args.steps
-    tflops_total = world * flop * args.steps / t_gemm / 1e12
-
-    # correctness spot check of the timed kernel (a few rows against fp64)
-    rows = torch.arange(0, n, max(1, n // 8), device=dev)
-    ref = a[rows].double() @ b.double()
-    rel_err = ((c[rows].double() - ref).abs().max() / ref.abs().max()).item()
-
-    ref_tflops = None
-    if not args.no_ref:
-        t_ref = timed(lambda: torch.matmul(a, b, out=c), max(3, args.steps // 2), 1)
-        ref_tflops = world * flop * max(3, args.steps // 2) / t_ref / 1e12
-    del a, b, c, ref
-    torch.cuda.empty_cache()
-
-    # ---- global reduction: local HBM reduce + RCCL all-reduce of the partial (every rank gets the sum)
+    # ---- reduce / scan: weak (rn per GPU) and strong (rn in total); identical runs at N = 1
     rn = int(args.reduce_n)
-    x = torch.empty(rn, device=dev)
-    ops.rand_uniform_(x, 3000 + rank, 0.0, 1.0)
-    total = torch.zeros((), device=dev)
+    for name, cls in (("reduce", W.Reduce), ("scan", W.Scan)):
+        if name not in sections:
+            continue
+        for mode, per_rank in (("weak", rn), ("strong", -(-rn // world))):
+            if mode == "strong" and world == 1:
+                for k in ("gbps", "ms_per_step", "rel_err_vs_fp64"):
+                    out[f"{name}_strong_{k}"] = out[f"{name}_weak_{k}"]
+                continue
+            w = cls(ctx, n=per_rank)
+            t = timed(ctx, w.step, K, Wm)
+            rep = w.report(t, K)
+            out[f"{name}_{mode}_gbps"] = _r(rep["value"], 1)
+            out[f"{name}_{mode}_ms_per_step"] = _r(rep["ms_per_step"])
+            out[f"{name}_{mode}_rel_err_vs_fp64"] = ctx.max_over_ranks(w.check()["rel_err_vs_fp64"])
+            del w
+            free()
+        log(f"{name} weak {out[name + '_weak_gbps']} GB/s, strong {out[name + '_strong_gbps']} GB/s")
 
-    def reduce_step():
-        s = ops.reduce(x, "sum")
-        if dist is not None:
-            dist.all_reduce(s)
-        total.copy_(s)
+    # ---- stencil 16384^2 bf16, strong scaling over row slabs with the overlapped fused halo exchange
+    if "stencil" in sections:
+        s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse)
+        t = timed(ctx, s.step, K, Wm)
+        rep = s.report(t, K)
+        chk = s.check()
+        out.update({"stencil_glups": _r(rep["value"], 1), "stencil_ms_per_step": _r(rep["ms_per_step"]),
+                    "stencil_updates_per_step": s.slab.fuse,
+                    "stencil_bit_exact": chk["bit_exact_vs_single_step_oracle"], "stencil_finite": chk["finite"]})
+        del s
+        free()
+        log(f"stencil {out['stencil_glups']} GLUP/s")
 
-    t_red = timed(reduce_step, args.steps, args.warmup)
-    red_gbps = world * 4.0 * rn * args.steps / t_red / 1e9
-    expect = 0.5 * rn * world
-    red_rel = abs(total.item() - expect) / expect  # uniform[0,1) mean 0.5 (statistical check)
+    # ---- SpMV 1e8-nnz power-law graph, strong scaling
+    if "spmv" in sections:
+        sp = W.SpMV(ctx, n_rows=int(args.spmv_rows), nnz=int(args.spmv_nnz), chunks=args.spmv_chunks)
+        t = timed(ctx, sp.step, K, Wm)
+        rep = sp.report(t, K)
+        out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
+                    "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks,
+                    "spmv_max_rel_err_vs_fp64": sp.check()["max_rel_err_vs_fp64"]})
+        del sp
+        free()
+        log(f"spmv {out['spmv_gflops']} GFLOP/s")
 
-    scan_gbps = None
-    if not args.no_scan:
-        y = torch.empty_like(x)
-        before = torch.zeros(1, device=dev)
+    # ---- RCCL all-reduce bus bandwidth over xGMI (N > 1)
+    if ctx.distributed and dev.type == "cuda":
+        import torch.distributed as dist
 
-        def scan_step():
-            # global prefix sum over the rank-ordered concatenation: N > 1 reduce-then-scan (local HBM reduce,
-            # RCCL all-gather of the N totals, single-pass scan seeded with the lower ranks' sum)
-            if dist is None:
-                native_ops().scan_out(x, y, False, None)
-                return
-            tot = ops.reduce(x, "sum").reshape(1)
-            tots = torch.empty(world, device=dev)
-            dist.all_gather_into_tensor(tots, tot)
-            before.copy_(tots[:rank].sum().reshape(1))
-            native_ops().scan_out(x, y, False, before)
-
-        t_scan = timed(scan_step, max(2, args.steps // 2), 1)
-        scan_gbps = world * 8.0 * rn * max(2, args.steps // 2) / t_scan / 1e9
-        del y
-
-    # vector all-reduce bandwidth over RCCL/xGMI (N > 1): 256 MiB of f32 per rank, ring bus bandwidth
-    ar_busbw = None
-    if dist is not None:
-        del x
-        torch.cuda.empty_cache()
         v = torch.ones(64 << 20, device=dev)
-        ar_steps = max(3, args.steps // 2)
-        t_ar = timed(lambda: dist.all_reduce(v), ar_steps, 1)
-        ar_busbw = v.numel() * 4 * 2 * (world - 1) / world * ar_steps / t_ar / 1e9
+        kr = max(3, K // 2)
+        t_ar = timed(ctx, lambda: dist.all_reduce(v), kr, 1)
+        out["allreduce_256MiB_busbw_gbps"] = _r(v.numel() * 4 * 2 * (world - 1) / world * kr / t_ar / 1e9, 1)
         del v
 
     if rank == 0:
-        out = {
+        line = {
             "metric": METRIC,
-            "value": round(tflops_total, 3),
+            "value": _r(tflops, 3),
             "unit": "TFLOPS",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_gemm, 4),
+            "steps": K,
+            "warmup": Wm,
+            "ms_per_step": _r(ms_gemm),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (uniform[-1,1) fp32 operands generated on device)",
+            "data": "synthetic (uniform random operands generated on device; power-law CSR generated per rank)",
             "config": {
-                "model": f"SGEMM {n}x{n}x{n} fp32 (v_mfma_f32_32x32x2_f32) + global reduce {rn:.0e} f32/GPU",
+                "model": f"SGEMM {n}x{n}x{n} fp32 (v_mfma_f32_32x32x2_f32) per GPU + global reduce/scan "
+                         f"{rn:.0e} f32 + stencil {args.stencil_n}^2 bf16 + SpMV {args.spmv_nnz:.0e} nnz",
                 "global_batch": world,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
             },
-            "sgemm_tflops_per_gpu": round(tflops_total / world, 3),
-            "sgemm_max_rel_err_vs_fp64": rel_err,
-            "hipblaslt_torch_matmul_tflops": None if ref_tflops is None else round(ref_tflops, 3),
-            "reduce_gbps": round(red_gbps, 1),
-            "reduce_ms_per_step": round(1e3 * t_red / args.steps, 4),
-            "reduce_elements_per_gpu": rn,
-            "reduce_rel_dev_from_expectation": red_rel,
-            "scan_gbps": None if scan_gbps is None else round(scan_gbps, 1),
-            "allreduce_256MiB_busbw_gbps": None if ar_busbw is None else round(ar_busbw, 1),
+            "device": dev.type,
+            **out,
         }
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+        print(json.dumps(line), flush=True)
+    finalize(ctx)
 
 
 if __name__ == "__main__":

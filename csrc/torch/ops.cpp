@@ -350,7 +350,7 @@ at::Tensor spmv_csr(const at::Tensor& row_ptr, const at::Tensor& col, const at::
 // slice item0[n_slices + 1]; ypart [n_slices * n_rows] and extra [n_items] are caller-owned scratch.
 at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::Tensor& val, const at::Tensor& x,
                        const at::Tensor& items, const at::Tensor& fix, const at::Tensor& meta, at::Tensor ypart,
-                       at::Tensor extra, int64_t n_rows) {
+                       at::Tensor extra, int64_t n_rows, const c10::optional<at::Tensor>& out) {
     check_gpu(lrow, "lrow", at::kShort), check_gpu(col, "col", at::kInt), check_gpu(val, "val", at::kFloat);
     check_gpu(x, "x", at::kFloat), check_gpu(items, "items", at::kLong), check_gpu(fix, "fix", at::kInt);
     check_gpu(ypart, "ypart", at::kFloat), check_gpu(extra, "extra", at::kFloat);
@@ -366,7 +366,15 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
     for (int64_t k = 0; k < S; ++k)
         TORCH_CHECK(m[k] >= 0 && m[k] <= col.numel() && m[S + k] <= m[S + k + 1], "spmv_sliced: meta");
     const at::DeviceGuard g(val.device());
-    auto y = at::empty({n_rows}, val.options());
+    at::Tensor y;
+    if (out.has_value()) {
+        y = *out;
+        check_gpu(y, "out", at::kFloat);
+        TORCH_CHECK(y.is_contiguous() && y.numel() >= n_rows && y.device() == val.device(),
+                    "spmv_sliced: out must be a contiguous float32 tensor of >= n_rows elements on val's device");
+    } else {
+        y = at::empty({n_rows}, val.options());
+    }
     check_rc(pcmx_spmv_sliced(reinterpret_cast<const unsigned short*>(lrow.data_ptr<int16_t>()), col.data_ptr<int>(),
                               val.data_ptr<float>(), x.data_ptr<float>(), ypart.data_ptr<float>(), extra.data_ptr<float>(),
                               y.data_ptr<float>(), (int)n_rows, (int)x.numel(), (int)S, (const long long*)m,
@@ -444,7 +452,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
-    m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows) -> Tensor");
+    m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None) -> Tensor");
     m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x) -> Tensor");
     m.def("pack_edges(Tensor tile) -> Tensor");
     m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask) -> ()");

@@ -142,25 +142,60 @@ class Stencil(Workload):
     def work_per_step(self):
         return float(self.cells_local) * (self.graph_steps or self.slab.fuse)
 
+    def report(self, seconds, steps):
+        r = super().report(seconds, steps)
+        # strong scaling (one fixed grid): the world-sum of local cells is the grid, not world x grid
+        t = self.ctx.scalar(float(self.cells_local))
+        self.ctx.all_reduce_(t)
+        r["value"] = t.item() * (self.graph_steps or self.slab.fuse) * steps / seconds / 1e9
+        return r
+
+    def check(self):
+        """The timed path at this world size, bit for bit: a small grid stepped through the same slab code
+        (row slabs, fused T-row halo exchange, overlap) equals the single-domain single-step oracle."""
+        from ..parallel.stencil import StencilSlab, reference_run
+
+        f = self.slab.fuse
+        n, cols, steps = max(64, 2 * f * self.ctx.world + 8), 200, 4 * f
+        small = StencilSlab(self.ctx, n, cols, fuse=f)
+        small.run(steps, self.overlap)
+        full = small.gather()
+        ok = 1.0
+        if self.ctx.is_root:
+            ref = reference_run(n, steps, cols, device=self.ctx.device)
+            ok = float(torch.equal(full.view(torch.int16), ref.view(torch.int16)))
+        ok = self.ctx.broadcast_(self.ctx.scalar(ok)).item()
+        finite = float(torch.isfinite(self.slab.interior().float()).all())
+        return {"bit_exact_vs_single_step_oracle": bool(ok),
+                "finite": bool(self.ctx.max_over_ranks(1.0 - finite) == 0.0)}
+
 
 class SpMV(Workload):
-    """Power-law CSR SpMV (nnz-balanced row blocks) + all-gather of y: x <- A x."""
+    """Power-law CSR SpMV (nnz-balanced row blocks) + chunked all-gather of y overlapped with the product
+    (parallel/spmv.py): y <- A x with x, y replicated in the padded layout. Strong scaling: one fixed matrix."""
 
     def __init__(self, ctx, n_rows=10_000_000, nnz=100_000_000, alpha=2.5, slices=16, head=0.0625,
-                 balance=0.0, **_):
+                 balance=0.0, chunks=0, **_):
         from ..parallel.spmv import DistributedSpMV
 
         slices = int(slices) if ctx.device.type == "cuda" else 0
-        super().__init__(ctx, {"n_rows": n_rows, "nnz": nnz, "slices": slices, "head": head},
-                         "spmv", "GFLOP/s")
         self.d = DistributedSpMV.powerlaw(ctx, n_rows, nnz, alpha, slices=slices, head=float(head),
-                                          balance=float(balance))
-        self.x = torch.empty(n_rows, device=ctx.device)
-        ops.rand_uniform_(self.x, 5, 0.0, 1.0)
+                                          balance=float(balance), chunks=int(chunks) or None)
+        super().__init__(ctx, {"n_rows": n_rows, "nnz": nnz, "slices": slices, "head": head,
+                               "chunks": self.d.chunks}, "spmv", "GFLOP/s")
+        x = ops.rand_uniform_(torch.empty(n_rows, device=ctx.device), 5, 0.0, 1.0)
+        self.xp = self.d.to_padded(x)
+        del x
         self.y = None
 
     def step(self):
-        self.y = self.d.step(self.x)
+        self.y = self.d.step_padded(self.xp)
+
+    def check(self):
+        got = self.y[self.d.local_positions()].double()
+        ref = self.d.reference_local(self.xp)
+        err = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item() if ref.numel() else 0.0
+        return {"max_rel_err_vs_fp64": self.ctx.max_over_ranks(err)}
 
     def work_per_step(self):
         return 2.0 * self.d.local_nnz

@@ -42,6 +42,11 @@ class CSR:
         self.items = items.to(self.row_ptr.device)
         return self
 
+    def row_block(self, r0: int, r1: int) -> "CSR":
+        """Rows [r0, r1) as their own CSR (views of col/val; the work-item plan is rebuilt on demand)."""
+        a, b = int(self.row_ptr[r0]), int(self.row_ptr[r1])
+        return CSR((self.row_ptr[r0:r1 + 1] - a).contiguous(), self.col[a:b], self.val[a:b], self.n_cols)
+
     def dense(self) -> torch.Tensor:
         rows = torch.repeat_interleave(torch.arange(self.n_rows, device=self.val.device),
                                        (self.row_ptr[1:] - self.row_ptr[:-1]).to(self.val.device))
@@ -134,9 +139,10 @@ class SlicedCSR:
         self.ypart = torch.empty(S * n, dtype=torch.float32, device=dev)
         self.extra = torch.empty(max(1, item0[-1]), dtype=torch.float32, device=dev)
 
-    def spmv(self, x: torch.Tensor) -> torch.Tensor:
+    def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """y = A x; `out` (contiguous f32, >= n_rows elements) receives y in place when given."""
         return ops().spmv_sliced(self.lrow, self.col, self.val, x, self.items, self.fix, self.meta, self.ypart,
-                                 self.extra, self.n_rows)
+                                 self.extra, self.n_rows, out)
 
     def rows(self) -> torch.Tensor:
         """Row of every stored nonzero, rebuilt from the items and lrow (the layout the kernel reads)."""

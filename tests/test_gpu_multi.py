@@ -1,0 +1,67 @@
+"""Multi-process GPU paths: the bench contract on the GPU at one rank, and every north-star workload under
+torchrun over RCCL on all visible GPUs (skipped on a 1-GPU box; the driver's 8-GPU node runs it)."""
+import json
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+from conftest import ASSETS, ROOT, cli_env
+
+from parallel_c_programs_amd.utils import bmp
+
+pytestmark = pytest.mark.gpu
+
+
+def _bench(nproc, *extra, timeout=240):
+    from parallel_c_programs_amd.parallel import free_port
+
+    if nproc == 1:
+        cmd = [sys.executable, str(ROOT / "bench.py")]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "bench.py")]
+    cmd += ["--gpus", str(nproc), *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=cli_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _check_line(out, n):
+    assert out["n_gpus"] == n and out["device"] == "cuda" and out["value"] > 0
+    for k in ("reduce_weak_gbps", "reduce_strong_gbps", "scan_weak_gbps", "scan_strong_gbps", "stencil_glups",
+              "spmv_gflops"):
+        assert out[k] > 0, k
+    assert out["stencil_bit_exact"] and out["stencil_finite"]
+    assert out["sgemm_max_rel_err_vs_fp64"] < 1e-5 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
+    assert out["reduce_strong_rel_err_vs_fp64"] < 1e-5 and out["scan_strong_rel_err_vs_fp64"] < 1e-5
+
+
+def test_bench_small_one_gpu(gpu):
+    _check_line(_bench(1, "--steps", "2", "--warmup", "1", "--small", "--no-ref"), 1)
+
+
+def _ngpu():
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 visible GPUs")
+def test_bench_small_torchrun_all_gpus(gpu):
+    n = min(_ngpu(), 8)
+    _check_line(_bench(n, "--steps", "2", "--warmup", "1", "--small", "--no-ref"), n)
+
+
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 visible GPUs")
+def test_region_torchrun_rccl_writes_golden(gpu, tmp_path):
+    from parallel_c_programs_amd.parallel import free_port
+
+    n = min(_ngpu(), 8)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "parallel_c_programs_amd.cli.run_region",
+           str(ASSETS / "pic1.bmp")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=cli_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert np.array_equal(bmp.read(tmp_path / "out.bmp"), bmp.read(ASSETS / "region_pic1_golden.bmp"))
