@@ -60,12 +60,15 @@ def parse(argv=None):
 
 
 def _r(v, nd=4):
-    return None if v is None else round(float(v), nd)
+    """Round to nd decimals, keeping at least 4 significant digits (tiny CPU-rehearsal values stay nonzero)."""
+    if v is None:
+        return None
+    v = float(v)
+    return round(v, nd) if abs(v) >= 10 ** (3 - nd) else float(f"{v:.4g}")
 
 
 def main(argv=None):
     args = parse(argv)
-    from parallel_c_programs_amd import ops
     from parallel_c_programs_amd.models import workloads as W
     from parallel_c_programs_amd.parallel import finalize, init
     from parallel_c_programs_amd.utils.harness import timed

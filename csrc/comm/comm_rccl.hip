@@ -248,6 +248,9 @@ int d_pack(const unsigned char* t, int h, int w, unsigned char* buf, void* ctx) 
 int d_unpack(unsigned char* t, int h, int w, const unsigned char* buf, int mask, void* ctx) {
     return pcmx_unpack_halo(t, 1, h, w, w + 2, buf, mask, static_cast<DevCtx*>(ctx)->s);
 }
+int d_unpack_changed(unsigned char* t, int h, int w, const unsigned char* buf, int mask, int* changed, void* ctx) {
+    return pcmx_unpack_halo_changed(t, 1, h, w, w + 2, buf, mask, changed, static_cast<DevCtx*>(ctx)->s);
+}
 int d_sync(void* ctx) { return (int)hipStreamSynchronize(static_cast<DevCtx*>(ctx)->s); }
 
 int env_int(const char* n, int d) {
@@ -261,6 +264,7 @@ extern "C" int pcmx_region_backend_hip(pcmx_region_backend_t* be, void* stream) 
     c->s = static_cast<hipStream_t>(stream);
     be->alloc = d_alloc, be->release = d_release, be->memset0 = d_memset0, be->h2d = d_h2d, be->d2h = d_d2h;
     be->copy2d = d_copy2d, be->grow = d_grow, be->pack = d_pack, be->unpack = d_unpack, be->sync = d_sync;
+    be->unpack_changed = d_unpack_changed;
     be->ctx = c;
     return 0;
 }

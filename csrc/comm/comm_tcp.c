@@ -140,21 +140,36 @@ static int tcp_push(pcmx_comm_t* c, int is_send, void* buf, size_t bytes, int pe
 static int tcp_progress(pcmx_comm_t* c) {
     tcp_impl_t* t = (tcp_impl_t*)c->impl;
     const int W = c->world;
-    /* self messages: match k-th send to self with k-th recv from self */
-    for (int i = 0; i < t->nops; ++i) {
+    int rc = 0;
+    /* self messages: match k-th send to self with k-th recv from self; a size mismatch or an op without a
+     * partner is an error (the group is dropped either way, so no stale op survives into the next group) */
+    for (int i = 0; i < t->nops && !rc; ++i) {
         tcp_op_t* s = &t->ops[i];
         if (!s->is_send || s->peer != c->rank || s->done == s->bytes + 1) continue;
+        int matched = 0;
         for (int j = 0; j < t->nops; ++j) {
             tcp_op_t* r = &t->ops[j];
             if (r->is_send || r->peer != c->rank || r->done == r->bytes + 1) continue;
-            if (r->bytes != s->bytes) return -3;
+            if (r->bytes != s->bytes) {
+                rc = -3;
+                break;
+            }
             memcpy(r->buf, s->buf, s->bytes);
             s->done = s->bytes + 1, r->done = r->bytes + 1; /* mark complete */
+            matched = 1;
             break;
         }
+        if (!matched && !rc) rc = -3; /* send to self without a recv from self */
+    }
+    for (int i = 0; i < t->nops && !rc; ++i) /* recv from self without a send to self */
+        if (!t->ops[i].is_send && t->ops[i].peer == c->rank && t->ops[i].done != t->ops[i].bytes + 1) rc = -3;
+    if (rc) {
+        t->nops = 0;
+        return rc;
     }
     struct pollfd* pf = (struct pollfd*)calloc((size_t)2 * W, sizeof(struct pollfd));
-    int rc = 0;
+    double t_start = now_s(); /* deadline: 60 s without progress */
+    const double t_limit = 60.0;
     for (;;) {
         int npf = 0, pending = 0;
         /* head-of-line op per (peer, direction) */
@@ -179,11 +194,14 @@ static int tcp_progress(pcmx_comm_t* c) {
             }
         }
         if (!pending) break;
-        int k = poll(pf, (nfds_t)npf, 60000);
+        const int left_ms = (int)((t_limit - (now_s() - t_start)) * 1e3);
+        int k = left_ms > 0 ? poll(pf, (nfds_t)npf, left_ms) : 0;
+        if (k < 0 && errno == EINTR) continue; /* a signal is not a transport failure: retry, same deadline */
         if (k <= 0) {
             rc = k == 0 ? -4 : -5; /* timeout / error */
             break;
         }
+        t_start = now_s();
         for (int q = 0; q < npf; ++q) {
             if (!pf[q].revents) continue;
             int p = -1;

@@ -10,7 +10,8 @@
  *   grow      local fixpoint on the tile; region cells in the halo ring act as seeds (ref DFS :499-527 +
  *             add_halo_to_stack :355)
  *   exchange  pack 4 edges -> grouped send/recv with N/S/W/E -> unpack (ref exchange :250-353)
- *   finish    MAX all-reduce of "halo changed" (ref finished(): MIN all-reduce of local_finish :435)
+ *   finish    device-resident "halo changed" flag raised by the unpack, MAX all-reduce in place, read by the
+ *             host every PCMX_REGION_CHECK_EVERY steps (ref finished(): MIN all-reduce of local_finish :435)
  *   gather    one message per rank to root (ref gather_region :391)
  * Any process count and image size (the reference handles square grids only, B8).
  */
@@ -104,6 +105,20 @@ static int h_unpack(unsigned char* t, int h, int w, const unsigned char* buf, in
     return 0;
 }
 
+static int h_unpack_changed(unsigned char* t, int h, int w, const unsigned char* buf, int mask, int* changed,
+                            void* ctx) {
+    const int ld = w + 2;
+    int diff = 0;
+    if (mask & 1) diff |= memcmp(t + 1, buf, (size_t)w) != 0;
+    if (mask & 2) diff |= memcmp(t + (size_t)(h + 1) * ld + 1, buf + w, (size_t)w) != 0;
+    for (int r = 0; r < h; ++r) {
+        if (mask & 4) diff |= t[(size_t)(r + 1) * ld] != buf[2 * w + r];
+        if (mask & 8) diff |= t[(size_t)(r + 1) * ld + w + 1] != buf[2 * w + h + r];
+    }
+    if (diff) *changed = 1;
+    return h_unpack(t, h, w, buf, mask, ctx);
+}
+
 static int h_sync(void* ctx) {
     (void)ctx;
     return 0;
@@ -112,6 +127,7 @@ static int h_sync(void* ctx) {
 void pcmx_region_backend_host(pcmx_region_backend_t* be) {
     be->alloc = h_alloc, be->release = h_release, be->memset0 = h_memset0, be->h2d = h_copy, be->d2h = h_copy;
     be->copy2d = h_copy2d, be->grow = h_grow, be->pack = h_pack, be->unpack = h_unpack, be->sync = h_sync;
+    be->unpack_changed = h_unpack_changed;
     be->ctx = NULL;
 }
 
@@ -125,12 +141,6 @@ void pcmx_region_backend_host(pcmx_region_backend_t* be) {
             goto done;          \
         }                       \
     } while (0)
-
-static long long halo_count_host(const unsigned char* packed_halo, int n) {
-    long long s = 0;
-    for (int i = 0; i < n; ++i) s += packed_halo[i] != 0;
-    return s;
-}
 
 int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, const unsigned char* image, int H,
                               int W, int threshold, const int* dims, unsigned char* region_out, int* stats) {
@@ -151,7 +161,7 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
     const size_t tbytes = (size_t)(h + 2) * (w + 2);
     const int nedge = 2 * w + 2 * h;
     unsigned char *img_p = NULL, *reg_p = NULL, *full_p = NULL, *stage = NULL, *sendb = NULL, *recvb = NULL;
-    unsigned char *host_halo = NULL, *full_reg = NULL;
+    unsigned char* full_reg = NULL;
     int* flag = NULL;
     int outer = 0;
     img_p = (unsigned char*)be->alloc(tbytes, ctx);
@@ -159,8 +169,7 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
     sendb = (unsigned char*)be->alloc((size_t)nedge, ctx);
     recvb = (unsigned char*)be->alloc((size_t)nedge, ctx);
     flag = (int*)be->alloc(sizeof(int), ctx);
-    host_halo = (unsigned char*)malloc((size_t)nedge);
-    if (!img_p || !reg_p || !sendb || !recvb || !flag || !host_halo) {
+    if (!img_p || !reg_p || !sendb || !recvb || !flag) {
         rc = -3;
         goto done;
     }
@@ -224,9 +233,12 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
     mask |= nb[2] >= 0 ? 4 : 0;
     mask |= nb[3] >= 0 ? 8 : 0;
     const int off_e[4] = {0, w, 2 * w, 2 * w + h}, len_e[4] = {w, w, h, h};
-    long long halo_before = 0;
 
-    /* ---- bulk-synchronous grow / exchange / terminate */
+    /* ---- bulk-synchronous grow / exchange / terminate. The "halo changed" flag lives in backend (device)
+     * memory: the unpack kernel raises it, the MAX all-reduce runs on it in place, and the host reads it once
+     * per PCMX_REGION_CHECK_EVERY outer steps (a window with no change on any rank = global fixpoint: a step
+     * whose halos did not change cannot grow anything new, so every later step is a no-op too). */
+    TRY(be->memset0(flag, sizeof(int), ctx));
     for (;;) {
         TRY(be->grow(reg_p, img_p, h, w, threshold, ctx));
         ++outer;
@@ -240,18 +252,13 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
             TRY(pcmx_comm_recv(c, recvb + off_e[k], (size_t)len_e[k], nb[k]));
         }
         TRY(pcmx_comm_group_end(c));
-        TRY(be->unpack(reg_p, h, w, recvb, mask, ctx));
-        /* halo cells only ever turn on: a changed count means new seeds arrived */
-        TRY(be->d2h(host_halo, recvb, (size_t)nedge, ctx));
-        long long now = 0;
-        for (int k = 0; k < 4; ++k)
-            if (nb[k] >= 0) now += halo_count_host(host_halo + off_e[k], len_e[k]);
-        int changed = now != halo_before;
-        halo_before = now;
-        TRY(be->h2d(flag, &changed, sizeof changed, ctx));
+        TRY(be->unpack_changed(reg_p, h, w, recvb, mask, flag, ctx));
+        if (outer % PCMX_REGION_CHECK_EVERY) continue;
         TRY(pcmx_comm_allreduce(c, flag, 1, PCMX_I32, PCMX_MAX));
-        TRY(be->d2h(&changed, flag, sizeof changed, ctx));
+        int changed = 1;
+        TRY(be->d2h(&changed, flag, sizeof changed, ctx));  /* the loop's only host read-back */
         if (!changed) break;
+        TRY(be->memset0(flag, sizeof(int), ctx));
     }
 
     /* ---- gather interiors to root (one message per rank) */
@@ -299,7 +306,6 @@ done:
     if (sendb) be->release(sendb, ctx);
     if (recvb) be->release(recvb, ctx);
     if (flag) be->release(flag, ctx);
-    free(host_halo);
     free(full_reg);
     return rc;
 }

@@ -90,14 +90,20 @@ typedef struct pcmx_region_backend {
     int (*grow)(unsigned char* region_p, const unsigned char* img_p, int h, int w, int threshold, void* ctx);
     int (*pack)(const unsigned char* tile_p, int h, int w, unsigned char* buf, void* ctx);    /* 2w+2h bytes */
     int (*unpack)(unsigned char* tile_p, int h, int w, const unsigned char* buf, int mask, void* ctx);
+    /* unpack + set *changed_flag (backend memory) to 1 when any halo cell takes a new value */
+    int (*unpack_changed)(unsigned char* tile_p, int h, int w, const unsigned char* buf, int mask, int* changed_flag,
+                          void* ctx);
     int (*sync)(void* ctx);
     void* ctx;
 } pcmx_region_backend_t;
 
+#define PCMX_REGION_CHECK_EVERY 2
 void pcmx_region_backend_host(pcmx_region_backend_t* be);
 int pcmx_region_backend_hip(pcmx_region_backend_t* be, void* stream); /* in libpcmx_hip */
 
 /* Distributed seeded region growing over the Cartesian grid of `c` (ref region.c:582-604).
+ * Termination is device-resident: the unpack kernel raises a "halo changed" flag in backend memory, the flag is
+ * MAX-all-reduced in place and read by the host once every PCMX_REGION_CHECK_EVERY outer steps.
  * image: H*W bytes on root (host memory; ignored elsewhere); region_out: H*W bytes on root (host).
  * dims: process grid or NULL. stats (optional): [outer_steps, local_grow_calls]. Returns 0 on success. */
 int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, const unsigned char* image, int H,

@@ -5,7 +5,8 @@
  *  - All pointers are DEVICE pointers unless the name says host. Every launcher is asynchronous on the
  *    given stream, allocates nothing and never synchronises, so a caller may capture it into a hipGraph.
  *    Workspaces are caller-provided; pcmx_*_workspace_bytes() says how much.
- *  - Return value: 0 on success, otherwise a hipError_t (or -1 for a shape/alignment precondition).
+ *  - Return value: 0 on success, a hipError_t (> 0), or one of the PCMX_ERR_* codes below (< 0).
+ *  - No launcher keeps process-global tuning state: every knob is a per-call argument.
  *  - Element counts are 64-bit: 1e9-element arrays (4 GB) are first-class on a 288 GB MI355X.
  *
  * Reference parity (file:line in anonyomous4/parallel-c-programs):
@@ -27,6 +28,14 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* ---------------------------------------------------------------- error codes (pcmx_error_string names them) */
+enum {
+    PCMX_ERR_ARG = -1,           /* shape / alignment / argument precondition */
+    PCMX_ERR_NOT_CONVERGED = -2, /* an iterate-to-fixpoint loop ran out of max_launches with work left */
+    PCMX_ERR_TIMEOUT = -3,       /* a bounded device-side wait gave up (result invalid) */
+    PCMX_ERR_COMM = -4           /* a transport / collective failed */
+};
 
 /* ---------------------------------------------------------------- runtime / device info */
 int pcmx_device_count(void);
@@ -58,12 +67,19 @@ int pcmx_dot_f32(const float* a, const float* b, long long n, float* out, void* 
 
 /* ---------------------------------------------------------------- prefix scan */
 long long pcmx_scan_workspace_bytes(long long n);
-int pcmx_scan_set_rows(int rows); /* tile shape knob: f32x4 rows per lane, 16 (8 waves, default) or 8 (16 waves) */
 /* out[i] = init + sum_{j<=i} x[j] (inclusive) or init + sum_{j<i} x[j] (exclusive), single pass with
  * decoupled look-back; init is read from device memory (init_dev may be NULL => 0) so a multi-GPU
- * offset can be fed without a host round trip. In-place (out == x) is allowed. */
+ * offset can be fed without a host round trip. In-place (out == x) is allowed.
+ * A look-back that exceeds its bounded spin (a stalled predecessor) leaves an INVALID result: it is recorded in
+ * the workspace (pcmx_scan_check) and OR-ed into *err_flag when err_flag != NULL (device or host-mapped word,
+ * sticky: the caller clears it). */
 int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
-                  hipStream_t s);
+                  unsigned* err_flag, hipStream_t s);
+/* same with an explicit tile shape: rows = f32x4 rows per lane, 16 (8 waves, the default) or 8 (16 waves) */
+int pcmx_scan_f32_rows(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
+                       unsigned* err_flag, int rows, hipStream_t s);
+/* synchronises s; PCMX_ERR_TIMEOUT if the last scan on this workspace gave up a look-back, else 0 */
+int pcmx_scan_check(const void* workspace, hipStream_t s);
 
 /* ---------------------------------------------------------------- SGEMM (fp32 MFMA) */
 /* C = alpha*A*B + beta*C, row-major. Fast path needs M%256==0, N%256==0 (or %128 for the small-tile
@@ -105,10 +121,9 @@ int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, 
  * (8-byte texels when every data value < 128, else 16-byte; the format flag is stored behind the texels),
  * dim <= 2048 */
 int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, void* tex, hipStream_t s);
-/* texture ray caster: steps per prefetch batch (1, 4 = default, 8, 16); returns the previous value */
-int pcmx_raycast_set_batch(int steps);
+/* texture ray caster; batch = steps per prefetch batch (1, 4, 8, 16; 0 = 4, the measured best) */
 int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* image, int image_dim,
-                         const float* cam12, float pixel_width, float step, int max_steps, hipStream_t s);
+                         const float* cam12, float pixel_width, float step, int max_steps, int batch, hipStream_t s);
 
 /* ---------------------------------------------------------------- stencil */
 int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, int ld, int r0, int r1, long long global_row0,
@@ -129,20 +144,23 @@ int pcmx_spmv_csr(const long long* row_ptr, const int* col, const float* val, co
  * and lrow (u16 row offset inside its item); per slice nnz-balanced items (a later piece of a split long row
  * has row1 == row0). Slice s runs on the blocks b with b % 8 == s % 8 (one XCD), writes ypart[s][0, n_rows);
  * a combine pass sums the partials into y and a fix-up adds extra[fix[k].item] to y[fix[k].row].
- * slice_nz0 / slice_item0 are HOST arrays (n_slices and n_slices + 1 entries). */
+ * slice_nz0 / slice_item0 are HOST arrays (n_slices and n_slices + 1 entries).
+ * mode: 0 = production; bit 0 = skip the x gathers (lab measurement only); mode >> 8 (if nonzero) = resident
+ * blocks per CU (default 2). */
 #define PCMX_SPMV_MAX_SLICES 32
 int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x, float* ypart,
                      float* extra, float* y, int n_rows, int n_cols, int n_slices, const long long* slice_nz0,
-                     const long long* slice_item0, const void* items, const void* fix, int n_fix, hipStream_t s);
-/* lab knob of the sliced kernel: bit 0 = skip the x gathers; mode >> 8 (if nonzero) = resident blocks per CU.
- * Returns the previous setting. */
-int pcmx_spmv_set_mode(int mode);
+                     const long long* slice_item0, const void* items, const void* fix, int n_fix, int mode,
+                     hipStream_t s);
 int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                      const float* x, float* y, hipStream_t s);
 
 /* ---------------------------------------------------------------- halo pack/unpack */
 int pcmx_pack_edges(const void* tile, int elem_bytes, int H, int W, int ld, void* buf, hipStream_t s);
 int pcmx_unpack_halo(void* tile, int elem_bytes, int H, int W, int ld, const void* buf, int mask, hipStream_t s);
+/* as pcmx_unpack_halo, and *changed (device int) is set to 1 when any halo cell takes a new value */
+int pcmx_unpack_halo_changed(void* tile, int elem_bytes, int H, int W, int ld, const void* buf, int mask, int* changed,
+                             hipStream_t s);
 
 #ifdef __cplusplus
 }

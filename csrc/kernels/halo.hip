@@ -26,9 +26,12 @@ __global__ __launch_bounds__(256) void pack_edges_kernel(const T* __restrict__ t
 
 template <class T>
 __global__ __launch_bounds__(256) void unpack_halo_kernel(T* __restrict__ tile, int H, int W, int ld,
-                                                         const T* __restrict__ buf, int mask) {
-    // mask bit 0: top halo valid, 1: bottom, 2: left, 3: right (absent neighbours leave the halo alone)
+                                                         const T* __restrict__ buf, int mask, int* __restrict__ changed) {
+    // mask bit 0: top halo valid, 1: bottom, 2: left, 3: right (absent neighbours leave the halo alone).
+    // changed (optional): set to 1 when any halo cell takes a new value — the device-resident "halo changed"
+    // flag of the distributed fixpoint loops (no host round trip to count halo cells).
     const int n = 2 * W + 2 * H;
+    bool diff = false;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         size_t dst;
         int side;
@@ -36,8 +39,13 @@ __global__ __launch_bounds__(256) void unpack_halo_kernel(T* __restrict__ tile, 
         else if (i < 2 * W) dst = (size_t)(H + 1) * ld + 1 + (i - W), side = 1;
         else if (i < 2 * W + H) dst = (size_t)(1 + i - 2 * W) * ld, side = 2;
         else dst = (size_t)(1 + i - 2 * W - H) * ld + W + 1, side = 3;
-        if (mask & (1 << side)) tile[dst] = buf[i];
+        if (mask & (1 << side)) {
+            const T v = buf[i];
+            diff |= tile[dst] != v;
+            tile[dst] = v;
+        }
     }
+    if (changed && __any(diff) && pcmx::lane_id() == 0) atomicOr(changed, 1);
 }
 
 inline int grid_for(int n) { return max(1, min(1024, (n + 255) / 256)); }
@@ -52,19 +60,24 @@ extern "C" int pcmx_pack_edges(const void* tile, int elem_bytes, int H, int W, i
     else if (elem_bytes == 4)
         pack_edges_kernel<unsigned><<<grid_for(n), 256, 0, s>>>((const unsigned*)tile, H, W, ld, (unsigned*)buf);
     else
-        return -1;
+        return PCMX_ERR_ARG;
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_unpack_halo_changed(void* tile, int elem_bytes, int H, int W, int ld, const void* buf, int mask,
+                                        int* changed, hipStream_t s) {
+    const int n = 2 * W + 2 * H;
+    if (elem_bytes == 1)
+        unpack_halo_kernel<unsigned char><<<grid_for(n), 256, 0, s>>>((unsigned char*)tile, H, W, ld, (const unsigned char*)buf, mask, changed);
+    else if (elem_bytes == 2)
+        unpack_halo_kernel<unsigned short><<<grid_for(n), 256, 0, s>>>((unsigned short*)tile, H, W, ld, (const unsigned short*)buf, mask, changed);
+    else if (elem_bytes == 4)
+        unpack_halo_kernel<unsigned><<<grid_for(n), 256, 0, s>>>((unsigned*)tile, H, W, ld, (const unsigned*)buf, mask, changed);
+    else
+        return PCMX_ERR_ARG;
     return (int)hipGetLastError();
 }
 
 extern "C" int pcmx_unpack_halo(void* tile, int elem_bytes, int H, int W, int ld, const void* buf, int mask, hipStream_t s) {
-    const int n = 2 * W + 2 * H;
-    if (elem_bytes == 1)
-        unpack_halo_kernel<unsigned char><<<grid_for(n), 256, 0, s>>>((unsigned char*)tile, H, W, ld, (const unsigned char*)buf, mask);
-    else if (elem_bytes == 2)
-        unpack_halo_kernel<unsigned short><<<grid_for(n), 256, 0, s>>>((unsigned short*)tile, H, W, ld, (const unsigned short*)buf, mask);
-    else if (elem_bytes == 4)
-        unpack_halo_kernel<unsigned><<<grid_for(n), 256, 0, s>>>((unsigned*)tile, H, W, ld, (const unsigned*)buf, mask);
-    else
-        return -1;
-    return (int)hipGetLastError();
+    return pcmx_unpack_halo_changed(tile, elem_bytes, H, W, ld, buf, mask, nullptr, s);
 }

@@ -350,8 +350,6 @@ __global__ __launch_bounds__(256) void raycast_tex_kernel(const void* __restrict
         raycast_tex_march<D, false>(tex, dim, image, image_dim, c);
 }
 
-int g_tex_batch = 4;  // steps per prefetch batch (pcmx_raycast_set_batch; measured best of 1/4/8/16)
-
 Cam make_cam(const float* cam12, float pw, float step, int max_steps) {
     Cam c;
     for (int k = 0; k < 3; ++k) {
@@ -401,13 +399,16 @@ extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* r
     return (int)hipGetLastError();
 }
 
+// batch = steps per prefetch batch (1, 4, 8, 16; 0 = 4, the measured best)
 extern "C" int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* image, int image_dim,
-                                    const float* cam12, float pixel_width, float step, int max_steps, hipStream_t s) {
-    if (dim <= 1 || dim > 2048 || image_dim <= 0) return -1;
+                                    const float* cam12, float pixel_width, float step, int max_steps, int batch,
+                                    hipStream_t s) {
+    if (dim <= 1 || dim > 2048 || image_dim <= 0) return PCMX_ERR_ARG;
+    if (batch != 0 && batch != 1 && batch != 4 && batch != 8 && batch != 16) return PCMX_ERR_ARG;
     const Cam c = make_cam(cam12, pixel_width, step, max_steps);
     dim3 grid((image_dim + 15) / 16, (image_dim + 15) / 16);
     const int* wide = reinterpret_cast<const int*>(reinterpret_cast<const char*>(tex) + (size_t)dim * dim * dim * 16);
-    switch (g_tex_batch) {
+    switch (batch) {
         case 1: raycast_tex_kernel<1><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
         case 16: raycast_tex_kernel<16><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
         case 8: raycast_tex_kernel<8><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
@@ -416,8 +417,3 @@ extern "C" int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* ima
     return (int)hipGetLastError();
 }
 
-extern "C" int pcmx_raycast_set_batch(int steps) {
-    const int old = g_tex_batch;
-    g_tex_batch = steps;
-    return old;
-}

@@ -491,7 +491,7 @@ extern "C" long long pcmx_region2d_workspace_bytes(int H, int W) {
 // ws: [flag | act0 | act1 | rb | hl | vl]. Host reads the changed flag once per `batch` launches.
 extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* region, int H, int W, int ld, int thr,
                                   void* ws, int batch, int max_launches, hipStream_t s, int* launches_out) {
-    if (H <= 0 || W <= 0 || ld < W + 2 || !ws || ((uintptr_t)ws & 7)) return -1;
+    if (H <= 0 || W <= 0 || ld < W + 2 || !ws || ((uintptr_t)ws & 7)) return PCMX_ERR_ARG;
     const Region2dGeom g = region2d_geom(H, W);
     int* flag = reinterpret_cast<int*>(ws);
     int* act[2] = {flag + 16, flag + 16 + g.nblocks};
@@ -506,7 +506,7 @@ extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* regio
     PCMX_HIP_RET(hipMemsetAsync(act[1], 0, g.nblocks * sizeof(int), s));
     const dim3 grid(g.nbx, g.nby);
     if (batch < 1) batch = 4;
-    int launches = 0, cur = 0;
+    int launches = 0, cur = 0, h = 1;
     while (launches < max_launches) {
         PCMX_HIP_RET(hipMemsetAsync(flag, 0, sizeof(int), s));
         for (int b = 0; b < batch && launches < max_launches; ++b, ++launches) {
@@ -514,7 +514,6 @@ extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* regio
             PCMX_HIP_RET(hipGetLastError());
             cur ^= 1;
         }
-        int h = 0;
         PCMX_HIP_RET(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, s));
         PCMX_HIP_RET(hipStreamSynchronize(s));
         if (!h) break;
@@ -522,7 +521,8 @@ extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* regio
     region2d_bits_store_kernel<<<(unsigned)(((long long)H * W + 255) / 256), 256, 0, s>>>(region, H, W, ld, g.nw, rb);
     PCMX_HIP_RET(hipGetLastError());
     if (launches_out) *launches_out = launches;
-    return 0;
+    // the last launch still changed something: the fixpoint was not confirmed (the region stored is partial)
+    return h ? PCMX_ERR_NOT_CONVERGED : 0;
 }
 
 extern "C" long long pcmx_region3d_workspace_bytes(int dim) {
@@ -549,7 +549,7 @@ extern "C" int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char
     region3d_seed_tiles_kernel<kBX, kBY, kBZ><<<nby * nbz, kSeedThreads, 0, s>>>(region, dim, nbx, nby, w, mark, lists);
     PCMX_HIP_RET(hipGetLastError());
     const int b = batch < 1 ? 8 : batch;
-    int launches = 0;
+    int launches = 0, h = 1;
     while (launches < max_launches) {
         PCMX_HIP_RET(hipMemsetAsync(&w->flag, 0, sizeof(int), s));
         for (int i = 0; i < b && launches < max_launches; ++i, ++launches) {
@@ -557,30 +557,28 @@ extern "C" int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char
                                                          lists, (int)nt);
             PCMX_HIP_RET(hipGetLastError());
         }
-        int h = 0;
         PCMX_HIP_RET(hipMemcpyAsync(&h, &w->flag, sizeof(int), hipMemcpyDeviceToHost, s));
         PCMX_HIP_RET(hipStreamSynchronize(s));
         if (!h) break;
     }
     if (launches_out) *launches_out = launches;
-    return 0;
+    return h ? PCMX_ERR_NOT_CONVERGED : 0;
 }
 
 extern "C" int pcmx_region3d_grow_naive(const unsigned char* data, unsigned char* region, int dim, int thr, int* flag_ws,
                                         int max_launches, hipStream_t s, int* launches_out) {
     if (dim <= 0 || !flag_ws) return -1;
     dim3 grid((dim + 63) / 64, (dim + 3) / 4, dim);
-    int launches = 0;
+    int launches = 0, h = 1;
     while (launches < max_launches) {
         PCMX_HIP_RET(hipMemsetAsync(flag_ws, 0, sizeof(int), s));
         region3d_step_kernel<<<grid, 256, 0, s>>>(data, region, dim, thr, flag_ws);
         PCMX_HIP_RET(hipGetLastError());
         ++launches;
-        int h = 0;
         PCMX_HIP_RET(hipMemcpyAsync(&h, flag_ws, sizeof(int), hipMemcpyDeviceToHost, s));
         PCMX_HIP_RET(hipStreamSynchronize(s));
         if (!h) break;
     }
     if (launches_out) *launches_out = launches;
-    return 0;
+    return h ? PCMX_ERR_NOT_CONVERGED : 0;
 }

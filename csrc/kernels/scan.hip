@@ -15,7 +15,10 @@
 //  * Hand-off = 8-byte {flag, value} granules written with ONE agent-scope relaxed atomic store and polled
 //    with agent-scope relaxed loads (cdna_hip_programming.md G16 recipe R2); one wave looks back 64 tiles per
 //    poll (wider per-lane windows measured slower). Status words and the ticket are zeroed by a
-//    hipMemsetAsync on the same stream before every launch; spins are bounded and report a timeout flag.
+//    hipMemsetAsync on the same stream before every launch. Spins are bounded: a look-back that gives up
+//    marks its result invalid in the workspace (ws->timeout) AND in the caller's sticky error word
+//    (err_flag, system-scope atomic OR: it may live in host-mapped pinned memory), which pcmx_scan_check /
+//    the torch op turn into an error instead of a silently wrong prefix.
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 
@@ -23,7 +26,13 @@ namespace {
 using pcmx::f32x4;
 using pcmx::kWave;
 constexpr unsigned kFlagAgg = 1u, kFlagIncl = 2u;
+#ifdef PCMX_FAULT_INJECT
+// test-only build (libpcmx_faultinj.so): the look-back of tile 1 never sees its predecessor and gives up fast
+constexpr unsigned kSpinLimit = 64u;
+constexpr long long kFaultTile = 1;
+#else
 constexpr unsigned kSpinLimit = 1u << 26;
+#endif
 constexpr int kTileElems = 32768;  // 128 KiB of f32 for every variant
 
 struct ScanWs {
@@ -72,8 +81,8 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ in, long lon
 template <int R, int W>
 __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float* __restrict__ out, long long n, long long tile,
                                             f32x4 (&v)[R], long long next, f32x4 (&vn)[R], long long ntiles, int exclusive,
-                                            float init, ScanWs* ws, float* s_wave_tot, float* s_prefix,
-                                            unsigned* s_next) {
+                                            float init, ScanWs* ws, unsigned* err_flag, float* s_wave_tot,
+                                            float* s_prefix, unsigned* s_next) {
     unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
     const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
     // ---- in-wave scan: per row, lane-local prefix, then a wave scan of the lane totals
@@ -119,9 +128,12 @@ __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float*
             unsigned spins = 0;
             while (true) {
                 const long long idx = look - lane;
-                const unsigned long long sv =
+                unsigned long long sv =
                     idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                              : pack(kFlagIncl, 0.f);
+#ifdef PCMX_FAULT_INJECT
+                if (tile == kFaultTile) sv = 0ull;  // fault injection: this tile never sees its predecessors
+#endif
                 const unsigned flag = (unsigned)(sv >> 32);
                 const float val = __uint_as_float((unsigned)sv);
                 const unsigned long long m_incl = __ballot(flag == kFlagIncl);
@@ -138,8 +150,11 @@ __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float*
                     look -= kWave;
                     continue;
                 }
-                if (++spins > kSpinLimit) {  // bounded spin: report and fall through
-                    if (lane == 0) atomicExch(&ws->timeout, 1u);
+                if (++spins > kSpinLimit) {  // bounded spin: report (workspace + sticky caller word) and fall through
+                    if (lane == 0) {
+                        atomicExch(&ws->timeout, 1u);
+                        if (err_flag) __hip_atomic_fetch_or(err_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -183,7 +198,7 @@ __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float*
 template <int R, int W>
 __global__ __launch_bounds__(W * kWave) void scan_persistent_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                                     long long n, long long ntiles, int exclusive,
-                                                                    const float* init_dev, ScanWs* ws) {
+                                                                    const float* init_dev, ScanWs* ws, unsigned* err_flag) {
     // two LDS slots so consecutive tiles never race on the broadcast values
     __shared__ float s_wave_tot[2][W];
     __shared__ float s_prefix[2];
@@ -201,17 +216,16 @@ __global__ __launch_bounds__(W * kWave) void scan_persistent_kernel(const float*
     // unrolled by two so both register buffers are statically named (every exit is block-uniform); each
     // finish_tile takes the ticket two tiles ahead and publishes it in s_tile[slot] by its last barrier
     while (true) {
-        finish_tile<R, W>(in, out, n, ta, va, tb, vb, ntiles, exclusive, init, ws, s_wave_tot[0], &s_prefix[0], &s_tile[0]);
+        finish_tile<R, W>(in, out, n, ta, va, tb, vb, ntiles, exclusive, init, ws, err_flag, s_wave_tot[0], &s_prefix[0], &s_tile[0]);
         if (tb >= ntiles) break;
         ta = s_tile[0];
-        finish_tile<R, W>(in, out, n, tb, vb, ta, va, ntiles, exclusive, init, ws, s_wave_tot[1], &s_prefix[1], &s_tile[1]);
+        finish_tile<R, W>(in, out, n, tb, vb, ta, va, ntiles, exclusive, init, ws, err_flag, s_wave_tot[1], &s_prefix[1], &s_tile[1]);
         if (ta >= ntiles) break;
         tb = s_tile[1];
     }
 }
 
 inline long long num_tiles(long long n) { return (n + kTileElems - 1) / kTileElems; }
-int g_scan_rows = 16;
 
 int device_cus() {
     static int cus[64] = {0};
@@ -223,26 +237,34 @@ int device_cus() {
 }
 }  // namespace
 
-extern "C" int pcmx_scan_set_rows(int rows) {
-    if (rows != 8 && rows != 16) return -1;
-    g_scan_rows = rows;
-    return 0;
-}
-
 extern "C" long long pcmx_scan_workspace_bytes(long long n) { return (long long)sizeof(ScanWs) + num_tiles(n) * 8; }
 
-extern "C" int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
-                             hipStream_t s) {
+extern "C" int pcmx_scan_f32_rows(const float* x, float* out, long long n, int exclusive, const float* init_dev,
+                                  void* workspace, unsigned* err_flag, int rows, hipStream_t s) {
     if (n <= 0) return 0;
-    if ((((uintptr_t)x) & 15u) || (((uintptr_t)out) & 15u) || !workspace) return -1;
+    if (rows != 8 && rows != 16) return PCMX_ERR_ARG;
+    if ((((uintptr_t)x) & 15u) || (((uintptr_t)out) & 15u) || !workspace) return PCMX_ERR_ARG;
     const long long tiles = num_tiles(n);
-    if (tiles > 0x7fffffffLL) return -1;
+    if (tiles > 0x7fffffffLL) return PCMX_ERR_ARG;
     PCMX_HIP_RET(hipMemsetAsync(workspace, 0, sizeof(ScanWs) + (size_t)tiles * 8, s));
     ScanWs* ws = reinterpret_cast<ScanWs*>(workspace);
     const unsigned grid = (unsigned)(tiles < device_cus() ? tiles : device_cus());  // one resident block per CU
-    if (g_scan_rows == 8)
-        scan_persistent_kernel<8, 16><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws);
+    if (rows == 8)
+        scan_persistent_kernel<8, 16><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag);
     else
-        scan_persistent_kernel<16, 8><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws);
+        scan_persistent_kernel<16, 8><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag);
     return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
+                             unsigned* err_flag, hipStream_t s) {
+    return pcmx_scan_f32_rows(x, out, n, exclusive, init_dev, workspace, err_flag, 16, s);
+}
+
+extern "C" int pcmx_scan_check(const void* workspace, hipStream_t s) {
+    if (!workspace) return PCMX_ERR_ARG;
+    unsigned t = 0;
+    PCMX_HIP_RET(hipMemcpyAsync(&t, &reinterpret_cast<const ScanWs*>(workspace)->timeout, sizeof(t), hipMemcpyDeviceToHost, s));
+    PCMX_HIP_RET(hipStreamSynchronize(s));
+    return t ? PCMX_ERR_TIMEOUT : 0;
 }

@@ -37,8 +37,7 @@ constexpr int kItemRows = 1023;           // rows per multi-row item (bounds the
 constexpr int kRpPerLane = (kItemRows + 1 + 63) / 64;  // row pointers per lane (kItemRows + 1 per item)
 constexpr int kPerLane = kItemNnz / kWave;  // nonzeros per lane
 constexpr int kMaxSlices = PCMX_SPMV_MAX_SLICES;
-int g_persist_blocks = 2;  // sliced kernel: resident blocks (of 4 waves) per CU (170 VGPRs -> 2 waves/SIMD)
-int g_spmv_mode = 0;       // lab knob (pcmx_spmv_set_mode): 1 = skip the x gathers
+constexpr int kPersistBlocks = 2;  // sliced kernel: resident blocks (of 4 waves) per CU (170 VGPRs -> 2 waves/SIMD)
 
 // ------------------------------------------------------------------------------------------ plain CSR
 // One wave per item. All column/value loads of the item AND its row pointers are issued up front, then all
@@ -350,9 +349,10 @@ extern "C" int pcmx_spmv_csr(const long long* row_ptr, const int* col, const flo
 extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x,
                                 float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
                                 const long long* slice_nz0, const long long* slice_item0, const void* items,
-                                const void* fix, int n_fix, hipStream_t s) {
+                                const void* fix, int n_fix, int mode, hipStream_t s) {
     if (n_rows <= 0) return 0;
     if (n_slices <= 0 || n_slices % 8 || n_slices > kMaxSlices) return (int)hipErrorInvalidValue;
+    const int persist_blocks = (mode >> 8) ? (mode >> 8) : kPersistBlocks;
     SliceMeta meta{};
     long long most = 0;
     for (int k = 0; k < n_slices; ++k) {
@@ -368,10 +368,10 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
         const long long need = (most + kWavesPerBlock - 1) / kWavesPerBlock;
-        const long long per = (long long)(cus / 8) * g_persist_blocks;  // resident blocks per XCD
+        const long long per = (long long)(cus / 8) * persist_blocks;  // resident blocks per XCD
         const int bp = (int)(need < per ? need : per);
         const unsigned nb = (unsigned)(bp * n_slices);
-        if (g_spmv_mode & 1)
+        if (mode & 1)
             spmv_sliced_kernel<1><<<nb, kWavesPerBlock * kWave, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra,
                                                                         reinterpret_cast<const Item*>(items), meta, n_rows, bp);
         else
@@ -390,13 +390,6 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
     if (n_fix > 0)
         spmv_fixup_kernel<<<(n_fix + 255) / 256, 256, 0, s>>>(extra, reinterpret_cast<const int2*>(fix), n_fix, y);
     return (int)hipGetLastError();
-}
-
-extern "C" int pcmx_spmv_set_mode(int mode) {
-    const int old = g_spmv_mode | (g_persist_blocks << 8);
-    g_spmv_mode = mode & 0xff;
-    if (mode >> 8) g_persist_blocks = mode >> 8;
-    return old;
 }
 
 extern "C" int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,

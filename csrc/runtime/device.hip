@@ -15,8 +15,13 @@ extern "C" int pcmx_device_count(void) {
 }
 
 extern "C" const char* pcmx_error_string(int err) {
-    if (err == -1) return "pcmx: shape/alignment precondition violated";
-    return hipGetErrorString((hipError_t)err);
+    switch (err) {
+        case PCMX_ERR_ARG: return "pcmx: shape/alignment/argument precondition violated";
+        case PCMX_ERR_NOT_CONVERGED: return "pcmx: not converged within max_launches (result incomplete)";
+        case PCMX_ERR_TIMEOUT: return "pcmx: bounded device wait timed out (result invalid)";
+        case PCMX_ERR_COMM: return "pcmx: communication failed";
+        default: return err < 0 ? "pcmx: unknown error" : hipGetErrorString((hipError_t)err);
+    }
 }
 
 extern "C" void pcmx_print_device_info(int device) {

@@ -113,14 +113,56 @@ at::Tensor dot(const at::Tensor& a, const at::Tensor& b) {
     return out;
 }
 
+// Sticky look-back-timeout word per device in host-mapped pinned memory: a scan kernel whose look-back gives
+// up ORs 1 into it (system-scope atomic), so the host sees it without a copy or a sync. The next scan on that
+// device (or scan_check) turns it into an error instead of a silently wrong prefix.
+volatile unsigned* scan_err_word(int dev, unsigned** dev_ptr) {
+    static std::mutex mu;
+    static unsigned* host[64] = {};
+    static unsigned* devp[64] = {};
+    TORCH_CHECK(dev >= 0 && dev < 64, "scan: device index");
+    std::lock_guard<std::mutex> lock(mu);
+    if (!host[dev]) {
+        void* p = nullptr;
+        TORCH_CHECK(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess,
+                    "scan: pinned error word");
+        *static_cast<volatile unsigned*>(p) = 0u;
+        void* d = nullptr;
+        TORCH_CHECK(hipHostGetDevicePointer(&d, p, 0) == hipSuccess, "scan: mapped error word");
+        host[dev] = static_cast<unsigned*>(p), devp[dev] = static_cast<unsigned*>(d);
+    }
+    if (dev_ptr) *dev_ptr = devp[dev];
+    return host[dev];
+}
+
+void raise_pending_scan_error(int dev) {
+    volatile unsigned* w = scan_err_word(dev, nullptr);
+    if (*w) {
+        *w = 0u;
+        TORCH_CHECK(false, "pcmx::scan: an earlier scan on device ", dev, " timed out in its decoupled look-back ",
+                    "(a predecessor tile never published); that result is invalid");
+    }
+}
+
+void scan_check(int64_t device) {
+    const at::DeviceGuard g(at::Device(at::kCUDA, (c10::DeviceIndex)device));
+    TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "scan_check: device synchronize");
+    raise_pending_scan_error((int)device);
+}
+
 at::Tensor scan_out(const at::Tensor& x, at::Tensor out, bool exclusive, const c10::optional<at::Tensor>& init) {
     check_gpu(x, "x", at::kFloat), check_gpu(out, "out", at::kFloat);
     TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() == out.numel(), "scan: contiguous same-size tensors");
+    TORCH_CHECK(out.device() == x.device(), "scan: out must be on x's device");
     const at::DeviceGuard g(x.device());
+    unsigned* err_dev = nullptr;
+    scan_err_word(x.device().index(), &err_dev);
+    raise_pending_scan_error(x.device().index());
     const float* init_ptr = nullptr;
     at::Tensor init_c;
     if (init.has_value() && init->defined()) {
         check_gpu(*init, "init", at::kFloat);
+        TORCH_CHECK(init->numel() >= 1 && init->device() == x.device(), "scan: init needs >= 1 element on x's device");
         init_c = init->contiguous();
         init_ptr = init_c.data_ptr<float>();
     }
@@ -131,7 +173,7 @@ at::Tensor scan_out(const at::Tensor& x, at::Tensor out, bool exclusive, const c
     }
     auto ws = workspace(x, pcmx_scan_workspace_bytes(xc.numel()));
     check_rc(pcmx_scan_f32(xc.data_ptr<float>(), oc.data_ptr<float>(), xc.numel(), exclusive ? 1 : 0, init_ptr, ws.data_ptr(),
-                           cur_stream(x)),
+                           err_dev, cur_stream(x)),
              "scan");
     if (!oc.is_same(out)) out.copy_(oc);
     return out;
@@ -206,15 +248,18 @@ at::Tensor histeq(const at::Tensor& img) {
     auto out = at::empty_like(ic);
     const hipStream_t s = cur_stream(img);
     auto& ws = histeq_workspace(ic, s);
-    check_rc(pcmx_histeq_u8(ic.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), ic.numel(), ws.data_ptr(), s),
-             "histeq");
+    const int rc = pcmx_histeq_u8(ic.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), ic.numel(), ws.data_ptr(), s);
+    if (rc) ws.zero_();  // a failed call may leave the self-cleaning replicas/ticket dirty: re-arm before raising
+    check_rc(rc, "histeq");
     return out;
 }
 
 // ---------------------------------------------------------------- region growing
 int64_t region2d_grow_(at::Tensor region, const at::Tensor& img, int64_t thr, int64_t batch, int64_t max_launches) {
     check_u8_gpu(region, "region"), check_u8_gpu(img, "img");
-    TORCH_CHECK(region.dim() == 2 && img.sizes() == region.sizes(), "region2d: padded (H+2, W+2) uint8 tensors");
+    TORCH_CHECK(region.dim() == 2 && img.sizes() == region.sizes() && region.device() == img.device() &&
+                    img.size(0) > 2 && img.size(1) > 2,
+                "region2d: padded (H+2, W+2) uint8 tensors on one device");
     const at::DeviceGuard g(img.device());
     const int H = (int)img.size(0) - 2, W = (int)img.size(1) - 2;
     auto ws = workspace(img, pcmx_region2d_workspace_bytes(H, W));
@@ -229,8 +274,8 @@ int64_t region3d_grow_(at::Tensor region, const at::Tensor& data, int64_t thr, b
                        int64_t max_launches) {
     check_u8_gpu(region, "region"), check_u8_gpu(data, "data");
     TORCH_CHECK(data.dim() == 3 && data.size(0) == data.size(1) && data.size(1) == data.size(2) &&
-                    region.sizes() == data.sizes(),
-                "region3d: cubic uint8 volumes");
+                    region.sizes() == data.sizes() && region.device() == data.device(),
+                "region3d: cubic uint8 volumes on one device");
     const at::DeviceGuard g(data.device());
     const int dim = (int)data.size(0);
     int launches = 0;
@@ -249,8 +294,14 @@ int64_t region3d_grow_(at::Tensor region, const at::Tensor& data, int64_t thr, b
 }
 
 // ---------------------------------------------------------------- volume + ray casting
+void check_cubic(const at::Tensor& v, const char* what) {
+    TORCH_CHECK(v.dim() == 3 && v.size(0) == v.size(1) && v.size(1) == v.size(2) && v.size(0) > 1, what,
+                ": a cubic (dim, dim, dim) volume with dim > 1");
+}
+
 at::Tensor volume_gen_(at::Tensor data, int64_t seed) {
     check_u8_gpu(data, "data");
+    check_cubic(data, "volume_gen_");
     const at::DeviceGuard g(data.device());
     check_rc(pcmx_volume_gen_u8(data.data_ptr<uint8_t>(), (int)data.size(0), (unsigned)seed, cur_stream(data)), "volume_gen_");
     return data;
@@ -266,6 +317,10 @@ std::vector<float> cam_vec(at::ArrayRef<double> cam12) {
 at::Tensor raycast_global(const at::Tensor& data, const at::Tensor& region, int64_t image_dim, at::ArrayRef<double> cam12,
                           double pixel_width, double step, int64_t max_steps, bool f64_color) {
     check_u8_gpu(data, "data"), check_u8_gpu(region, "region");
+    check_cubic(data, "raycast_global");
+    TORCH_CHECK(region.sizes() == data.sizes() && region.device() == data.device(),
+                "raycast_global: region must match data's shape and device");
+    TORCH_CHECK(image_dim > 0, "raycast_global: image_dim > 0");
     const at::DeviceGuard g(data.device());
     auto img = at::empty({image_dim, image_dim}, data.options());
     auto c = cam_vec(cam12);
@@ -290,7 +345,7 @@ at::Tensor brick_pack(const at::Tensor& data, const at::Tensor& region) {
 }
 
 at::Tensor raycast_bricked(const at::Tensor& tex, int64_t image_dim, at::ArrayRef<double> cam12, double pixel_width,
-                           double step, int64_t max_steps) {
+                           double step, int64_t max_steps, int64_t batch) {
     check_gpu(tex, "tex", at::kLong);
     TORCH_CHECK(tex.dim() == 1 && tex.numel() >= 18 && tex.is_contiguous(), "raycast_bricked: tex from brick_pack");
     const int64_t nvox = (tex.numel() - 2) / 2;
@@ -301,7 +356,7 @@ at::Tensor raycast_bricked(const at::Tensor& tex, int64_t image_dim, at::ArrayRe
     auto c = cam_vec(cam12);
     check_rc(pcmx_raycast_bricked(tex.data_ptr(), (int)dim,
                                   img.data_ptr<uint8_t>(), (int)image_dim, c.data(), (float)pixel_width, (float)step,
-                                  (int)max_steps, cur_stream(tex)),
+                                  (int)max_steps, (int)batch, cur_stream(tex)),
              "raycast_bricked");
     return img;
 }
@@ -350,7 +405,7 @@ at::Tensor spmv_csr(const at::Tensor& row_ptr, const at::Tensor& col, const at::
 // slice item0[n_slices + 1]; ypart [n_slices * n_rows] and extra [n_items] are caller-owned scratch.
 at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::Tensor& val, const at::Tensor& x,
                        const at::Tensor& items, const at::Tensor& fix, const at::Tensor& meta, at::Tensor ypart,
-                       at::Tensor extra, int64_t n_rows, const c10::optional<at::Tensor>& out) {
+                       at::Tensor extra, int64_t n_rows, const c10::optional<at::Tensor>& out, int64_t mode) {
     check_gpu(lrow, "lrow", at::kShort), check_gpu(col, "col", at::kInt), check_gpu(val, "val", at::kFloat);
     check_gpu(x, "x", at::kFloat), check_gpu(items, "items", at::kLong), check_gpu(fix, "fix", at::kInt);
     check_gpu(ypart, "ypart", at::kFloat), check_gpu(extra, "extra", at::kFloat);
@@ -378,7 +433,8 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
     check_rc(pcmx_spmv_sliced(reinterpret_cast<const unsigned short*>(lrow.data_ptr<int16_t>()), col.data_ptr<int>(),
                               val.data_ptr<float>(), x.data_ptr<float>(), ypart.data_ptr<float>(), extra.data_ptr<float>(),
                               y.data_ptr<float>(), (int)n_rows, (int)x.numel(), (int)S, (const long long*)m,
-                              (const long long*)m + S, items.data_ptr(), fix.data_ptr(), (int)fix.size(0), cur_stream(val)),
+                              (const long long*)m + S, items.data_ptr(), fix.data_ptr(), (int)fix.size(0), (int)mode,
+                              cur_stream(val)),
              "spmv_sliced");
     return y;
 }
@@ -405,13 +461,20 @@ at::Tensor pack_edges(const at::Tensor& tile) {
     return buf;
 }
 
-void unpack_halo_(at::Tensor tile, const at::Tensor& buf, int64_t mask) {
+void unpack_halo_(at::Tensor tile, const at::Tensor& buf, int64_t mask, const c10::optional<at::Tensor>& changed) {
     TORCH_CHECK(tile.is_cuda() && tile.dim() == 2 && tile.is_contiguous() && buf.dtype() == tile.dtype(), "unpack_halo_");
+    TORCH_CHECK(buf.is_cuda() && buf.is_contiguous() && buf.device() == tile.device(), "unpack_halo_: buf on tile's device");
     const at::DeviceGuard g(tile.device());
     const int H = (int)tile.size(0) - 2, W = (int)tile.size(1) - 2;
     TORCH_CHECK(buf.numel() == 2 * W + 2 * H, "unpack_halo_: buffer size");
-    check_rc(pcmx_unpack_halo(tile.data_ptr(), (int)tile.element_size(), H, W, (int)tile.size(1), buf.data_ptr(), (int)mask,
-                              cur_stream(tile)),
+    int* flag = nullptr;
+    if (changed.has_value()) {
+        check_gpu(*changed, "changed", at::kInt);
+        TORCH_CHECK(changed->numel() >= 1 && changed->device() == tile.device(), "unpack_halo_: changed flag");
+        flag = changed->data_ptr<int>();
+    }
+    check_rc(pcmx_unpack_halo_changed(tile.data_ptr(), (int)tile.element_size(), H, W, (int)tile.size(1), buf.data_ptr(),
+                                      (int)mask, flag, cur_stream(tile)),
              "unpack_halo_");
 }
 
@@ -438,6 +501,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("dot(Tensor a, Tensor b) -> Tensor");
     m.def("scan(Tensor x, bool exclusive=False, Tensor? init=None) -> Tensor");
     m.def("scan_out(Tensor x, Tensor(a!) out, bool exclusive=False, Tensor? init=None) -> Tensor(a!)");
+    m.def("scan_check(int device=0) -> ()", scan_check);
     m.def("sgemm(Tensor a, Tensor b, int variant=-1) -> Tensor");
     m.def("sgemm_out(Tensor a, Tensor b, Tensor(a!) c, float alpha=1., float beta=0., int variant=-1) -> Tensor(a!)");
     m.def("sgemm_simt(Tensor a, Tensor b) -> Tensor");
@@ -448,14 +512,14 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("volume_gen_(Tensor(a!) data, int seed) -> Tensor(a!)");
     m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True) -> Tensor");
     m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
-    m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps) -> Tensor");
+    m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, int batch=4) -> Tensor");
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
-    m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None) -> Tensor");
+    m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None, int mode=0) -> Tensor");
     m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x) -> Tensor");
     m.def("pack_edges(Tensor tile) -> Tensor");
-    m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask) -> ()");
+    m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask, Tensor(b!)? changed=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
@@ -491,8 +555,4 @@ PYBIND11_MODULE(_C, mod) {
     mod.doc() = "pcmx MI355X kernels (ops live under torch.ops.pcmx)";
     mod.def("device_count", []() { return pcmx_device_count(); });
     mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr");
-    mod.def("raycast_set_batch", [](int steps) { return pcmx_raycast_set_batch(steps); }, "texture ray caster prefetch batch");
-    mod.def("spmv_set_mode", [](int mode) { return pcmx_spmv_set_mode(mode); }, "sliced SpMV lab knob (0 = normal)");
-    mod.def("sgemm_set_tuning", [](int order, int diag) { return pcmx_sgemm_set_tuning(order, diag); });
-    mod.def("scan_set_rows", [](int rows) { return pcmx_scan_set_rows(rows); }, "scan tile shape: f32x4 rows per lane (16 = 8 waves, 8 = 16 waves)");
 }

@@ -5,6 +5,8 @@ Artefacts (all git-ignored, all shipped to the GPU box by gpurun's snapshot):
   parallel_c_programs_amd/lib/libpcmx_hip.so   HIP kernels for gfx950 + C-ABI launchers + device runtime
   parallel_c_programs_amd/_C.so                torch op registrations (TORCH_LIBRARY(pcmx, ...))
   bin/<tool>                                   reference-style CLIs (spmv, histogram_*, matrix_demo, ...)
+  parallel_c_programs_amd/lib/libpcmx_faultinj.so  TEST ONLY: kernels built with -DPCMX_FAULT_INJECT (a forced
+                                               scan look-back stall) so tests can observe the error paths
 
 Everything is compiled for gfx950 only (`--offload-arch=gfx950`). Native libraries link the HIP runtime
 that ships inside torch (torch/lib/libamdhip64.so, same SONAME as /opt/rocm's) with an rpath to it, so a
@@ -120,6 +122,30 @@ def build_hip(force=False, jobs=8):
     return so
 
 
+FAULT_SRCS = ["kernels/scan.hip"]
+
+
+def build_faultinj(force=False):
+    """Test-only library: the same kernel sources compiled with -DPCMX_FAULT_INJECT (never loaded by the package)."""
+    _, tlib, _ = _torch_paths()
+    (OBJ / "fault").mkdir(parents=True, exist_ok=True)
+    so = LIB / "libpcmx_faultinj.so"
+    hdrs = _headers()
+    objs = []
+    todo = []
+    for s in FAULT_SRCS:
+        o = OBJ / "fault" / (s.replace("/", "_") + ".o")
+        objs.append(o)
+        if force or _newer(o, [CSRC / s, *hdrs]):
+            todo.append([HIPCC, *HIPFLAGS, "-DPCMX_FAULT_INJECT", "-c", str(CSRC / s), "-o", str(o)])
+    for cmd in todo:
+        _run(cmd)
+    if force or todo or not so.exists():
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(so), *map(str, objs), f"-L{tlib}", "-lamdhip64",
+              f"-Wl,-rpath,{tlib}"])
+    return so
+
+
 def build_torch(force=False):
     incs, tlib, torch = _torch_paths()
     src = CSRC / "torch" / "ops.cpp"
@@ -185,7 +211,7 @@ def build_bin(force=False, jobs=8):
 
 def build_all(force=False, jobs=None, only=None):
     jobs = jobs or min(8, os.cpu_count() or 4)
-    steps = only or ["cpu", "hip", "torch", "bin"]
+    steps = only or ["cpu", "hip", "torch", "bin", "test"]
     if "cpu" in steps:
         build_cpu(force, jobs)
     if "hip" in steps:
@@ -194,13 +220,15 @@ def build_all(force=False, jobs=None, only=None):
         build_torch(force)
     if "bin" in steps:
         build_bin(force, jobs)
+    if "test" in steps:
+        build_faultinj(force)
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
-    ap.add_argument("--only", action="append", choices=["cpu", "hip", "torch", "bin"])
+    ap.add_argument("--only", action="append", choices=["cpu", "hip", "torch", "bin", "test"])
     a = ap.parse_args(argv)
     build_all(a.force, a.jobs, a.only)
     print("pcmx build ok")

@@ -16,19 +16,27 @@ def pack_edges(tile: torch.Tensor) -> torch.Tensor:
     return torch.cat([tile[1, 1:-1], tile[-2, 1:-1], tile[1:-1, 1], tile[1:-1, -2]]).contiguous()
 
 
-def unpack_halo_(tile: torch.Tensor, buf: torch.Tensor, mask: int = TOP | BOTTOM | LEFT | RIGHT) -> torch.Tensor:
+def unpack_halo_(tile: torch.Tensor, buf: torch.Tensor, mask: int = TOP | BOTTOM | LEFT | RIGHT,
+                 changed: torch.Tensor | None = None) -> torch.Tensor:
+    """Scatter `buf` into the halo ring; `changed` (int32 [1], same device) is set to 1 when any halo cell takes a
+    new value (device-resident change detection: nothing is read back to the host)."""
     if tile.is_cuda:
-        ops().unpack_halo_(tile, buf, int(mask))
+        ops().unpack_halo_(tile, buf, int(mask), changed)
         return tile
     H, W = tile.shape[0] - 2, tile.shape[1] - 2
+    parts = []
     if mask & TOP:
-        tile[0, 1:-1] = buf[:W]
+        parts.append((tile[0, 1:-1], buf[:W]))
     if mask & BOTTOM:
-        tile[-1, 1:-1] = buf[W:2 * W]
+        parts.append((tile[-1, 1:-1], buf[W:2 * W]))
     if mask & LEFT:
-        tile[1:-1, 0] = buf[2 * W:2 * W + H]
+        parts.append((tile[1:-1, 0], buf[2 * W:2 * W + H]))
     if mask & RIGHT:
-        tile[1:-1, -1] = buf[2 * W + H:]
+        parts.append((tile[1:-1, -1], buf[2 * W + H:]))
+    for dst, src in parts:
+        if changed is not None and not torch.equal(dst, src):
+            changed.fill_(1)
+        dst.copy_(src)
     return tile
 
 

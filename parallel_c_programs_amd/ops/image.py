@@ -182,12 +182,13 @@ def default_camera(image_dim: int) -> Camera:
 
 
 def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, method: str = "global",
-            cam: Camera | None = None) -> torch.Tensor:
+            cam: Camera | None = None, batch: int = 4) -> torch.Tensor:
     """Render the volume (ray marching, trilinear sampling of data and region).
 
     method: "global" — bit-compatible with the reference's serial/global-memory caster (f64 colour update);
             "global_f32" — f32 colour update like the CUDA kernel; "texture" — the texture path
-            (texel-centre addressing, correct weights, 8-bit fractional weights) on a packed brick volume.
+            (texel-centre addressing, correct weights, 8-bit fractional weights) on a packed brick volume;
+            `batch` = its march steps per prefetch batch (1, 4, 8, 16: same image, 4 is fastest).
     """
     cam = cam or default_camera(image_dim)
     if not data.is_cuda:
@@ -204,5 +205,5 @@ def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, meth
     if method == "texture":
         tex = o.brick_pack(data, region)
         return o.raycast_bricked(tex, int(image_dim), cam.cam12(), float(cam.pixel_width), float(cam.step_size),
-                                 int(cam.max_steps))
+                                 int(cam.max_steps), int(batch))
     raise ValueError(f"unknown raycast method {method!r}")

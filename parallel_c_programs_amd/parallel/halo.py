@@ -32,8 +32,9 @@ class HaloExchanger2D:
         m |= RIGHT if self.nb["east"] >= 0 else 0
         return m
 
-    def exchange_(self, tile: torch.Tensor) -> torch.Tensor:
-        """In-place halo update of `tile`; returns the received edge buffer (for change detection)."""
+    def exchange_(self, tile: torch.Tensor, changed: torch.Tensor | None = None) -> torch.Tensor:
+        """In-place halo update of `tile`; returns the received edge buffer. `changed` (int32 [1]) is raised to 1
+        on the device when any halo cell takes a new value."""
         H, W = tile.shape[0] - 2, tile.shape[1] - 2
         send = pack_edges(tile)
         recv = torch.zeros_like(send)
@@ -61,5 +62,5 @@ class HaloExchanger2D:
                 req.wait()
         for side, (buf, sl) in recv_parts.items():
             recv[sl] = buf
-        unpack_halo_(tile, recv, self.mask())
+        unpack_halo_(tile, recv, self.mask(), changed)
         return recv

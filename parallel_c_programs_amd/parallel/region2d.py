@@ -10,8 +10,10 @@ MI355X design (one process per GPU, RCCL over xGMI):
     (many sweeps per launch; SURVEY §7.5 hard part 2) — the reference's DFS flood fill (region.c:499-527).
   * exchange: pack 4 edges -> one grouped RCCL send/recv -> unpack (parallel/halo.py); the halo region
     cells act as seeds for the next local step (ref add_halo_to_stack :355).
-  * termination: one MAX all-reduce of "did any halo cell change" per outer step (ref finished() :435
-    all-reduces MIN of local_finish).
+  * termination: device-resident. The unpack kernel raises a "halo changed" flag on the device, the flag is
+    MAX-all-reduced in place, and the host reads it once every CHECK_EVERY outer steps (ref finished() :435
+    all-reduces MIN of local_finish every step). A window in which no rank's halo changed is a global fixpoint:
+    a step whose halos did not change cannot grow anything, so every later step is a no-op too.
   * gather: each rank sends its interior once; root places the blocks (ref gather_region :391, B10).
 
 Generalises the reference to any world size (B8: 1/2/4/8 ranks on a node, any image size).
@@ -29,9 +31,7 @@ from .halo import HaloExchanger2D
 from .topology import CartTopology
 
 
-def _halo_count(reg_p: torch.Tensor) -> torch.Tensor:
-    return (reg_p[0].sum(dtype=torch.int32) + reg_p[-1].sum(dtype=torch.int32)
-            + reg_p[1:-1, 0].sum(dtype=torch.int32) + reg_p[1:-1, -1].sum(dtype=torch.int32))
+CHECK_EVERY = 2  # outer steps per host read of the all-reduced "halo changed" flag
 
 
 def _bcast_shape(ctx: Context, image: torch.Tensor | None) -> tuple[int, int]:
@@ -95,18 +95,21 @@ def grow_distributed(ctx: Context, image: torch.Tensor | None, threshold: int = 
         if r0 <= y < r1 and c0 <= x < c1:
             reg_p[y - r0 + 1, x - c0 + 1] = 1
     ex = HaloExchanger2D(ctx, topo)
-    outer, launches = 0, 0
+    outer, launches, reads = 0, 0, 0
+    changed = torch.zeros(1, dtype=torch.int32, device=ctx.device)
     while True:
         launches += ops.region2d_grow_padded_(reg_p, img_p, threshold)
         outer += 1
         if not ctx.distributed:
             break
-        before = _halo_count(reg_p)
-        ex.exchange_(reg_p)
-        changed = (_halo_count(reg_p) - before).reshape(1)
+        ex.exchange_(reg_p, changed)
+        if outer % CHECK_EVERY:
+            continue
         ctx.all_reduce_(changed, "max")
-        if int(changed.item()) == 0:
+        reads += 1
+        if int(changed.item()) == 0:  # the loop's only host read-back
             break
+        changed.zero_()
     if stats is not None:
-        stats.update(outer_steps=outer, launches=launches, dims=topo.dims)
+        stats.update(outer_steps=outer, launches=launches, dims=topo.dims, host_reads=reads)
     return gather_tiles(ctx, topo, reg_p[1:-1, 1:-1], H, W)

@@ -5,7 +5,7 @@ import sys
 import torch
 
 sys.path.insert(0, ".")
-from parallel_c_programs_amd import _C, ops  # noqa: E402
+from parallel_c_programs_amd import ops  # noqa: E402
 from parallel_c_programs_amd._native import ops as native  # noqa: E402
 from parallel_c_programs_amd.ops.image import default_camera  # noqa: E402
 
@@ -16,9 +16,9 @@ tex = native().brick_pack(vol, (reg != 0).to(torch.uint8))
 cam = default_camera(512)
 
 
-def run(max_steps=None):
+def run(max_steps=None, batch=4):
     return native().raycast_bricked(tex, 512, cam.cam12(), float(cam.pixel_width), float(cam.step_size),
-                                    int(max_steps or cam.max_steps))
+                                    int(max_steps or cam.max_steps), batch)
 
 
 def timeit(fn, reps=10):
@@ -41,13 +41,12 @@ for ms in (1000, 2000, 3000, 4000, 5000):
 
 ref = None
 for b in (1, 4, 8, 16):
-    _C.raycast_set_batch(b)
     for _ in range(2):
-        img = run()
+        img = run(batch=b)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(10):
-        run()
+        run(batch=b)
     e1.record()
     torch.cuda.synchronize()
     ref = img if ref is None else ref

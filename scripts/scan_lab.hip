@@ -15,8 +15,10 @@
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 
-extern "C" int pcmx_scan_set_rows(int rows);
+extern "C" int pcmx_scan_f32_rows(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* ws,
+                                  unsigned* err_flag, int rows, hipStream_t s);
 extern "C" int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* ws,
+                             unsigned* err_flag,
                              hipStream_t s);
 
 using pcmx::f32x4;
@@ -401,8 +403,7 @@ int main(int argc, char** argv) {
     PIPE(12, 16, 1, 1) PIPE(12, 16, 1, 2) PIPE(10, 16, 1, 2) PIPE(14, 8, 1, 2) PIPE(20, 8, 1, 2) PIPE(6, 16, 1, 2)
     PIPE(8, 8, 2, 2) PIPE(12, 8, 1, 2)
     for (int rows : {4, 8, 16}) {
-        pcmx_scan_set_rows(rows);
-        float ms = time_ms([&] { pcmx_scan_f32(x, y, n, 0, nullptr, ws, 0); });
+        float ms = time_ms([&] { pcmx_scan_f32_rows(x, y, n, 0, nullptr, ws, nullptr, rows, 0); });
         printf("lib scan rows=%2d      %7.3f ms %7.1f GB/s\n", rows, ms, gb / ms * 1e3);
     }
     check();

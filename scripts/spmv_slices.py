@@ -13,29 +13,30 @@ S = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 HEAD = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0625
 ctx = init(None, None)
 d = DistributedSpMV.powerlaw(ctx, 10_000_000, 100_000_000, 2.5, slices=S, head=HEAD)
-s = d.sliced
+s = d.parts[0][2]  # one rank, one chunk: the whole matrix
 x = torch.rand(s.n_cols, device="cuda")
+
+
+MODE = 0
 
 
 def bench(meta, reps=20):
     for _ in range(3):
-        native().spmv_sliced(s.lrow, s.col, s.val, x, s.items, s.fix, meta, s.ypart, s.extra, s.n_rows)
+        native().spmv_sliced(s.lrow, s.col, s.val, x, s.items, s.fix, meta, s.ypart, s.extra, s.n_rows, None, MODE)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        native().spmv_sliced(s.lrow, s.col, s.val, x, s.items, s.fix, meta, s.ypart, s.extra, s.n_rows)
+        native().spmv_sliced(s.lrow, s.col, s.val, x, s.items, s.fix, meta, s.ypart, s.extra, s.n_rows, None, MODE)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
 
 
-from parallel_c_programs_amd import _C  # noqa: E402
-
 for mode, what in [(1 | 2 << 8, "no x gathers"), (1 << 8, "1 block/CU"), (2 << 8, "2 blocks/CU"),
                    (3 << 8, "3 blocks/CU"), (4 << 8, "4 blocks/CU")]:
-    _C.spmv_set_mode(mode)
+    MODE = mode
     print(f"mode {mode} ({what}): {bench(s.meta):.3f} ms")
-_C.spmv_set_mode(2 << 8)
+MODE = 0
 full = bench(s.meta)
 print(f"S={S} head={HEAD} H={s.head_cols} all slices: {full:.3f} ms  bounds={s.bounds.tolist()}")
 nz0, item0 = s.meta[:S], s.meta[S:]
