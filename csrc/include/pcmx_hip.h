@@ -86,13 +86,12 @@ int pcmx_scan_check(const void* workspace, hipStream_t s);
  * kernel), K%32==0, 16-B aligned rows; anything else returns -1 (the torch layer pads). */
 int pcmx_sgemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
                    float alpha, float beta, hipStream_t s);
-/* tile selection used by pcmx_sgemm_f32: 0 = 256x256x32 / 8 waves, 1 = 128x128x32 / 4 waves */
+/* explicit kernel: 16 = register-staged 256x256x32 / 8 waves (large problems), 0 = LDS-DMA 256x256x32 / 8 waves,
+ * 1 = LDS-DMA 128x128x32 / 4 waves (the lab variants live in scripts/sgemm_lab.hip) */
 int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
                            int ldc, float alpha, float beta, int variant, hipStream_t s);
 /* Reference-style f32 VALU GEMM (one thread per output, LDS tiles) for A/B comparisons. */
 int pcmx_sgemm_f32_simt(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t s);
-/* tile order (remap<<8 | group_m) and the L2-resident timing diagnostic (k0_diag=0) — tuning only */
-int pcmx_sgemm_set_tuning(int tile_order, int k0_diag);
 
 /* ---------------------------------------------------------------- histogram equalisation */
 /* out = tf[img] (bit-identical to the serial reference). ws: pcmx_histeq_workspace_bytes(), 16-B aligned, ZEROED

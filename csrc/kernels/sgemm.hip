@@ -1,23 +1,23 @@
 // FP32 SGEMM on the gfx950 matrix cores — the headline "TFLOPS SGEMM 8192^2" kernel.
 // Reference ancestor: matrix_multiply, ref 1-introduction/matrix.c:63-81 (naive i-j-k on float**).
 //
+// Production kernels only (every experimental variant and tuning knob lives in scripts/sgemm_lab.hip):
+//   variant 16  register-staged 256x256x32 tile, 8 waves (2 per SIMD, 64x128 wave tiles) — large problems
+//   variant 0   LDS-DMA 256x256x32 tile, 8 waves — fallback when buffer offsets would exceed 2 GiB
+//   variant 1   LDS-DMA 128x128x32 tile, 4 waves — problems with fewer than 192 256x256 tiles (fills 256 CUs)
+//   simt        reference-style f32 VALU GEMM (the "CUDA port recompiled" baseline), any shape
+//
 // Why this shape (MI355X_MICROARCH.md "Matrix cores", cdna_hip_programming.md §3/§5):
 //  * v_mfma_f32_32x32x2_f32 is exact f32 (a k-ordered fmaf chain) at 64 FLOP/clk/SIMD = the f32 peak
-//    (157 TF); one VGPR per operand per lane, so operand traffic is tiny and the kernel is MFMA-bound
-//    as long as the issue stream stays clean.
-//  * 256x256x32 block tile, 8 waves as 2(M) x 4(N), each wave 128x64 = 4x2 MFMA tiles (128 accumulator
-//    registers) -> 2 waves per SIMD at <=256 registers. Per 32-deep K-step one block issues 1024 MFMAs
-//    (16k SIMD-cycles) against 64 KiB of staging, so load latency hides completely.
-//  * Global->LDS with global_load_lds_dwordx4 (1 KiB per wave instruction, no VGPR round trip), two LDS
-//    stages (128 KiB in ONE __shared__ array). The LDS image is lane-linear, so the bank-conflict swizzle
-//    of the A tile is applied to the SOURCE address and undone on the ds_read_b128 (rule 21):
-//    slot = chunk ^ ((row>>1)&7) puts every 16-lane group of a ds_read_b128 on 16 distinct 16-B slots.
-//  * K-permutation: the MFMA's two k-slots (h = lane>>5) are fed k = 8c+4h+s at step s, so ONE
-//    ds_read_b128 delivers a lane's A operands for 4 MFMA steps; B is read row-wise with conflict-free
-//    ds_read_b32 (32 lanes -> 32 consecutive floats). A and B agree on the permutation, so the sum is
-//    the full K sum.
-//  * XCD-aware bijective block remap (T1) + grouped tile order: the blocks resident on one XCD share
-//    A/B panels in that XCD's L2.
+//    (157 TF); one VGPR per operand per lane, so operand traffic is tiny and the kernel is MFMA-bound as long
+//    as the issue stream stays clean.
+//  * K-permutation: the MFMA's two k-slots (h = lane>>5) are fed k = 8c+4h+s at step s, so ONE ds_read_b128
+//    delivers a lane's A operands for 4 MFMA steps. A and B agree on the permutation, so the sum is the full
+//    K sum.
+//  * A-tile bank-conflict swizzle: slot = chunk ^ ((row>>1)&7) puts every 16-lane group of a ds_read_b128
+//    on 16 distinct 16-B slots.
+//  * XCD-aware bijective block remap + grouped tile order (8 tile-rows per column strip): the blocks resident
+//    on one XCD share A/B panels in that XCD's L2.
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 
@@ -25,6 +25,7 @@ namespace {
 using pcmx::kWave;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) float lds_float;
+typedef __attribute__((address_space(3))) pcmx::f32x4 lds_f4;
 
 template <int BM_, int BN_, int WM_, int WN_>
 struct Cfg {
@@ -37,16 +38,31 @@ struct Cfg {
     static constexpr int kStage = kAFloats + kBFloats;
     static constexpr int kAPieces = kAFloats / 256, kBPieces = kBFloats / 256;  // 1-KiB DMA pieces
     static constexpr int kBLanesPerRow = BN / 4;                               // 16-B chunks per B k-row
-    static constexpr int kGroupM = 8;
     static_assert(kAPieces % kWaves == 0 && kBPieces % kWaves == 0, "DMA pieces must split over waves");
     static_assert(BN <= 256 && 256 % BN == 0, "a B piece holds whole k-rows");
     static_assert(MT >= 1 && NT >= 1, "wave tile must hold a 32x32 MFMA tile");
 };
+using Big = Cfg<256, 256, 2, 4>;
+using Small = Cfg<128, 128, 2, 2>;
 
-// 16-B global->LDS DMA issued from inline asm: hipcc does not count asm memory ops, so it cannot insert
-// the conservative `s_waitcnt vmcnt(0)` it emits before every ds_read that *might* alias an in-flight
-// builtin LDS-DMA (observed in the .s). The kernel waits for the DMA itself (vmcnt(0) + barrier) once per
-// K-step. M0 is set and restored inside the same statement (cdna_hip_programming.md §5.7).
+// Tile of block blockIdx.x: XCD remap (blocks dealt to one XCD get consecutive ids), then column strips 8
+// tile-rows tall (any bijection is correct; this order keeps an XCD's concurrent tiles on shared panels).
+template <int BM, int BN>
+__device__ __forceinline__ void tile_coords(int M, int N, int& m0, int& n0) {
+    constexpr int kGroupM = 8;
+    const int tiles_m = M / BM, tiles_n = N / BN;
+    const int t = pcmx::xcd_remap((int)blockIdx.x, tiles_m * tiles_n);
+    const int per_group = kGroupM * tiles_n;
+    const int first_m = (t / per_group) * kGroupM;
+    const int gsz = min(tiles_m - first_m, kGroupM);
+    m0 = (first_m + (t % per_group) % gsz) * BM;
+    n0 = ((t % per_group) / gsz) * BN;
+}
+
+// 16-B global->LDS DMA issued from inline asm: hipcc does not count asm memory ops, so it cannot insert the
+// conservative `s_waitcnt vmcnt(0)` it emits before every ds_read that *might* alias an in-flight builtin
+// LDS-DMA. The kernel waits for the DMA itself (vmcnt(0) + barrier) once per K-step. M0 is set and restored
+// inside the same statement (cdna_hip_programming.md §5.7).
 __device__ __forceinline__ void glds16(const float* gsrc, lds_float* lds_base) {
     const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_base);
     unsigned keep;
@@ -61,6 +77,7 @@ __device__ __forceinline__ void glds16(const float* gsrc, lds_float* lds_base) {
         : "memory");
 }
 
+// One K-step stage of A (swizzle applied to the SOURCE chunk, the LDS image is lane-linear) and B.
 template <class C>
 __device__ __forceinline__ void stage_load(const float* __restrict__ A, const float* __restrict__ B, int lda, int ldb,
                                            int m0, int n0, int k0, lds_float* sA, lds_float* sB, int wave, int lane) {
@@ -80,37 +97,14 @@ __device__ __forceinline__ void stage_load(const float* __restrict__ A, const fl
     }
 }
 
-// Tile order (a speed choice only — any bijection is correct). order = remap<<8 | group_m:
-// remap=1 applies the bijective XCD remap, group_m>0 walks tiles in column strips group_m rows tall.
-__constant__ int g_tile_order = (1 << 8) | 8;
-__constant__ int g_k0_diag = 1;  // 0: every stage re-reads k0=0 (L2-resident timing diagnostic only)
-
-template <class C>
-__device__ __forceinline__ void tile_coords(int M, int N, int& m0, int& n0) {
-    const int tiles_m = M / C::BM, tiles_n = N / C::BN;
-    const int nwg = tiles_m * tiles_n;
-    const int order = g_tile_order;
-    const int t = (order >> 8) ? pcmx::xcd_remap((int)blockIdx.x, nwg) : (int)blockIdx.x;
-    const int group_m = order & 0xff;
-    if (group_m == 0) {
-        m0 = (t / tiles_n) * C::BM;
-        n0 = (t % tiles_n) * C::BN;
-        return;
-    }
-    const int per_group = group_m * tiles_n;
-    const int g = t / per_group;
-    const int first_m = g * group_m;
-    const int gsz = min(tiles_m - first_m, group_m);
-    const int tm = first_m + (t % per_group) % gsz;
-    const int tn = (t % per_group) / gsz;
-    m0 = tm * C::BM;
-    n0 = tn * C::BN;
-}
-
-template <class C, bool BETA, bool PIPE>
-__global__ __launch_bounds__(C::kThreads) void sgemm_mfma_kernel(const float* __restrict__ A, const float* __restrict__ B,
-                                                                float* __restrict__ Cmat, int M, int N, int K, int lda,
-                                                                int ldb, int ldc, float alpha, float beta) {
+// ---------------------------------------------------------------------------------------------------
+// Variants 0 / 1: LDS-DMA staging (global_load_lds_dwordx4, 1 KiB per wave instruction, no VGPR round trip),
+// two LDS stages, rotated schedule: fragments of step kc+1 are read while the MFMAs of step kc run; the barrier
+// that publishes stage t+1 sits between the LAST fragment reads of stage t and the first reads of stage t+1.
+template <class C, bool BETA>
+__global__ __launch_bounds__(C::kThreads) void sgemm_dma_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                               float* __restrict__ Cmat, int M, int N, int K, int lda,
+                                                               int ldb, int ldc, float alpha, float beta) {
     __shared__ __attribute__((aligned(16))) float smem[2 * C::kStage];
     lds_float* lds = (lds_float*)smem;
     const int lane = pcmx::lane_id();
@@ -118,17 +112,14 @@ __global__ __launch_bounds__(C::kThreads) void sgemm_mfma_kernel(const float* __
     const int wm = wave / C::WN, wn = wave % C::WN;
     const int h = lane >> 5, l32 = lane & 31;
     int m0, n0;
-    tile_coords<C>(M, N, m0, n0);
+    tile_coords<C::BM, C::BN>(M, N, m0, n0);
 
     f32x16 acc[C::MT][C::NT];
 #pragma unroll
     for (int i = 0; i < C::MT; ++i)
 #pragma unroll
         for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x16{0};
-
-    // per-lane LDS read offsets (floats) inside a stage
-    int a_row_off[C::MT];
-    int a_swz[C::MT];
+    int a_row_off[C::MT], a_swz[C::MT];
 #pragma unroll
     for (int i = 0; i < C::MT; ++i) {
         const int r = wm * C::kWaveM + i * 32 + l32;
@@ -142,86 +133,40 @@ __global__ __launch_bounds__(C::kThreads) void sgemm_mfma_kernel(const float* __
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    if constexpr (PIPE) {
-        // Rotated schedule: fragments of step kc+1 are read while the MFMAs of step kc run; the barrier
-        // that publishes stage t+1 sits between the LAST fragment reads of stage t (retired by the
-        // barrier's lgkmcnt(0)) and the first reads of stage t+1, so the MFMA pipe never waits on LDS.
-        pcmx::f32x4 fa0[C::MT], fa1[C::MT];
-        float fb0[C::NT][4], fb1[C::NT][4];
-        auto read = [&](const lds_float* stage, int kc, pcmx::f32x4(&a)[C::MT], float(&b)[C::NT][4]) {
-            const lds_float* sA = stage;
-            const lds_float* sB = stage + C::kAFloats;
+    pcmx::f32x4 fa0[C::MT], fa1[C::MT];
+    float fb0[C::NT][4], fb1[C::NT][4];
+    auto read = [&](const lds_float* stage, int kc, pcmx::f32x4(&a)[C::MT], float(&b)[C::NT][4]) {
+        const lds_float* sB = stage + C::kAFloats;
 #pragma unroll
-            for (int i = 0; i < C::MT; ++i) {
-                const int slot = (2 * kc + h) ^ a_swz[i];
-                a[i] = *(const __attribute__((address_space(3))) pcmx::f32x4*)(sA + a_row_off[i] + slot * 4);
-            }
+        for (int i = 0; i < C::MT; ++i) a[i] = *(const lds_f4*)(stage + a_row_off[i] + ((2 * kc + h) ^ a_swz[i]) * 4);
 #pragma unroll
-            for (int j = 0; j < C::NT; ++j)
+        for (int j = 0; j < C::NT; ++j)
 #pragma unroll
-                for (int s = 0; s < 4; ++s) b[j][s] = sB[(kc * 8 + 4 * h + s) * C::BN + b_col + j * 32];
-        };
-        auto mma = [&](const pcmx::f32x4(&a)[C::MT], const float(&b)[C::NT][4]) {
+            for (int s = 0; s < 4; ++s) b[j][s] = sB[(kc * 8 + 4 * h + s) * C::BN + b_col + j * 32];
+    };
+    auto mma = [&](const pcmx::f32x4(&a)[C::MT], const float(&b)[C::NT][4]) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-                for (int i = 0; i < C::MT; ++i)
+            for (int i = 0; i < C::MT; ++i)
 #pragma unroll
-                    for (int j = 0; j < C::NT; ++j) {
-                        const float av = s == 0 ? a[i].x : (s == 1 ? a[i].y : (s == 2 ? a[i].z : a[i].w));
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[j][s], acc[i][j], 0, 0, 0);
-                    }
-        };
-        read(lds, 0, fa0, fb0);
-        for (int t = 0; t < nk; ++t) {
-            lds_float* cur = lds + (t & 1) * C::kStage;
-            lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
-            if (t + 1 < nk) stage_load<C>(A, B, lda, ldb, m0, n0, (t + 1) * C::BK, nxt, nxt + C::kAFloats, wave, lane);
-            read(cur, 1, fa1, fb1);
-            mma(fa0, fb0);
-            read(cur, 2, fa0, fb0);
-            mma(fa1, fb1);
-            read(cur, 3, fa1, fb1);
-            mma(fa0, fb0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (t + 1 < nk) read(nxt, 0, fa0, fb0);
-            mma(fa1, fb1);
-        }
-    } else
+                for (int j = 0; j < C::NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+    };
+    read(lds, 0, fa0, fb0);
     for (int t = 0; t < nk; ++t) {
         lds_float* cur = lds + (t & 1) * C::kStage;
-        if (t + 1 < nk) {
-            lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
-            stage_load<C>(A, B, lda, ldb, m0, n0, (t + 1) * C::BK, nxt, nxt + C::kAFloats, wave, lane);
-        }
-        const lds_float* sA = cur;
-        const lds_float* sB = cur + C::kAFloats;
-#pragma unroll
-        for (int kc = 0; kc < C::BK / 8; ++kc) {
-            pcmx::f32x4 a[C::MT];
-            float b[C::NT][4];
-#pragma unroll
-            for (int i = 0; i < C::MT; ++i) {
-                const int slot = (2 * kc + h) ^ a_swz[i];
-                a[i] = *(const __attribute__((address_space(3))) pcmx::f32x4*)(sA + a_row_off[i] + slot * 4);
-            }
-#pragma unroll
-            for (int j = 0; j < C::NT; ++j)
-#pragma unroll
-                for (int s = 0; s < 4; ++s) b[j][s] = sB[(kc * 8 + 4 * h + s) * C::BN + b_col + j * 32];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-                    for (int j = 0; j < C::NT; ++j) {
-                        const float av = s == 0 ? a[i].x : (s == 1 ? a[i].y : (s == 2 ? a[i].z : a[i].w));
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[j][s], acc[i][j], 0, 0, 0);
-                    }
-        }
+        lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
+        if (t + 1 < nk) stage_load<C>(A, B, lda, ldb, m0, n0, (t + 1) * C::BK, nxt, nxt + C::kAFloats, wave, lane);
+        read(cur, 1, fa1, fb1);
+        mma(fa0, fb0);
+        read(cur, 2, fa0, fb0);
+        mma(fa1, fb1);
+        read(cur, 3, fa1, fb1);
+        mma(fa0, fb0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (t + 1 < nk) read(nxt, 0, fa0, fb0);
+        mma(fa1, fb1);
     }
 
     // epilogue: lane holds column l32 and rows (r&3) + 8*(r>>2) + 4*h of each 32x32 tile
@@ -233,16 +178,192 @@ __global__ __launch_bounds__(C::kThreads) void sgemm_mfma_kernel(const float* __
             const int rbase = m0 + wm * C::kWaveM + i * 32 + 4 * h;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = rbase + (r & 3) + 8 * (r >> 2);
-                float* p = Cmat + (size_t)row * ldc + col;
+                float* p = Cmat + (size_t)(rbase + (r & 3) + 8 * (r >> 2)) * ldc + col;
                 const float v = alpha * acc[i][j][r];
                 *p = BETA ? v + beta * (*p) : v;
             }
         }
 }
 
-// Reference-style SIMT kernel (f32 VALU FMAs, 64x64 LDS tiles, 4x4 outputs per thread) — the
-// "CUDA port recompiled" baseline the MFMA kernel is compared against. Any shape.
+// ---------------------------------------------------------------------------------------------------
+// Variant 16 (production for large problems): register-staged, 8 waves (2 per SIMD) as 4(M) x 2(N), wave tile
+// 64x128 = 2x4 MFMA tiles (128 accumulators in VGPRs): the second wave of a SIMD issues MFMAs while the other
+// waits at the per-stage barrier. Every LDS access is 16 B wide.
+//  * Staging: buffer_load_dwordx4 (one SRD per operand, 32-bit voffset + scalar soffset) into 8 x 16-B
+//    registers, ds_write_b128 into the other LDS stage. Loads run TWO stages ahead (the registers holding
+//    stage t+1 are written to LDS during stage t and immediately reloaded with stage t+2), so HBM/L2 latency
+//    never reaches the MFMA stream. (The LDS-DMA form of the same kernel loses ~5% to DMA issue cost.)
+//  * B columns are interleaved across the wave's 4 N-tiles (tile j owns columns 4c+j), so ONE ds_read_b128 of a
+//    B row yields the operands of all 4 tiles for one k (no transpose, conflict-free) and the epilogue stores
+//    16 B per lane (512 contiguous bytes per row).
+//  * Each staging piece (ds_write + buffer load) is pinned between MFMA groups (sched_barrier) in chunks 0-1
+//    of the stage, so it issues in the MFMA shadow. (Spreading them over all 4 chunks is a race: chunk 3 runs
+//    after the barrier while other waves already read `nxt`.)
+struct CfgRS8 {
+    static constexpr int BM = 256, BN = 256, BK = 32, WM = 4, WN = 2;
+    static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
+    static constexpr int kWaveM = BM / WM, kWaveN = BN / WN;
+    static constexpr int MT = kWaveM / 32, NT = kWaveN / 32;
+    static constexpr int kAFloats = BM * BK, kBFloats = BK * BN;
+    static constexpr int kStage = kAFloats + kBFloats;
+    static constexpr int kAPW = BM / 8 / kWaves;  // A pieces (8 rows x 128 B) per wave
+    static constexpr int kBPW = BK / kWaves;      // B pieces (one 1-KiB k-row) per wave
+    static_assert(NT == 4, "interleaved-column B read assumes 4 N-tiles per wave");
+};
+
+template <bool BETA>
+__global__ __launch_bounds__(CfgRS8::kThreads, 1) void sgemm_rs_kernel(const float* __restrict__ A,
+                                                                      const float* __restrict__ B,
+                                                                      float* __restrict__ Cmat, int M, int N, int K,
+                                                                      int lda, int ldb, int ldc, float alpha, float beta) {
+    using C = CfgRS8;
+    __shared__ __attribute__((aligned(16))) float smem[2 * C::kStage];
+    lds_float* lds = (lds_float*)smem;
+    const int lane = pcmx::lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int h = lane >> 5, l32 = lane & 31;
+    int m0, n0;
+    tile_coords<C::BM, C::BN>(M, N, m0, n0);
+
+    // buffer resources: A rows of this block, B columns of this block (bounds = whole K extent)
+    const __amdgpu_buffer_rsrc_t rA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, C::BM * lda * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)(B + n0), (short)0, K * ldb * 4, 0x00020000);
+    const int voA = ((lane >> 3) * lda + (lane & 7) * 4) * 4;
+    const int voB = lane * 16;
+    int lwA[C::kAPW];  // LDS byte addresses of this lane's A pieces (identical every stage up to the stage base)
+#pragma unroll
+    for (int i = 0; i < C::kAPW; ++i) {
+        const int r = (wave * C::kAPW + i) * 8 + (lane >> 3);
+        lwA[i] = r * C::BK * 4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16);
+    }
+    const int lwB = (C::kAFloats + wave * C::kBPW * C::BN) * 4 + lane * 16;
+
+    pcmx::f32x4 R[C::kAPW + C::kBPW];
+    auto gload = [&](int q, int k0) {  // piece q (A pieces first, then B) of the stage starting at k0
+        if (q < C::kAPW) {
+            const int so = ((wave * C::kAPW + q) * 8 * lda + k0) * 4;
+            R[q] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, voA, so, 0));
+        } else {
+            const int so = (k0 + wave * C::kBPW + (q - C::kAPW)) * ldb * 4;
+            R[q] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, voB, so, 0));
+        }
+    };
+    typedef __attribute__((address_space(3))) char lds_char;
+    auto lwrite = [&](int q, lds_float* stage) {
+        lds_char* base = (lds_char*)stage;
+        if (q < C::kAPW)
+            *(lds_f4*)(base + lwA[q]) = R[q];
+        else
+            *(lds_f4*)(base + lwB + (q - C::kAPW) * C::BN * 4) = R[q];
+    };
+
+    f32x16 acc[C::MT][C::NT];
+#pragma unroll
+    for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+        for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x16{0};
+    int a_off[C::MT], a_swz[C::MT];
+#pragma unroll
+    for (int i = 0; i < C::MT; ++i) {
+        const int r = wm * C::kWaveM + i * 32 + l32;
+        a_off[i] = r * C::BK;
+        a_swz[i] = (r >> 1) & 7;
+    }
+    const int b_off = C::kAFloats + wn * C::kWaveN + 4 * l32;
+
+    auto read = [&](const lds_float* stage, int kc, pcmx::f32x4(&a)[C::MT], pcmx::f32x4(&b)[4]) {
+#pragma unroll
+        for (int i = 0; i < C::MT; ++i) a[i] = *(const lds_f4*)(stage + a_off[i] + (((2 * kc + h) ^ a_swz[i]) * 4));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[s] = *(const lds_f4*)(stage + b_off + (kc * 8 + 4 * h + s) * C::BN);
+    };
+    // filler(slot) runs after every NT MFMAs (slot = s * MT + i)
+    auto mma = [&](const pcmx::f32x4(&a)[C::MT], const pcmx::f32x4(&b)[4], auto&& filler) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int i = 0; i < C::MT; ++i) {
+#pragma unroll
+                for (int j = 0; j < C::NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[s][j], acc[i][j], 0, 0, 0);
+                filler(s * C::MT + i);
+            }
+    };
+    auto pin = [](auto&& f) {
+        __builtin_amdgcn_sched_barrier(0);
+        f();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    const int nk = K / C::BK;
+    // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
+#pragma unroll
+    for (int q = 0; q < C::kAPW + C::kBPW; ++q) gload(q, 0);
+#pragma unroll
+    for (int q = 0; q < C::kAPW + C::kBPW; ++q) lwrite(q, lds);
+    if (nk > 1) {
+#pragma unroll
+        for (int q = 0; q < C::kAPW + C::kBPW; ++q) gload(q, C::BK);
+    }
+    __syncthreads();
+
+    pcmx::f32x4 fa0[C::MT], fa1[C::MT], fb0[4], fb1[4];
+    read(lds, 0, fa0, fb0);
+    auto stage = [&](int t, auto write_c, auto load_c) {
+        constexpr bool WRITE = decltype(write_c)::value;  // registers hold stage t+1
+        constexpr bool LOAD = decltype(load_c)::value;    // stage t+2 exists
+        lds_float* cur = lds + (t & 1) * C::kStage;
+        lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
+        const int k2 = (t + 2) * C::BK;
+        // the stage's P = kAPW + kBPW pieces spread evenly over chunks 0-1, one per kEvery filler slots
+        auto chunk_filler = [&](int chunk) __attribute__((always_inline)) {
+            return [&, chunk](int slot) __attribute__((always_inline)) {
+                if constexpr (!WRITE) return;
+                constexpr int P = C::kAPW + C::kBPW, kSlots = 4 * C::MT;
+                constexpr int kChunks = 2, kPer = P / kChunks, kEvery = kSlots / kPer;
+                static_assert(P % kChunks == 0 && kSlots % kPer == 0, "even piece spread");
+                if (chunk < kChunks && (slot + 1) % kEvery == 0) {
+                    const int qq = chunk * kPer + slot / kEvery;
+                    pin([&] {
+                        lwrite(qq, nxt);
+                        if constexpr (LOAD) gload(qq, k2);
+                    });
+                }
+            };
+        };
+        read(cur, 1, fa1, fb1);
+        mma(fa0, fb0, chunk_filler(0));
+        read(cur, 2, fa0, fb0);
+        mma(fa1, fb1, chunk_filler(1));
+        read(cur, 3, fa1, fb1);
+        mma(fa0, fb0, chunk_filler(2));
+        __syncthreads();
+        if constexpr (WRITE) read(nxt, 0, fa0, fb0);
+        mma(fa1, fb1, chunk_filler(3));
+    };
+    int t = 0;
+    for (; t + 2 < nk; ++t) stage(t, std::true_type{}, std::true_type{});
+    if (t + 1 < nk) stage(t++, std::true_type{}, std::false_type{});
+    stage(t, std::false_type{}, std::false_type{});
+
+    // epilogue: tile j holds columns 4c+j, so a lane's 4 tiles form one contiguous 16-B store
+#pragma unroll
+    for (int i = 0; i < C::MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm * C::kWaveM + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+            pcmx::f32x4* p = reinterpret_cast<pcmx::f32x4*>(Cmat + (size_t)row * ldc + n0 + wn * C::kWaveN + 4 * l32);
+            pcmx::f32x4 v{alpha * acc[i][0][r], alpha * acc[i][1][r], alpha * acc[i][2][r], alpha * acc[i][3][r]};
+            if constexpr (BETA) v += beta * (*p);
+            *p = v;
+        }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Reference-style SIMT kernel (f32 VALU FMAs, 64x64 LDS tiles, 4x4 outputs per thread) — the "CUDA port
+// recompiled" baseline the MFMA kernel is compared against. Any shape.
 constexpr int kSimtT = 64;
 __global__ __launch_bounds__(256) void sgemm_simt_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                          float* __restrict__ C, int M, int N, int K) {
@@ -281,984 +402,36 @@ __global__ __launch_bounds__(256) void sgemm_simt_kernel(const float* __restrict
         }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// 16x16x4 form: v_mfma_f32_16x16x4_f32 (32-cycle issue, 4 accumulators per tile). Same 256x256x32 tile
-// and 2x4 wave grid, each wave 128x64 = 8x4 tiles. A fragments: lane l reads row l&15 at k-chunk
-// q = l>>4 (one ds_read_b128 = 4 MFMA steps, k = 16c + 4q + s). B rows are padded to 260 floats so the
-// two 16-lane halves of a ds_read_b32 (rows k and k+4) land on disjoint banks; each 1-KiB DMA piece is
-// exactly one padded B row, so the lane-linear DMA image keeps working.
-struct Cfg16 {
-    static constexpr int BM = 256, BN = 256, BK = 32, WM = 2, WN = 4;
-    static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
-    static constexpr int kWaveM = BM / WM, kWaveN = BN / WN;
-    static constexpr int MT = kWaveM / 16, NT = kWaveN / 16;
-    static constexpr int kBStride = BN + 4;
-    static constexpr int kAFloats = BM * BK, kBFloats = BK * kBStride;
-    static constexpr int kStage = kAFloats + kBFloats;
-    static constexpr int kAPieces = kAFloats / 256, kBPieces = BK;
-    static constexpr int kGroupM = 8;
-};
-
-template <bool BETA>
-__global__ __launch_bounds__(Cfg16::kThreads) void sgemm_mfma16_kernel(const float* __restrict__ A,
-                                                                      const float* __restrict__ B,
-                                                                      float* __restrict__ Cmat, int M, int N, int K,
-                                                                      int lda, int ldb, int ldc, float alpha,
-                                                                      float beta) {
-    using C = Cfg16;
-    typedef float f32x4v __attribute__((ext_vector_type(4)));
-    __shared__ __attribute__((aligned(16))) float smem[2 * C::kStage];
-    lds_float* lds = (lds_float*)smem;
-    const int lane = pcmx::lane_id();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    const int q = lane >> 4, l16 = lane & 15;
-    int m0, n0;
-    tile_coords<Cfg<256, 256, 2, 4>>(M, N, m0, n0);
-
-    f32x4v acc[C::MT][C::NT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-    int a_off[C::MT], a_swz[C::MT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i) {
-        const int r = wm * C::kWaveM + i * 16 + l16;
-        a_off[i] = r * C::BK;
-        a_swz[i] = (r >> 1) & 7;
-    }
-    const int b_off = wn * C::kWaveN + l16;
-
-    auto load_stage = [&](int k0, lds_float* sA, lds_float* sB) {
-#pragma unroll
-        for (int i = 0; i < C::kAPieces / C::kWaves; ++i) {
-            const int p = wave * (C::kAPieces / C::kWaves) + i;
-            const int r = p * 8 + (lane >> 3);
-            const int chunk = (lane & 7) ^ ((r >> 1) & 7);
-            glds16(A + (size_t)(m0 + r) * lda + k0 + chunk * 4, sA + p * 256);
-        }
-#pragma unroll
-        for (int i = 0; i < C::kBPieces / C::kWaves; ++i) {
-            const int kr = wave * (C::kBPieces / C::kWaves) + i;
-            glds16(B + (size_t)(k0 + kr) * ldb + n0 + lane * 4, sB + kr * C::kBStride);
-        }
-    };
-
-    const int nk = K / C::BK;
-    load_stage(0, lds, lds + C::kAFloats);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-        lds_float* cur = lds + (t & 1) * C::kStage;
-        if (t + 1 < nk) {
-            lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
-            load_stage((t + 1) * C::BK, nxt, nxt + C::kAFloats);
-        }
-        const lds_float* sA = cur;
-        const lds_float* sB = cur + C::kAFloats;
-#pragma unroll
-        for (int c = 0; c < C::BK / 16; ++c) {
-            f32x4v a[C::MT];
-            float b[C::NT][4];
-#pragma unroll
-            for (int i = 0; i < C::MT; ++i) {
-                const int slot = (4 * c + q) ^ a_swz[i];
-                a[i] = *(const __attribute__((address_space(3))) f32x4v*)(sA + a_off[i] + slot * 4);
-            }
-#pragma unroll
-            for (int j = 0; j < C::NT; ++j)
-#pragma unroll
-                for (int s = 0; s < 4; ++s) b[j][s] = sB[(16 * c + 4 * q + s) * C::kBStride + b_off + j * 16];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-                    for (int j = 0; j < C::NT; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    // epilogue: lane holds column l16 and rows 4q .. 4q+3 of each 16x16 tile
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) {
-            const int col = n0 + wn * C::kWaveN + j * 16 + l16;
-            const int rbase = m0 + wm * C::kWaveM + i * 16 + 4 * q;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float* p = Cmat + (size_t)(rbase + r) * ldc + col;
-                const float v = alpha * acc[i][j][r];
-                *p = BETA ? v + beta * (*p) : v;
-            }
-        }
+template <class C>
+bool tile_aligned(int M, int N, int K) {
+    return M > 0 && N > 0 && K > 0 && M % C::BM == 0 && N % C::BN == 0 && K % C::BK == 0;
 }
 
-int launch16(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-             float beta, hipStream_t s) {
-    using C = Cfg16;
-    if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
-    if ((lda | ldb) & 3 || (((uintptr_t)A | (uintptr_t)B) & 15)) return -1;
+template <class C>
+int launch_dma(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+               float beta, hipStream_t s) {
+    if (!tile_aligned<C>(M, N, K)) return PCMX_ERR_ARG;
+    if ((lda | ldb) & 3 || (((uintptr_t)A | (uintptr_t)B) & 15)) return PCMX_ERR_ARG;
     const int grid = (M / C::BM) * (N / C::BN);
     if (beta != 0.f)
-        sgemm_mfma16_kernel<true><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_dma_kernel<C, true><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     else
-        sgemm_mfma16_kernel<false><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_dma_kernel<C, false><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     return (int)hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------------------------------
-// One wave per SIMD (the production kernel). 256x256x32 tile, 4 waves as 2x2, each wave owns 128x128 =
-// 4x4 tiles of 32x32 (256 accumulators: the AGPR half of the unified 512-register file). With a single
-// wave per SIMD nobody competes for the matrix pipe, and every non-MFMA instruction (LDS fragment reads
-// for the next k-chunk, the 16 LDS-DMA pieces of the next stage) is issued INSIDE the 64-cycle shadow of
-// the MFMAs: the DMA pieces are spread one per 8 MFMAs over the first half of the stage (pinned with
-// sched_barrier), fragments are double-buffered in registers, and the stage barrier sits between the
-// last fragment reads of stage t and the first of stage t+1 (rotated schedule).
-struct Cfg1W {
-    static constexpr int BM = 256, BN = 256, BK = 32, WM = 2, WN = 2;
-    static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
-    static constexpr int kWaveM = BM / WM, kWaveN = BN / WN;
-    static constexpr int MT = kWaveM / 32, NT = kWaveN / 32;
-    static constexpr int kAFloats = BM * BK, kBFloats = BK * BN;
-    static constexpr int kStage = kAFloats + kBFloats;
-    static constexpr int kAPieces = kAFloats / 256, kBPieces = kBFloats / 256;
-    static constexpr int kPiecesPerWave = (kAPieces + kBPieces) / kWaves;  // 16
-};
-
-template <bool BETA, bool REGSTAGE>
-__global__ __launch_bounds__(Cfg1W::kThreads, 1) void sgemm_mfma_1w_kernel(const float* __restrict__ A,
-                                                                          const float* __restrict__ B,
-                                                                          float* __restrict__ Cmat, int M, int N,
-                                                                          int K, int lda, int ldb, int ldc,
-                                                                          float alpha, float beta) {
-    using C = Cfg1W;
-    __shared__ __attribute__((aligned(16))) float smem[2 * C::kStage];
-    lds_float* lds = (lds_float*)smem;
-    const int lane = pcmx::lane_id();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    const int h = lane >> 5, l32 = lane & 31;
-    int m0, n0;
-    tile_coords<Cfg<256, 256, 2, 4>>(M, N, m0, n0);
-
-    f32x16 acc[C::MT][C::NT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x16{0};
-
-    int a_off[C::MT], a_swz[C::MT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i) {
-        const int r = wm * C::kWaveM + i * 32 + l32;
-        a_off[i] = r * C::BK;
-        a_swz[i] = (r >> 1) & 7;
-    }
-    const int b_col = wn * C::kWaveN + l32;
-    constexpr int kAPW = C::kAPieces / C::kWaves;  // A pieces per wave (8); B pieces follow
-
-    // ---- staging of piece pc (0..15) of this wave: A pieces are 8 rows x 128 B, B pieces one 1-KiB k-row
-    auto piece_src = [&](int pc, int k0, int& lds_off) -> const float* {
-        if (pc < kAPW) {
-            const int p = wave * kAPW + pc;
-            const int r = p * 8 + (lane >> 3);
-            if constexpr (REGSTAGE) {
-                // natural (coalesced) source order; the swizzle goes on the LDS write address
-                lds_off = r * C::BK + (((lane & 7) ^ ((r >> 1) & 7)) * 4);
-                return A + (size_t)(m0 + r) * lda + k0 + (lane & 7) * 4;
-            } else {
-                lds_off = p * 256;  // lane-linear DMA image: swizzle applied to the source chunk
-                return A + (size_t)(m0 + r) * lda + k0 + (((lane & 7) ^ ((r >> 1) & 7)) * 4);
-            }
-        }
-        const int kr = wave * (C::kBPieces / C::kWaves) + (pc - kAPW);
-        lds_off = C::kAFloats + kr * C::BN + (REGSTAGE ? lane * 4 : 0);
-        return B + (size_t)(k0 + kr) * ldb + n0 + lane * 4;
-    };
-    auto dma_piece = [&](int pc, int k0, lds_float* stage) {
-        int off;
-        const float* src = piece_src(pc, k0, off);
-        glds16(src, stage + off);
-    };
-    pcmx::f32x4 stg[8];
-    auto gload = [&](int slot, int pc, int k0) {
-        int off;
-        stg[slot] = *reinterpret_cast<const pcmx::f32x4*>(piece_src(pc, k0, off));
-    };
-    auto lwrite = [&](int slot, int pc, lds_float* stage) {
-        int off;
-        (void)piece_src(pc, 0, off);
-        *(__attribute__((address_space(3))) pcmx::f32x4*)(stage + off) = stg[slot];
-    };
-    auto read = [&](const lds_float* stage, int kc, pcmx::f32x4(&a)[C::MT], float(&b)[C::NT][4]) {
-        const lds_float* sB = stage + C::kAFloats;
-#pragma unroll
-        for (int i = 0; i < C::MT; ++i) {
-            const int slot = (2 * kc + h) ^ a_swz[i];
-            a[i] = *(const __attribute__((address_space(3))) pcmx::f32x4*)(stage + a_off[i] + slot * 4);
-        }
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) b[j][s] = sB[(kc * 8 + 4 * h + s) * C::BN + b_col + j * 32];
-    };
-    // 64 MFMAs of one 8-deep k-chunk; filler(q) runs after every 8 MFMAs (q = 0..7), pinned in place
-    auto mma = [&](const pcmx::f32x4(&a)[C::MT], const float(&b)[C::NT][4], auto&& filler) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int i = 0; i < C::MT; ++i) {
-#pragma unroll
-                for (int j = 0; j < C::NT; ++j) {
-                    const float av = s == 0 ? a[i].x : (s == 1 ? a[i].y : (s == 2 ? a[i].z : a[i].w));
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[j][s], acc[i][j], 0, 0, 0);
-                }
-                if ((i & 1) == 1) filler(s * 2 + (i >> 1));
-            }
-    };
-    auto none = [](int) {};
-
-    const int nk = K / C::BK;
-#pragma unroll
-    for (int pc = 0; pc < C::kPiecesPerWave; ++pc) dma_piece(pc, 0, lds);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    pcmx::f32x4 fa0[C::MT], fa1[C::MT];
-    float fb0[C::NT][4], fb1[C::NT][4];
-    read(lds, 0, fa0, fb0);
-    const int kdiag = g_k0_diag & 1;
-    // `more` is a compile-time flag so the staging issue points carry no branches
-    auto stage = [&](int t, auto more_c) {
-        constexpr bool more = decltype(more_c)::value;
-        lds_float* cur = lds + (t & 1) * C::kStage;
-        lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
-        const int k1 = (t + 1) * C::BK * kdiag;
-        auto pin = [](auto&& f) {
-            __builtin_amdgcn_sched_barrier(0);
-            f();
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        read(cur, 1, fa1, fb1);
-        if constexpr (!more) {
-            mma(fa0, fb0, none);
-        } else if constexpr (REGSTAGE) {
-            mma(fa0, fb0, [&](int q) { pin([&] { gload(q, q, k1); }); });
-        } else {
-            mma(fa0, fb0, [&](int q) { pin([&] { dma_piece(q, k1, nxt); }); });
-        }
-        read(cur, 2, fa0, fb0);
-        if constexpr (!more) {
-            mma(fa1, fb1, none);
-        } else if constexpr (REGSTAGE) {
-            mma(fa1, fb1, [&](int q) { pin([&] { lwrite(q, q, nxt); gload(q, 8 + q, k1); }); });
-        } else {
-            mma(fa1, fb1, [&](int q) { pin([&] { dma_piece(8 + q, k1, nxt); }); });
-        }
-        read(cur, 3, fa1, fb1);
-        if constexpr (more && REGSTAGE) {
-            mma(fa0, fb0, [&](int q) { pin([&] { lwrite(q, 8 + q, nxt); }); });
-        } else {
-            mma(fa0, fb0, none);
-        }
-        if constexpr (!REGSTAGE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (more) read(nxt, 0, fa0, fb0);
-        mma(fa1, fb1, none);
-    };
-    if (g_k0_diag & 2) {
-        // diagnostic: MFMA stream only (fragments fixed, no LDS reads, no staging, no barriers)
-        for (int t = 0; t < nk; ++t) {
-            mma(fa0, fb0, none);
-            mma(fa0, fb0, none);
-            mma(fa0, fb0, none);
-            mma(fa0, fb0, none);
-        }
-    } else {
-        for (int t = 0; t + 1 < nk; ++t) stage(t, std::true_type{});
-        stage(nk - 1, std::false_type{});
-    }
-
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) {
-            const int col = n0 + wn * C::kWaveN + j * 32 + l32;
-            const int rbase = m0 + wm * C::kWaveM + i * 32 + 4 * h;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = rbase + (r & 3) + 8 * (r >> 2);
-                float* p = Cmat + (size_t)row * ldc + col;
-                const float v = alpha * acc[i][j][r];
-                *p = BETA ? v + beta * (*p) : v;
-            }
-        }
-}
-
-template <bool REGSTAGE>
-int launch1w(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-             float beta, hipStream_t s) {
-    using C = Cfg1W;
-    if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
-    if ((lda | ldb) & 3 || (((uintptr_t)A | (uintptr_t)B) & 15)) return -1;
-    const int grid = (M / C::BM) * (N / C::BN);
-    if (beta != 0.f)
-        sgemm_mfma_1w_kernel<true, REGSTAGE><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    else
-        sgemm_mfma_1w_kernel<false, REGSTAGE><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    return (int)hipGetLastError();
-}
-
-
-// ---------------------------------------------------------------------------------------------------
-// Register-staged kernels: variant 7 (4 waves, one per SIMD) and the production variant 16 (CfgRS8: 8 waves,
-// two per SIMD, wave tile 64x128, 128 accumulators in VGPRs — the second wave per SIMD issues MFMAs while the
-// other waits at the per-stage barrier; +1.1% at 8192^3, 148.1 -> 149.8 TFLOPS). Every LDS access 16 B wide.
-//  * 256x256x32 tile, 4 waves as 2x2, each wave 128x128 = 4x4 tiles of v_mfma_f32_32x32x2_f32
-//    (256 accumulators in AGPRs).
-//  * Staging: buffer_load_dwordx4 (one SRD per operand, 32-bit voffset + scalar soffset: 2 VGPRs of
-//    addressing total) into 16 x 16-B registers, ds_write_b128 into the other LDS stage. Loads run
-//    TWO stages ahead (the registers holding stage t+1 are written to LDS during stage t and immediately
-//    reloaded with stage t+2), so HBM/L2 latency never reaches the MFMA stream. Measured on MI355X: the
-//    LDS-DMA (global_load_lds) form of the same kernel loses ~5% to DMA issue cost at 8192^3.
-//  * B columns are interleaved across the wave's 4 N-tiles (tile j owns columns 4c+j), so ONE
-//    ds_read_b128 of a B row yields the operands of all 4 tiles for one k — no transpose, conflict-free —
-//    and the epilogue stores 16 B per lane (512 contiguous bytes per row).
-//  * 32 ds_read_b128 + 16 ds_write_b128 + 16 buffer loads per 256 MFMAs per wave, each non-MFMA
-//    instruction pinned between MFMA groups (sched_barrier) so it issues in the MFMA shadow.
-template <int WM_, int WN_>
-struct CfgRSW {
-    static constexpr int BM = 256, BN = 256, BK = 32, WM = WM_, WN = WN_;
-    static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
-    static constexpr int kWaveM = BM / WM, kWaveN = BN / WN;
-    static constexpr int MT = kWaveM / 32, NT = kWaveN / 32;
-    static constexpr int kAFloats = BM * BK, kBFloats = BK * BN;
-    static constexpr int kStage = kAFloats + kBFloats;
-    static constexpr int kAPW = BM / 8 / kWaves;   // A pieces (8 rows x 128 B) per wave: 8 (4 waves) / 4 (8 waves)
-    static constexpr int kBPW = BK / kWaves;       // B pieces (one 1-KiB k-row) per wave: 8 / 4
-    // padded-A layout (PADA): rows of BK+4 floats (144 B): 8 consecutive rows of a ds_read_b128 group hit
-    // disjoint 16-B bank slots (144r mod 256 = 0,144,32,176,...), so the k-chunk enters the address as a
-    // compile-time constant (ds_read offset field) instead of an XOR with a lane-dependent swizzle.
-    static constexpr int kAStridePad = BK + 4;
-    static constexpr int kAFloatsPad = BM * kAStridePad;
-    static constexpr int kStagePad = kAFloatsPad + kBFloats;
-    static_assert(NT == 4, "interleaved-column B read assumes 4 N-tiles per wave");
-};
-using CfgRS = CfgRSW<2, 2>;   // production: 4 waves (1 per SIMD), wave tile 128x128 (256 accumulators)
-using CfgRS8 = CfgRSW<4, 2>;  // 8 waves (2 per SIMD), wave tile 64x128 (128 accumulators)
-
-template <bool BETA, int SCHED, bool PADA = false, class C = CfgRS>
-__global__ __launch_bounds__(C::kThreads, 1) void sgemm_rs_kernel(const float* __restrict__ A,
-                                                                     const float* __restrict__ B,
-                                                                     float* __restrict__ Cmat, int M, int N, int K,
-                                                                     int lda, int ldb, int ldc, float alpha,
-                                                                     float beta) {
-    typedef __attribute__((address_space(3))) pcmx::f32x4 lds_f4;
-    constexpr int kSt = PADA ? C::kStagePad : C::kStage;      // floats per LDS stage
-    constexpr int kAF = PADA ? C::kAFloatsPad : C::kAFloats;  // floats of the A part of a stage
-    constexpr int kAS = PADA ? C::kAStridePad : C::BK;        // A row stride in LDS (floats)
-    __shared__ __attribute__((aligned(16))) float smem[2 * kSt];
-    lds_float* lds = (lds_float*)smem;
-    const int lane = pcmx::lane_id();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    const int h = lane >> 5, l32 = lane & 31;
-    int m0, n0;
-    tile_coords<Cfg<256, 256, 2, 4>>(M, N, m0, n0);
-
-    // buffer resources: A rows of this block, B columns of this block (bounds = whole K extent)
-    const __amdgpu_buffer_rsrc_t rA =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, C::BM * lda * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rB =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(B + n0), (short)0, K * ldb * 4, 0x00020000);
-    const int voA = ((lane >> 3) * lda + (lane & 7) * 4) * 4;
-    const int voB = lane * 16;
-    // LDS byte addresses of this lane's staged pieces (identical every stage up to the stage base)
-    int lwA[C::kAPW];
-#pragma unroll
-    for (int i = 0; i < C::kAPW; ++i) {
-        const int r = (wave * C::kAPW + i) * 8 + (lane >> 3);
-        lwA[i] = r * kAS * 4 + (PADA ? (lane & 7) * 16 : (((lane & 7) ^ ((r >> 1) & 7)) * 16));
-    }
-    const int lwB = (kAF + wave * C::kBPW * C::BN) * 4 + lane * 16;
-
-    pcmx::f32x4 R[C::kAPW + C::kBPW];
-    auto gload = [&](int q, int k0) {  // piece q (0..7 A, 8..15 B) of the stage starting at k0
-        if (q < C::kAPW) {
-            const int so = ((wave * C::kAPW + q) * 8 * lda + k0) * 4;
-            R[q] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, voA, so, 0));
-        } else {
-            const int so = (k0 + wave * C::kBPW + (q - C::kAPW)) * ldb * 4;
-            R[q] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, voB, so, 0));
-        }
-    };
-    auto lwrite = [&](int q, lds_float* stage) {
-        char* base = (char*)(stage);
-        if (q < C::kAPW)
-            *(lds_f4*)((__attribute__((address_space(3))) char*)stage + lwA[q]) = R[q];
-        else
-            *(lds_f4*)((__attribute__((address_space(3))) char*)stage + lwB + (q - C::kAPW) * C::BN * 4) = R[q];
-        (void)base;
-    };
-
-    f32x16 acc[C::MT][C::NT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x16{0};
-
-    int a_off[C::MT], a_swz[C::MT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i) {
-        const int r = wm * C::kWaveM + i * 32 + l32;
-        a_off[i] = r * kAS + (PADA ? 4 * h : 0);
-        a_swz[i] = (r >> 1) & 7;
-    }
-    const int b_off = kAF + wn * C::kWaveN + 4 * l32;
-
-    auto read = [&](const lds_float* stage, int kc, pcmx::f32x4(&a)[C::MT], pcmx::f32x4(&b)[4]) {
-#pragma unroll
-        for (int i = 0; i < C::MT; ++i) {
-            if constexpr (PADA)
-                a[i] = *(const lds_f4*)(stage + a_off[i] + 8 * kc);
-            else
-                a[i] = *(const lds_f4*)(stage + a_off[i] + (((2 * kc + h) ^ a_swz[i]) * 4));
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) b[s] = *(const lds_f4*)(stage + b_off + (kc * 8 + 4 * h + s) * C::BN);
-    };
-    auto mma = [&](const pcmx::f32x4(&a)[C::MT], const pcmx::f32x4(&b)[4], auto&& filler) __attribute__((always_inline)) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int i = 0; i < C::MT; ++i) {
-#pragma unroll
-                for (int j = 0; j < C::NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[s][j], acc[i][j], 0, 0, 0);
-                filler(s * C::MT + i);
-            }
-    };
-    auto none = [](int) {};
-    auto pin = [](auto&& f) {
-        __builtin_amdgcn_sched_barrier(0);
-        f();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    const int nk = K / C::BK;
-    // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
-#pragma unroll
-    for (int q = 0; q < C::kAPW + C::kBPW; ++q) gload(q, 0);
-#pragma unroll
-    for (int q = 0; q < C::kAPW + C::kBPW; ++q) lwrite(q, lds);
-    if (nk > 1) {
-#pragma unroll
-        for (int q = 0; q < C::kAPW + C::kBPW; ++q) gload(q, C::BK);
-    }
-    __syncthreads();
-
-    pcmx::f32x4 fa0[C::MT], fa1[C::MT], fb0[4], fb1[4];
-    read(lds, 0, fa0, fb0);
-    if constexpr (SCHED == 3) {  // the loop is entered with no LDS op pending (see the end of stage())
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    auto stage = [&](int t, auto write_c, auto load_c) {
-        constexpr bool WRITE = decltype(write_c)::value;  // registers hold stage t+1
-        constexpr bool LOAD = decltype(load_c)::value;    // stage t+2 exists
-        lds_float* cur = lds + (t & 1) * kSt;
-        lds_float* nxt = lds + ((t + 1) & 1) * kSt;
-        const int k2 = (t + 2) * C::BK;
-        // SCHED 0: the stage's pieces spread over chunks 0-1, each pinned between MFMA groups; 2: as 0 without
-        // sched_barrier pinning; 3: as 0 plus pinned LDS reads and explicit stage-boundary waits (below).
-        auto fill = [&](int qq) __attribute__((always_inline)) {
-            auto body = [&] {
-                lwrite(qq, nxt);
-                if constexpr (LOAD) gload(qq, k2);
-            };
-            if constexpr (SCHED == 2) body(); else pin(body);
-        };
-        // filler(slot) runs after every NT MFMAs (slot = s * MT + i, 4 * MT slots per chunk); the stage's
-        // P = kAPW + kBPW pieces are spread evenly over chunks 0-1. (Spreading them over all 4 chunks, a former
-        // SCHED 1, is a race: chunk 3 runs after the barrier while other waves already read `nxt`.)
-        auto chunk_filler = [&](int chunk) __attribute__((always_inline)) {
-            return [&, chunk](int slot) __attribute__((always_inline)) {
-                if constexpr (!WRITE) return;
-                constexpr int P = C::kAPW + C::kBPW, kSlots = 4 * C::MT;
-                constexpr int kChunks = 2, kPer = P / kChunks, kEvery = kSlots / kPer;
-                static_assert(P % kChunks == 0 && kSlots % kPer == 0, "even piece spread");
-                if (chunk < kChunks && (slot + 1) % kEvery == 0) fill(chunk * kPer + slot / kEvery);
-            };
-        };
-        // SCHED 3: every chunk's LDS reads pinned where they are written (the scheduler otherwise sinks the
-        // chunk-3 B reads next to the barrier, whose lgkmcnt(0) then exposes their latency every stage)
-        auto rd = [&](const lds_float* st, int kc, pcmx::f32x4(&a)[C::MT], pcmx::f32x4(&b)[4]) __attribute__((always_inline)) {
-            if constexpr (SCHED == 3) pin([&] { read(st, kc, a, b); }); else read(st, kc, a, b);
-        };
-        rd(cur, 1, fa1, fb1);
-        mma(fa0, fb0, chunk_filler(0));
-        rd(cur, 2, fa0, fb0);
-        mma(fa1, fb1, chunk_filler(1));
-        rd(cur, 3, fa1, fb1);
-        mma(fa0, fb0, chunk_filler(2));
-        // SCHED 3: chunk 2's MFMAs stay above the barrier (they would sink below it and leave the barrier
-        // waiting on the chunk-3 reads just issued) ...
-        if constexpr (SCHED == 3) __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
-        if constexpr (WRITE) rd(nxt, 0, fa0, fb0);
-        mma(fa1, fb1, chunk_filler(3));
-        // ... and the stage ends with no LDS read pending (the next-stage reads completed under chunk 3's 64
-        // MFMAs), so the waitcnt pass need not guess across the loop back-edge (it emitted lgkmcnt(0) right
-        // after the next stage's first reads)
-        if constexpr (SCHED == 3) {
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    int t = 0;
-    for (; t + 2 < nk; ++t) stage(t, std::true_type{}, std::true_type{});
-    if (t + 1 < nk) stage(t++, std::true_type{}, std::false_type{});
-    stage(t, std::false_type{}, std::false_type{});
-
-    // epilogue: tile j holds columns 4c+j, so a lane's 4 tiles form one contiguous 16-B store
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = m0 + wm * C::kWaveM + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
-            pcmx::f32x4* p = reinterpret_cast<pcmx::f32x4*>(Cmat + (size_t)row * ldc + n0 + wn * C::kWaveN + 4 * l32);
-            pcmx::f32x4 v{alpha * acc[i][0][r], alpha * acc[i][1][r], alpha * acc[i][2][r], alpha * acc[i][3][r]};
-            if constexpr (BETA) v += beta * (*p);
-            *p = v;
-        }
-}
-
-template <int SCHED, bool PADA = false, class C = CfgRS>
 int launch_rs(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
               float beta, hipStream_t s) {
-    if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
-    if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return -1;
+    using C = CfgRS8;
+    if (!tile_aligned<C>(M, N, K)) return PCMX_ERR_ARG;
+    if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return PCMX_ERR_ARG;
     // 32-bit buffer offsets: the block's A rows and the whole B panel must stay below 2 GiB
-    if ((long long)C::BM * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31)) return -1;
+    if ((long long)C::BM * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31)) return PCMX_ERR_ARG;
     const int grid = (M / C::BM) * (N / C::BN);
     if (beta != 0.f)
-        sgemm_rs_kernel<true, SCHED, PADA, C><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_rs_kernel<true><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     else
-        sgemm_rs_kernel<false, SCHED, PADA, C><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    return (int)hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------------
-// Variant 8: the register-staged structure of variant 7 on v_mfma_f32_16x16x4_f32 (32-cycle issue,
-// 8x8 tiles of 16x16 per wave). B columns are interleaved 8-way (tile j owns columns 8c+j): two
-// ds_read_b128 of a B row give one k for all 8 tiles; B rows are stored with their 16-B chunks XOR-ed by
-// bit 2 of k so the two k-rows a 16-lane read group touches (q even/odd) land on disjoint bank slots.
-struct CfgRS16 {
-    static constexpr int BM = 256, BN = 256, BK = 32, WM = 2, WN = 2;
-    static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
-    static constexpr int kWaveM = BM / WM, kWaveN = BN / WN;
-    static constexpr int MT = kWaveM / 16, NT = kWaveN / 16;
-    static constexpr int kAFloats = BM * BK, kBFloats = BK * BN;
-    static constexpr int kStage = kAFloats + kBFloats;
-    static constexpr int kAPW = BM / 8 / kWaves;
-    static constexpr int kBPW = BK / kWaves;
-    static_assert(NT == 8, "interleaved-column B read assumes 8 N-tiles per wave");
-};
-
-template <bool BETA>
-__global__ __launch_bounds__(CfgRS16::kThreads, 1) void sgemm_rs16_kernel(const float* __restrict__ A,
-                                                                         const float* __restrict__ B,
-                                                                         float* __restrict__ Cmat, int M, int N,
-                                                                         int K, int lda, int ldb, int ldc,
-                                                                         float alpha, float beta) {
-    using C = CfgRS16;
-    typedef __attribute__((address_space(3))) pcmx::f32x4 lds_f4;
-    typedef __attribute__((address_space(3))) char lds_char;
-    __shared__ __attribute__((aligned(16))) float smem[2 * C::kStage];
-    lds_float* lds = (lds_float*)smem;
-    const int lane = pcmx::lane_id();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    const int q = lane >> 4, l16 = lane & 15;
-    int m0, n0;
-    tile_coords<Cfg<256, 256, 2, 4>>(M, N, m0, n0);
-
-    const __amdgpu_buffer_rsrc_t rA =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, C::BM * lda * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rB =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(B + n0), (short)0, K * ldb * 4, 0x00020000);
-    const int voA = ((lane >> 3) * lda + (lane & 7) * 4) * 4;
-    const int voB = lane * 16;
-    int lwA[C::kAPW];
-#pragma unroll
-    for (int i = 0; i < C::kAPW; ++i) {
-        const int r = (wave * C::kAPW + i) * 8 + (lane >> 3);
-        lwA[i] = r * C::BK * 4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16);
-    }
-    // B piece = k-row kr = wave*8 + i; chunk `lane` stored at slot lane ^ ((kr >> 2) & 1)
-    int lwB[2];
-#pragma unroll
-    for (int par = 0; par < 2; ++par) lwB[par] = (lane ^ par) * 16;
-
-    pcmx::f32x4 R[C::kAPW + C::kBPW];
-    auto gload = [&](int qq, int k0) {
-        if (qq < C::kAPW) {
-            const int so = ((wave * C::kAPW + qq) * 8 * lda + k0) * 4;
-            R[qq] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, voA, so, 0));
-        } else {
-            const int so = (k0 + wave * C::kBPW + (qq - C::kAPW)) * ldb * 4;
-            R[qq] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, voB, so, 0));
-        }
-    };
-    auto lwrite = [&](int qq, lds_float* stage) {
-        lds_char* base = (lds_char*)stage;
-        if (qq < C::kAPW) {
-            *(lds_f4*)(base + lwA[qq]) = R[qq];
-        } else {
-            const int kr = wave * C::kBPW + (qq - C::kAPW);  // wave-uniform
-            *(lds_f4*)(base + (C::kAFloats + kr * C::BN) * 4 + lwB[(kr >> 2) & 1]) = R[qq];
-        }
-    };
-
-    typedef float f32x4v __attribute__((ext_vector_type(4)));
-    f32x4v acc[C::MT][C::NT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-    int a_off[C::MT], a_swz[C::MT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i) {
-        const int r = wm * C::kWaveM + i * 16 + l16;
-        a_off[i] = r * C::BK;
-        a_swz[i] = (r >> 1) & 7;
-    }
-    // lane's B chunk pair: logical chunks 2*(wn*16 + l16) + {0,1}; physical ^= (k>>2)&1 = q&1
-    const int b_row0 = C::kAFloats + 4 * q * C::BN;  // + (16c + s) * BN per step
-    const int b_ch0 = (2 * (wn * 16 + l16)) ^ (q & 1);
-    const int b_ch1 = (2 * (wn * 16 + l16) + 1) ^ (q & 1);
-
-    auto read = [&](const lds_float* stage, int c, f32x4v(&a)[C::MT], f32x4v(&b)[4][2]) {
-#pragma unroll
-        for (int i = 0; i < C::MT; ++i) a[i] = *(const lds_f4*)(stage + a_off[i] + (((4 * c + q) ^ a_swz[i]) * 4));
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const lds_float* row = stage + b_row0 + (16 * c + s) * C::BN;
-            b[s][0] = *(const lds_f4*)(row + b_ch0 * 4);
-            b[s][1] = *(const lds_f4*)(row + b_ch1 * 4);
-        }
-    };
-    auto mma = [&](const f32x4v(&a)[C::MT], const f32x4v(&b)[4][2], auto&& filler) __attribute__((always_inline)) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int i = 0; i < C::MT; ++i) {
-#pragma unroll
-                for (int j = 0; j < C::NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[s][j >> 2][j & 3], acc[i][j], 0, 0, 0);
-                if (i & 1) filler(s * 4 + (i >> 1));
-            }
-    };
-    auto none = [](int) {};
-    auto pin = [](auto&& f) {
-        __builtin_amdgcn_sched_barrier(0);
-        f();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    const int nk = K / C::BK;
-#pragma unroll
-    for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) gload(qq, 0);
-#pragma unroll
-    for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) lwrite(qq, lds);
-    if (nk > 1) {
-#pragma unroll
-        for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) gload(qq, C::BK);
-    }
-    __syncthreads();
-
-    f32x4v fa0[C::MT], fa1[C::MT], fb0[4][2], fb1[4][2];
-    read(lds, 0, fa0, fb0);
-    auto stage = [&](int t, auto write_c, auto load_c) {
-        constexpr bool WRITE = decltype(write_c)::value;
-        constexpr bool LOAD = decltype(load_c)::value;
-        lds_float* cur = lds + (t & 1) * C::kStage;
-        lds_float* nxt = lds + ((t + 1) & 1) * C::kStage;
-        const int k2 = (t + 2) * C::BK;
-        read(cur, 1, fa1, fb1);
-        if constexpr (WRITE)
-            mma(fa0, fb0, [&](int qq) {
-                pin([&] {
-                    lwrite(qq, nxt);
-                    if constexpr (LOAD) gload(qq, k2);
-                });
-            });
-        else
-            mma(fa0, fb0, none);
-        __syncthreads();
-        if constexpr (WRITE) read(nxt, 0, fa0, fb0);
-        mma(fa1, fb1, none);
-    };
-    int t = 0;
-    for (; t + 2 < nk; ++t) stage(t, std::true_type{}, std::true_type{});
-    if (t + 1 < nk) stage(t++, std::true_type{}, std::false_type{});
-    stage(t, std::false_type{}, std::false_type{});
-
-    // epilogue: tile j holds column 8*l16 + j of the wave's 128 columns -> two 16-B stores per row
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = m0 + wm * C::kWaveM + i * 16 + 4 * q + r;
-            pcmx::f32x4* p = reinterpret_cast<pcmx::f32x4*>(Cmat + (size_t)row * ldc + n0 + wn * C::kWaveN + 8 * l16);
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                pcmx::f32x4 v{alpha * acc[i][4 * g][r], alpha * acc[i][4 * g + 1][r], alpha * acc[i][4 * g + 2][r],
-                              alpha * acc[i][4 * g + 3][r]};
-                if constexpr (BETA) v += beta * p[g];
-                p[g] = v;
-            }
-        }
-}
-
-int launch_rs16(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-                float beta, hipStream_t s) {
-    using C = CfgRS16;
-    if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
-    if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return -1;
-    if ((long long)C::BM * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31)) return -1;
-    const int grid = (M / C::BM) * (N / C::BN);
-    if (beta != 0.f)
-        sgemm_rs16_kernel<true><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    else
-        sgemm_rs16_kernel<false><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    return (int)hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------------
-// Variant 13: v_mfma_f32_16x16x4_f32 with low register pressure (no spills, unlike variant 8).
-//  * Same tile / staging / LDS layouts as variant 8 (256x256x32, 4 waves 2x2, wave 128x128 = 8x8 tiles).
-//  * MFMA order is i-major (A tile i, then k-step s, then the 8 N tiles), so an A fragment is dead after
-//    its 32 MFMAs: A is read just in time into a 4-slot ring, two i-iterations (2 x 1024 cycles) ahead.
-//    B fragments (32 VGPRs per 16-k chunk) are double-buffered by chunk. Per wave: ~12 + 64 + 64 staging
-//    VGPRs instead of 2 x 64 fragment + 64 staging.
-//  * One barrier per stage, placed after the first 6 of the 8 i-iterations of chunk 1: every read of the
-//    current stage and every LDS write of the next stage (16 fillers, lwrite + global load two stages
-//    ahead) is issued before it, and the next stage's first fragments are read right after it while the
-//    last 2 x 32 MFMAs run.
-template <bool BETA>
-__global__ __launch_bounds__(CfgRS16::kThreads, 1) void sgemm_rs16i_kernel(const float* __restrict__ A,
-                                                                          const float* __restrict__ B,
-                                                                          float* __restrict__ Cmat, int M, int N,
-                                                                          int K, int lda, int ldb, int ldc,
-                                                                          float alpha, float beta) {
-    using C = CfgRS16;
-    typedef __attribute__((address_space(3))) pcmx::f32x4 lds_f4;
-    typedef __attribute__((address_space(3))) char lds_char;
-    typedef float f32x4v __attribute__((ext_vector_type(4)));
-    constexpr int kAS = C::BK + 4;          // padded A row (144 B): conflict-free b128 reads, additive k
-    constexpr int kAF = C::BM * kAS;        // A floats per stage
-    constexpr int kSt = kAF + C::kBFloats;  // floats per stage
-    __shared__ __attribute__((aligned(16))) float smem[2 * kSt];
-    lds_float* lds = (lds_float*)smem;
-    const int lane = pcmx::lane_id();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    const int q = lane >> 4, l16 = lane & 15;
-    int m0, n0;
-    tile_coords<Cfg<256, 256, 2, 4>>(M, N, m0, n0);
-
-    const __amdgpu_buffer_rsrc_t rA =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, C::BM * lda * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rB =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(B + n0), (short)0, K * ldb * 4, 0x00020000);
-    const int voA = ((lane >> 3) * lda + (lane & 7) * 4) * 4;
-    const int voB = lane * 16;
-    int lwA[C::kAPW];
-#pragma unroll
-    for (int i = 0; i < C::kAPW; ++i) {
-        const int r = (wave * C::kAPW + i) * 8 + (lane >> 3);
-        lwA[i] = r * kAS * 4 + (lane & 7) * 16;
-    }
-    int lwB[2];
-#pragma unroll
-    for (int par = 0; par < 2; ++par) lwB[par] = (lane ^ par) * 16;
-
-    pcmx::f32x4 R[C::kAPW + C::kBPW];
-    auto gload = [&](int qq, int k0) __attribute__((always_inline)) {
-        if (qq < C::kAPW) {
-            const int so = ((wave * C::kAPW + qq) * 8 * lda + k0) * 4;
-            R[qq] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, voA, so, 0));
-        } else {
-            const int so = (k0 + wave * C::kBPW + (qq - C::kAPW)) * ldb * 4;
-            R[qq] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, voB, so, 0));
-        }
-    };
-    auto lwrite = [&](int qq, lds_float* stage) __attribute__((always_inline)) {
-        lds_char* base = (lds_char*)stage;
-        if (qq < C::kAPW) {
-            *(lds_f4*)(base + lwA[qq]) = R[qq];
-        } else {
-            const int kr = wave * C::kBPW + (qq - C::kAPW);
-            *(lds_f4*)(base + (kAF + kr * C::BN) * 4 + lwB[(kr >> 2) & 1]) = R[qq];
-        }
-    };
-
-    f32x4v acc[C::MT][C::NT];
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-    // lane base of the A reads: row wm*128 + l16, k-chunk q; tile i and chunk c add compile-time offsets
-    const int a_lane = (wm * C::kWaveM + l16) * kAS + 4 * q;
-    const int b_row0 = kAF + 4 * q * C::BN;
-    const int b_ch0 = (2 * (wn * 16 + l16)) ^ (q & 1);
-    const int b_ch1 = (2 * (wn * 16 + l16) + 1) ^ (q & 1);
-    const int b_lane0 = b_row0 + b_ch0 * 4, b_lane1 = b_row0 + b_ch1 * 4;
-
-    f32x4v ring[4];            // A fragments, slot = (16*stage + 8*chunk + i) % 4
-    f32x4v bA[4][2], bB[4][2];  // B fragments of chunk 0 (bA) and chunk 1 (bB)
-    auto readA = [&](const lds_float* stage, int c, int i, f32x4v& dst) __attribute__((always_inline)) {
-        dst = *(const lds_f4*)(stage + a_lane + i * 16 * kAS + 16 * c);
-    };
-    auto readB = [&](const lds_float* stage, int c, int s, f32x4v(&dst)[4][2]) __attribute__((always_inline)) {
-        dst[s][0] = *(const lds_f4*)(stage + b_lane0 + (16 * c + s) * C::BN);
-        dst[s][1] = *(const lds_f4*)(stage + b_lane1 + (16 * c + s) * C::BN);
-    };
-    auto pin = [](auto&& f) __attribute__((always_inline)) {
-        __builtin_amdgcn_sched_barrier(0);
-        f();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto mma_i = [&](int i, const f32x4v& a, const f32x4v(&b)[4][2]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int j = 0; j < C::NT; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][j >> 2][j & 3], acc[i][j], 0, 0, 0);
-    };
-
-    const int nk = K / C::BK;
-#pragma unroll
-    for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) gload(qq, 0);
-#pragma unroll
-    for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) lwrite(qq, lds);
-    if (nk > 1) {
-#pragma unroll
-        for (int qq = 0; qq < C::kAPW + C::kBPW; ++qq) gload(qq, C::BK);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) readB(lds, 0, s, bA);
-    readA(lds, 0, 0, ring[0]);
-    readA(lds, 0, 1, ring[1]);
-
-    auto stage = [&](int t, auto write_c, auto load_c) __attribute__((always_inline)) {
-        constexpr bool WRITE = decltype(write_c)::value;  // registers hold stage t+1 (and stage t+1 exists)
-        constexpr bool LOAD = decltype(load_c)::value;    // stage t+2 exists
-        lds_float* cur = lds + (t & 1) * kSt;
-        lds_float* nxt = lds + ((t + 1) & 1) * kSt;
-        const int k2 = (t + 2) * C::BK;
-        auto fill = [&](int qq) __attribute__((always_inline)) {
-            if constexpr (WRITE) {
-                pin([&] {
-                    lwrite(qq, nxt);
-                    if constexpr (LOAD) gload(qq, k2);
-                });
-            }
-        };
-        // ---- chunk 0: A ring slots 0..7 (mod 4); B chunk 1 prefetched into bB during i = 0..3
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            pin([&] {
-                if (i <= 5) readA(cur, 0, i + 2, ring[(i + 2) & 3]);
-                else readA(cur, 1, i - 6, ring[(i + 2) & 3]);
-                if (i <= 3) readB(cur, 1, i, bB);
-            });
-            mma_i(i, ring[i & 3], bA);
-            fill(i);
-        }
-        // ---- chunk 1
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (i == 6) {
-                __syncthreads();  // all reads of `cur` issued, all fillers of `nxt` written
-                if constexpr (WRITE) {
-                    pin([&] {
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) readB(nxt, 0, s, bA);
-                        readA(nxt, 0, 0, ring[0]);
-                        readA(nxt, 0, 1, ring[1]);
-                    });
-                }
-            }
-            if (i <= 5) pin([&] { readA(cur, 1, i + 2, ring[(i + 2) & 3]); });
-            mma_i(i, ring[i & 3], bB);
-            if (i < 2) {
-                fill(8 + 2 * i);
-                fill(9 + 2 * i);
-            } else if (i < 6) {
-                fill(10 + i);
-            }
-        }
-    };
-    int t = 0;
-    for (; t + 2 < nk; ++t) stage(t, std::true_type{}, std::true_type{});
-    if (t + 1 < nk) stage(t++, std::true_type{}, std::false_type{});
-    stage(t, std::false_type{}, std::false_type{});
-
-#pragma unroll
-    for (int i = 0; i < C::MT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = m0 + wm * C::kWaveM + i * 16 + 4 * q + r;
-            pcmx::f32x4* p = reinterpret_cast<pcmx::f32x4*>(Cmat + (size_t)row * ldc + n0 + wn * C::kWaveN + 8 * l16);
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                pcmx::f32x4 v{alpha * acc[i][4 * g][r], alpha * acc[i][4 * g + 1][r], alpha * acc[i][4 * g + 2][r],
-                              alpha * acc[i][4 * g + 3][r]};
-                if constexpr (BETA) v += beta * p[g];
-                p[g] = v;
-            }
-        }
-}
-
-int launch_rs16i(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc,
-                 float alpha, float beta, hipStream_t s) {
-    using C = CfgRS16;
-    if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
-    if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return -1;
-    if ((long long)C::BM * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31)) return -1;
-    const int grid = (M / C::BM) * (N / C::BN);
-    if (beta != 0.f)
-        sgemm_rs16i_kernel<true><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    else
-        sgemm_rs16i_kernel<false><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    return (int)hipGetLastError();
-}
-
-using Big = Cfg<256, 256, 2, 4>;
-using Small = Cfg<128, 128, 2, 2>;
-
-template <class C, bool PIPE>
-int launch(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-           float beta, hipStream_t s) {
-    if (M % C::BM || N % C::BN || K % C::BK || M <= 0 || N <= 0 || K <= 0) return -1;
-    if ((lda | ldb) & 3 || (((uintptr_t)A | (uintptr_t)B) & 15)) return -1;
-    const int grid = (M / C::BM) * (N / C::BN);
-    if (beta != 0.f)
-        sgemm_mfma_kernel<C, true, PIPE><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
-    else
-        sgemm_mfma_kernel<C, false, PIPE><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_rs_kernel<false><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     return (int)hipGetLastError();
 }
 }  // namespace
@@ -1266,46 +439,27 @@ int launch(const float* A, const float* B, float* Cm, int M, int N, int K, int l
 extern "C" int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
                                       int ldc, float alpha, float beta, int variant, hipStream_t s) {
     switch (variant) {
-        case 0: return launch<Big, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 1: return launch<Small, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 2: return launch<Big, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 3: return launch<Small, false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 4: return launch16(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 5: return launch1w<false>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 7: return launch_rs<0>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 10: return launch_rs<2>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 14: return launch_rs<3>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 15: return launch_rs<3, false, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 16: return launch_rs<0, false, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 18: return launch_rs<2, false, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 11: return launch_rs<0, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 8: return launch_rs16(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        case 13: return launch_rs16i(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
-        default: return -1;
+        case 0: return launch_dma<Big>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 1: return launch_dma<Small>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 16: return launch_rs(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        default: return PCMX_ERR_ARG;
     }
 }
 
 extern "C" int pcmx_sgemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
                               float alpha, float beta, hipStream_t s) {
-    // 256x256 tiles (register-staged, 8 waves = two per SIMD, variant 16) when the grid fills the 256 CUs;
-    // otherwise the 128x128 two-waves-per-SIMD kernel (4x more tiles).
-    const bool big_ok = (M % 256 == 0) && (N % 256 == 0) && (long long)(M / 256) * (N / 256) >= 192;
+    // 256x256 tiles when the grid fills the 256 CUs (register-staged variant 16; the LDS-DMA variant 0 when its
+    // 32-bit buffer offsets do not reach), otherwise the 128x128 kernel (4x more tiles).
+    const bool big_ok = tile_aligned<Big>(M, N, K) && (long long)(M / 256) * (N / 256) >= 192;
     if (big_ok) {
-        const int rc = pcmx_sgemm_f32_variant(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 16, s);
-        if (rc != -1) return rc;  // -1: offsets exceed the 32-bit buffer range -> fall back
+        const int rc = launch_rs(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        return rc == PCMX_ERR_ARG ? launch_dma<Big>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s) : rc;
     }
-    if (M % 256 == 0 && N % 256 == 0 && big_ok)
-        return pcmx_sgemm_f32_variant(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 0, s);
-    return pcmx_sgemm_f32_variant(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 1, s);
-}
-
-extern "C" int pcmx_sgemm_set_tuning(int tile_order, int k0_diag) {
-    PCMX_HIP_RET(hipMemcpyToSymbol(HIP_SYMBOL(g_tile_order), &tile_order, sizeof(int)));
-    PCMX_HIP_RET(hipMemcpyToSymbol(HIP_SYMBOL(g_k0_diag), &k0_diag, sizeof(int)));
-    return 0;
+    return launch_dma<Small>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
 }
 
 extern "C" int pcmx_sgemm_f32_simt(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t s) {
+    if (M <= 0 || N <= 0 || K <= 0) return PCMX_ERR_ARG;
     dim3 grid((N + kSimtT - 1) / kSimtT, (M + kSimtT - 1) / kSimtT);
     sgemm_simt_kernel<<<grid, 256, 0, s>>>(A, B, C, M, N, K);
     return (int)hipGetLastError();

@@ -29,7 +29,7 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, variant: int = -1) -> torch.Tensor:
         c = torch.empty(m, n, dtype=torch.float32)
         cpu_lib().pcmx_sgemm_host(ac.data_ptr(), bc.data_ptr(), c.data_ptr(), m, n, k)
         return c
-    tile = 256 if variant in (0, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13) else 128
+    tile = 256 if variant in (0, 16) else 128
     mp, np_, kp = _round_up(m, tile), _round_up(n, tile), _round_up(k, 32)
     ac = a if a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0 else a.contiguous()
     bc = b if b.stride(1) == 1 and b.stride(0) % 4 == 0 and b.data_ptr() % 16 == 0 else b.contiguous()

@@ -42,12 +42,9 @@ def bench_sgemm(size, reps):
         b = torch.rand(n, n, device=dev) * 2 - 1
         flop = 2.0 * n * n * n
         cands = {
+            "pcmx_mfma_rs8_256": lambda: ops.sgemm(a, b, variant=16),
             "pcmx_mfma_256": lambda: ops.sgemm(a, b, variant=0),
             "pcmx_mfma_128": lambda: ops.sgemm(a, b, variant=1),
-            "pcmx_mfma_256_nopipe": lambda: ops.sgemm(a, b, variant=2),
-            "pcmx_mfma_128_nopipe": lambda: ops.sgemm(a, b, variant=3),
-            "pcmx_mfma16_256": lambda: ops.sgemm(a, b, variant=4),
-            "pcmx_mfma_1w": lambda: ops.sgemm(a, b, variant=5),
             "torch_matmul": lambda: a @ b,
         }
         if n <= 4096:

@@ -1,5 +1,4 @@
 """SGEMM tile-order / memory-ceiling sweep (interleaved rounds in one process, random operands)."""
-import ctypes
 import json
 import sys
 from pathlib import Path
@@ -7,8 +6,9 @@ from pathlib import Path
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-from parallel_c_programs_amd import ops  # noqa: E402
-from parallel_c_programs_amd._native import hip_lib  # noqa: E402
+from parallel_c_programs_amd import ops  # noqa: E402,F401
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+import _lab  # noqa: E402
 
 
 def t_ms(fn, reps=5):
@@ -25,8 +25,6 @@ def t_ms(fn, reps=5):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
-    lib = hip_lib()
-    lib.pcmx_sgemm_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
     a = torch.rand(n, n, device="cuda") * 2 - 1
     b = torch.rand(n, n, device="cuda") * 2 - 1
     flop = 2.0 * n ** 3
@@ -34,12 +32,12 @@ def main():
     res = {}
     for rnd in range(3):
         for remap, grp, kd in configs:
-            lib.pcmx_sgemm_set_tuning((remap << 8) | grp, kd)
+            _lab.set_tuning((remap << 8) | grp, kd)
             for v in (5, 4):
                 key = f"v{v}_remap{remap}_g{grp}_k{kd}"
-                res.setdefault(key, []).append(t_ms(lambda: ops.sgemm(a, b, variant=v)))
+                res.setdefault(key, []).append(t_ms(lambda: _lab.sgemm(a, b, v)))
         res.setdefault("torch", []).append(t_ms(lambda: a @ b))
-    lib.pcmx_sgemm_set_tuning((1 << 8) | 8, 1)
+    _lab.set_tuning((1 << 8) | 8, 1)
     for k, v in res.items():
         print(json.dumps({"cfg": k, "ms": min(v), "tflops": flop / min(v) / 1e9}))
 
