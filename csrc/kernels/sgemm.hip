@@ -14,8 +14,8 @@
 //  * K-permutation: the MFMA's two k-slots (h = lane>>5) are fed k = 8c+4h+s at step s, so ONE ds_read_b128
 //    delivers a lane's A operands for 4 MFMA steps. A and B agree on the permutation, so the sum is the full
 //    K sum.
-//  * A-tile bank-conflict swizzle: slot = chunk ^ ((row>>1)&7) puts every 16-lane group of a ds_read_b128
-//    on 16 distinct 16-B slots.
+//  * A-tile bank conflicts: the LDS-DMA kernels swizzle 16-B chunks (slot = chunk ^ ((row>>1)&7)); the
+//    register-staged kernel pads A rows instead (see variant 16).
 //  * XCD-aware bijective block remap + grouped tile order (8 tile-rows per column strip): the blocks resident
 //    on one XCD share A/B panels in that XCD's L2.
 #include "pcmx_common.h"
@@ -196,6 +196,10 @@ __global__ __launch_bounds__(C::kThreads) void sgemm_dma_kernel(const float* __r
 //  * B columns are interleaved across the wave's 4 N-tiles (tile j owns columns 4c+j), so ONE ds_read_b128 of a
 //    B row yields the operands of all 4 tiles for one k (no transpose, conflict-free) and the epilogue stores
 //    16 B per lane (512 contiguous bytes per row).
+//  * Padded A rows (BK + 4 = 36 floats, 144 B): the 16 rows of a ds_read_b128 lane group start 36 dwords apart,
+//    which covers all 64 banks exactly once (conflict-free without a swizzle), so the k-chunk enters the read
+//    address as a compile-time offset instead of a lane-dependent XOR. Measured at 8192^3 (interleaved A/B,
+//    scripts/sgemm_ab.py): 149.2-149.8 TFLOPS with the XOR swizzle -> 151.2-151.4 padded (lab variant 19).
 //  * Each staging piece (ds_write + buffer load) is pinned between MFMA groups (sched_barrier) in chunks 0-1
 //    of the stage, so it issues in the MFMA shadow. (Spreading them over all 4 chunks is a race: chunk 3 runs
 //    after the barrier while other waves already read `nxt`.)
@@ -204,8 +208,9 @@ struct CfgRS8 {
     static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
     static constexpr int kWaveM = BM / WM, kWaveN = BN / WN;
     static constexpr int MT = kWaveM / 32, NT = kWaveN / 32;
-    static constexpr int kAFloats = BM * BK, kBFloats = BK * BN;
-    static constexpr int kStage = kAFloats + kBFloats;
+    static constexpr int kAStride = BK + 4;  // padded A row (floats)
+    static constexpr int kAFloats = BM * kAStride, kBFloats = BK * BN;
+    static constexpr int kStage = kAFloats + kBFloats;  // 2 stages = 136 KiB of the 160 KiB LDS
     static constexpr int kAPW = BM / 8 / kWaves;  // A pieces (8 rows x 128 B) per wave
     static constexpr int kBPW = BK / kWaves;      // B pieces (one 1-KiB k-row) per wave
     static_assert(NT == 4, "interleaved-column B read assumes 4 N-tiles per wave");
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(CfgRS8::kThreads, 1) void sgemm_rs_kernel(const flo
 #pragma unroll
     for (int i = 0; i < C::kAPW; ++i) {
         const int r = (wave * C::kAPW + i) * 8 + (lane >> 3);
-        lwA[i] = r * C::BK * 4 + (((lane & 7) ^ ((r >> 1) & 7)) * 16);
+        lwA[i] = r * C::kAStride * 4 + (lane & 7) * 16;
     }
     const int lwB = (C::kAFloats + wave * C::kBPW * C::BN) * 4 + lane * 16;
 
@@ -264,18 +269,14 @@ __global__ __launch_bounds__(CfgRS8::kThreads, 1) void sgemm_rs_kernel(const flo
     for (int i = 0; i < C::MT; ++i)
 #pragma unroll
         for (int j = 0; j < C::NT; ++j) acc[i][j] = f32x16{0};
-    int a_off[C::MT], a_swz[C::MT];
+    int a_off[C::MT];  // lane's A row, k offset 4h (the K-permutation); chunk kc adds 8 kc floats
 #pragma unroll
-    for (int i = 0; i < C::MT; ++i) {
-        const int r = wm * C::kWaveM + i * 32 + l32;
-        a_off[i] = r * C::BK;
-        a_swz[i] = (r >> 1) & 7;
-    }
+    for (int i = 0; i < C::MT; ++i) a_off[i] = (wm * C::kWaveM + i * 32 + l32) * C::kAStride + 4 * h;
     const int b_off = C::kAFloats + wn * C::kWaveN + 4 * l32;
 
     auto read = [&](const lds_float* stage, int kc, pcmx::f32x4(&a)[C::MT], pcmx::f32x4(&b)[4]) {
 #pragma unroll
-        for (int i = 0; i < C::MT; ++i) a[i] = *(const lds_f4*)(stage + a_off[i] + (((2 * kc + h) ^ a_swz[i]) * 4));
+        for (int i = 0; i < C::MT; ++i) a[i] = *(const lds_f4*)(stage + a_off[i] + 8 * kc);
 #pragma unroll
         for (int s = 0; s < 4; ++s) b[s] = *(const lds_f4*)(stage + b_off + (kc * 8 + 4 * h + s) * C::BN);
     };

@@ -816,7 +816,7 @@ __global__ __launch_bounds__(C::kThreads, 1) void sgemm_rs_kernel(const float* _
         // SCHED 3: chunk 2's MFMAs stay above the barrier (they would sink below it and leave the barrier
         // waiting on the chunk-3 reads just issued) ...
         if constexpr (SCHED == 3) __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
+        if (!(g_k0_diag & 4)) __syncthreads();  // diag bit 2: no stage barrier (timing only, wrong result)
         if constexpr (WRITE) rd(nxt, 0, fa0, fb0);
         mma(fa1, fb1, chunk_filler(3));
         // ... and the stage ends with no LDS read pending (the next-stage reads completed under chunk 3's 64
@@ -1287,6 +1287,10 @@ extern "C" int pcmx_sgemm_lab_variant(const float* A, const float* B, float* C, 
         case 11: return launch_rs<0, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 8: return launch_rs16(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 13: return launch_rs16i(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 19: return launch_rs<0, true, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 20: return launch_rs<3, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 21: return launch_rs<3, true, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 22: return launch_rs<2, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         default: return -1;
     }
 }
