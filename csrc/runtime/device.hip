@@ -33,7 +33,7 @@ extern "C" void pcmx_print_device_info(int device) {
         printf("hipGetDeviceProperties failed for device %d\n", device);
         return;
     }
-    printf("Name: %s\n", p.name);
+    printf("Name: %s\n", p.name[0] ? p.name : p.gcnArchName);
     printf("Architecture: %s (compute capability %d.%d)\n", p.gcnArchName, p.major, p.minor);
     printf("Compute units: %d, wavefront size: %d\n", p.multiProcessorCount, p.warpSize);
     printf("LDS per workgroup: %zu KiB, max threads per workgroup: %d\n", p.sharedMemPerBlock / 1024,

@@ -64,7 +64,7 @@ def _run(cmd, cwd=None):
 
 
 CPU_SRCS = ["cpu/bmp.c", "cpu/matrix.c", "cpu/spmv.c", "cpu/histogram.c", "cpu/vec.c", "cpu/oracles.c",
-            "cpu/demos.c", "comm/comm_tcp.c", "comm/region_dist.c"]
+            "cpu/pipeline3d_host.c", "cpu/demos.c", "comm/comm_tcp.c", "comm/region_dist.c"]
 CFLAGS = ["-O3", "-fPIC", "-std=gnu11", "-fopenmp", "-march=x86-64-v3", "-Wall", "-Wno-unknown-pragmas",
           f"-I{CSRC / 'include'}"]
 # files whose float rounding must match the reference build bit-for-bit
@@ -181,6 +181,10 @@ BIN_TOOLS = {
     "mpi_ring": ("bin/mpi_ring_main.cpp", "hip"),
     "vmul": ("bin/vmul_main.cpp", "hip"),
     "pcmx_launch": ("bin/launch_main.c", "c"),
+    # C programs written only against the reference 3-D entry points (pcmx_pipeline3d.h): host C, linked with
+    # libpcmx_hip + libpcmx_cpu
+    "pipeline3d": ("bin/pipeline3d_main.c", "c+hip"),
+    "pipeline3d_opencl": ("bin/pipeline3d_main.c", "c+hip"),
 }
 
 
@@ -193,12 +197,17 @@ def build_bin(force=False, jobs=8):
         if not s.exists():
             continue
         out = BIN / name
-        deps = [s, LIB / "libpcmx_cpu.so", *_headers()] + ([LIB / "libpcmx_hip.so"] if kind == "hip" else [])
+        deps = [s, LIB / "libpcmx_cpu.so", *_headers()] + ([LIB / "libpcmx_hip.so"] if "hip" in kind else [])
         if not (force or _newer(out, deps)):
             continue
         variant = f"-DPCMX_TOOL_{name.upper()}"
         rpath = "-Wl,-rpath,$ORIGIN/../parallel_c_programs_amd/lib"
-        if kind == "c":
+        if kind == "c+hip":
+            extra = ["-DPCMX_OPENCL_PROGRAM"] if name.endswith("_opencl") else []
+            todo.append(["gcc", "-O2", "-std=gnu11", *extra, f"-I{CSRC / 'include'}", str(s), "-o", str(out),
+                         f"-L{LIB}", f"-L{tlib}", "-lpcmx_hip", "-lpcmx_cpu", "-lamdhip64", "-lm", rpath,
+                         f"-Wl,-rpath,{tlib}"])
+        elif kind == "c":
             todo.append(["gcc", "-O2", "-std=gnu11", "-fopenmp", variant, f"-I{CSRC / 'include'}", str(s),
                          "-o", str(out), f"-L{LIB}", "-lpcmx_cpu", "-lm", rpath])
         else:

@@ -199,3 +199,30 @@ def test_native_raycast_cuda_program(gpu, tmp_path):
     assert "Grow time:" in r.stdout and "Raycast time: " in r.stdout and r.stdout.count("Time : ") == 2
     img = bmp.read(tmp_path / "out.bmp")
     assert img.shape == (512, 512) and int((img == 255).sum()) > 0
+
+
+def test_reference_entry_points_opencl_program(gpu, tmp_path):
+    """bin/pipeline3d_opencl: a C program using only the reference names (IMAGE_DIM 64 via the header),
+    grow_region_gpu + raycast_gpu: T2 region and the T5 64x64 image (sum 127,180, bit-identical to serial)."""
+    import subprocess
+
+    r = subprocess.run([_bin("pipeline3d_opencl")], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "region voxels: 2197899 (serial 2197899) identical" in r.stdout
+    assert "serial caster sum: 127180, global caster bit-identical" in r.stdout
+    assert bmp.read(tmp_path / "out.bmp").shape == (64, 64)
+
+
+def test_reference_entry_points_cuda_program(gpu, tmp_path):
+    """bin/pipeline3d: print_properties, create_data, grow_region_gpu_shared / grow_region_gpu (both equal to
+    grow_region_serial), raycast_gpu_texture -> out.bmp, raycast_gpu = the serial 512^2 image (sum 8,154,839)."""
+    import subprocess
+
+    r = subprocess.run([_bin("pipeline3d")], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Device count:" in r.stdout and "Compute capability: 9.5" in r.stdout
+    assert "Grow time:" in r.stdout and "Raycast time: " in r.stdout
+    assert "region voxels: 2197899 (serial 2197899) identical" in r.stdout
+    assert "(global-memory caster 8154839)" in r.stdout
+    img = bmp.read(tmp_path / "out.bmp")
+    assert img.shape == (512, 512) and int(img.astype(np.int64).sum()) > 0
