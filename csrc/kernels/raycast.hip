@@ -186,7 +186,9 @@ __global__ __launch_bounds__(256) void brick_pack_kernel(const unsigned char* __
 
 // 4 voxels per thread (dim % 4 == 0): each of the 8 source rows is read as one aligned u32 (+ the next byte);
 // the 4 texels go through LDS so the stores leave fully coalesced (consecutive lanes, consecutive texels).
-// (4 rows per thread, re-using the shared source rows, measured slower: 64 KB of LDS halves occupancy.)
+// (4 rows per thread, re-using the shared source rows, measured slower: 64 KB of LDS halves occupancy. Taking
+// the next byte from the neighbour lane (DPP shift) with a guarded load for lane 63 measured 700 vs 510 us at
+// 512^3: the 8 divergent guarded loads serialise their waits.)
 __device__ __forceinline__ unsigned row5(const unsigned char* __restrict__ p, int x, int dim, unsigned& next) {
     next = p[min(x + 4, dim - 1)];
     return *reinterpret_cast<const unsigned*>(p + x);
@@ -198,6 +200,13 @@ __device__ __forceinline__ unsigned pair(unsigned a, unsigned an, unsigned b, un
     const unsigned b0 = (b >> (8 * i)) & 0xff, b1 = i < 3 ? (b >> (8 * i + 8)) & 0xff : bn;
     return a0 | (a1 << 8) | (b0 << 16) | (b1 << 24);
 }
+
+// LDS slot of texel j of the block's 1024: slot = j ^ ((j >> 3) & 3). The write (ds_write_b128: 8-lane groups,
+// bank = (a/4) mod 32, i.e. 8 16-B slots) has lane t at texel 4t+i: the XOR makes the 8 lanes of a group hit 8
+// distinct slots mod 8 (the unswizzled 4t+i, or the former +j/16 pad, is 2-way: 5.0e7 conflict cycles per pack at
+// 512^3). The read-back (texel j by lane j, ds_read_b128 groups of 16 lanes made of aligned 4-lane blocks) only
+// permutes slots inside aligned groups of 4, so its groups still cover 16 distinct slots mod 16.
+__device__ __forceinline__ int tex_slot(int j) { return j ^ ((j >> 3) & 3); }
 
 __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* __restrict__ data,
                                                          const unsigned char* __restrict__ region, int dim,
@@ -218,23 +227,21 @@ __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* _
                ((r[q] & 0xff000000) ? 0x1000000u : 0u);
         rn[q] = rn[q] ? 1u : 0u;
     }
-    // texel j lives in slot j + j/16: the 16-B slots written by lanes t, t+4, ... (texels 4t+i) then fall on
-    // distinct LDS banks, and the coalesced read-back (texels j, j+1, ...) stays contiguous
-    __shared__ uint4 stage[1024 + 64];
+    __shared__ uint4 stage[1024];
     const int xb = blockIdx.x * 1024;  // first voxel of this block's row segment
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const unsigned r0 = pair(r[0], rn[0], r[1], rn[1], i), r1 = pair(r[2], rn[2], r[3], rn[3], i);
         const unsigned d0 = pair(d[0], dn[0], d[1], dn[1], i), d1 = pair(d[2], dn[2], d[3], dn[3], i);
-        const int j = threadIdx.x * 4 + i;
-        stage[j + (j >> 4)] = wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
+        stage[tex_slot(threadIdx.x * 4 + i)] =
+            wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int j = i * 256 + threadIdx.x;
         if (xb + j >= dim) continue;
-        const uint4 t = stage[j + (j >> 4)];
+        const uint4 t = stage[tex_slot(j)];
         if (wide)
             reinterpret_cast<uint4*>(tex)[rows[0] + xb + j] = t;
         else
