@@ -230,3 +230,119 @@ void pcmx_raycast_serial(const unsigned char* data, const unsigned char* region,
             image[(y + half) * image_dim + (x + half)] = (unsigned char)(color > 255 ? 255 : color);
         }
 }
+
+/* ------------------------------------------------------- z-slab decomposition of the 3-D pipeline (host side) */
+
+void pcmx_create_data_hash_slab(unsigned char* data, int dim, int z_first, int nplanes, unsigned int seed) {
+#pragma omp parallel for schedule(static)
+    for (int k = 0; k < nplanes; ++k) {
+        const int z = z_first + k;
+        unsigned char* pl = data + (size_t)k * dim * dim;
+        if (z < 0 || z >= dim) {
+            memset(pl, 0, (size_t)dim * dim);
+            continue;
+        }
+        for (int y = 0; y < dim; ++y)
+            for (int x = 0; x < dim; ++x) {
+                int s = volume_shape(x, y, z);
+                pl[(size_t)y * dim + x] =
+                    (unsigned char)(s >= 0 ? s : (int)(pcmx_hash3((unsigned)x, (unsigned)y, (unsigned)z, seed) % 20u));
+            }
+    }
+}
+
+long long pcmx_region3d_slab_host(const unsigned char* data, unsigned char* region, int dim, int nz, int halos, int thr) {
+    /* data/region point at the slab's first OWNED plane; planes -1 / nz are readable when halos bit 0 / 1 */
+    const long long P = (long long)dim * dim;
+    idx_stack_t st = {0, 0, 0};
+    const long long lo = (halos & 1) ? -P : 0, hi = (halos & 2) ? (nz + 1) * P : nz * P;
+    for (long long i = lo; i < hi; ++i) /* every region voxel (owned or halo) seeds the fill */
+        if (region[i]) stack_push(&st, i);
+    long long added = 0;
+    while (st.n > 0) {
+        const long long p = st.v[--st.n];
+        const int z = p >= 0 ? (int)(p / P) : -1; /* p in [-P, 0): the halo plane below */
+        const long long rem = p - (long long)z * P;
+        const int y = (int)(rem / dim), x = (int)(rem % dim);
+        const int nb[6][3] = {{-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
+        for (int k = 0; k < 6; ++k) {
+            const int cx = x + nb[k][0], cy = y + nb[k][1], cz = z + nb[k][2];
+            if (cx < 0 || cy < 0 || cx >= dim || cy >= dim || cz < 0 || cz >= nz) continue; /* grow owned planes only */
+            const long long q = (long long)cz * P + (long long)cy * dim + cx;
+            if (region[q]) continue;
+            if (abs((int)data[p] - (int)data[q]) < thr) {
+                region[q] = 1;
+                ++added;
+                stack_push(&st, q);
+            }
+        }
+    }
+    free(st.v);
+    return added;
+}
+
+/* value_at_ref on a slab whose plane 0 is global plane zoff */
+static float value_at_slab(const float* pos, const unsigned char* d, int dim, int zoff) {
+    if (!inside_f(pos, dim)) return 0;
+    int x = (int)floor(pos[0]), y = (int)floor(pos[1]), z = (int)floor(pos[2]);
+    int xu = (int)ceil(pos[0]), yu = (int)ceil(pos[1]), zu = (int)ceil(pos[2]);
+    float rx = pos[0] - x, ry = pos[1] - y, rz = pos[2] - z;
+    const size_t P = (size_t)dim * dim;
+#define D(zz, yy, xx) d[(size_t)((zz) - zoff) * P + (size_t)(yy) * dim + (xx)]
+    float a0 = rx * D(z, y, x) + (1 - rx) * D(z, y, xu);
+    float a1 = rx * D(z, yu, x) + (1 - rx) * D(z, yu, xu);
+    float a2 = rx * D(zu, y, x) + (1 - rx) * D(zu, y, xu);
+    float a3 = rx * D(zu, yu, x) + (1 - rx) * D(zu, yu, xu);
+#undef D
+    float b0 = ry * a0 + (1 - ry) * a1;
+    float b1 = ry * a2 + (1 - ry) * a3;
+    return rz * b0 + (1 - rz) * b1;
+}
+
+void pcmx_raycast_slab_host(const unsigned char* data, const unsigned char* region, int dim, int z0, int z1,
+                            int image_dim, int* state, int init, int bottom, unsigned char* image) {
+    pcmx_camera_t cam;
+    pcmx_default_camera(image_dim, &cam);
+    const int half = image_dim / 2;
+    const int zoff = z0 - 1; /* the slab buffers start at global plane z0 - 1 (halo below) */
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int py = 0; py < image_dim; ++py)
+        for (int px = 0; px < image_dim; ++px) {
+            const int x = px - half, y = py - half;
+            int* stp = state + 6 * ((size_t)py * image_dim + px);
+            float ray[3], pos[3], color;
+            int i, flags;
+            for (int k = 0; k < 3; ++k) {
+                float sc = cam.camera[k] + cam.forward[k];
+                float t = (sc + cam.right[k] * (x * cam.pixel_width)) + cam.up[k] * (y * cam.pixel_width);
+                ray[k] = t + cam.camera[k] * -1;
+            }
+            v3_normalize(ray);
+            if (init) {
+                pos[0] = cam.camera[0], pos[1] = cam.camera[1], pos[2] = cam.camera[2];
+                color = 0, i = 0, flags = 0;
+            } else {
+                memcpy(pos, stp, 3 * sizeof(float));
+                memcpy(&color, stp + 3, sizeof(float));
+                i = stp[4], flags = stp[5];
+            }
+            while (!(flags & 2) && color < 255 && i < cam.max_steps) {
+                float nxt[3];
+                for (int k = 0; k < 3; ++k) nxt[k] = pos[k] + ray[k] * cam.step_size;
+                if (!bottom && nxt[2] < (float)z0) break; /* the next sample belongs to a lower slab */
+                ++i;
+                pos[0] = nxt[0], pos[1] = nxt[1], pos[2] = nxt[2];
+                if (!inside_f(pos, dim)) {
+                    if (flags & 1) flags |= 2; /* left the convex volume: every later sample is 0 */
+                    continue;
+                }
+                flags |= 1;
+                int r = (int)value_at_slab(pos, region, dim, zoff);
+                color = (float)((double)color + (double)value_at_slab(pos, data, dim, zoff) * (0.01 + r));
+            }
+            memcpy(stp, pos, 3 * sizeof(float));
+            memcpy(stp + 3, &color, sizeof(float));
+            stp[4] = i, stp[5] = flags;
+            if (bottom) image[(size_t)py * image_dim + px] = (unsigned char)(color > 255 ? 255 : color);
+        }
+}

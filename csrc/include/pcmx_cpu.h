@@ -141,6 +141,15 @@ typedef struct {
     int max_steps;
 } pcmx_camera_t;
 void pcmx_default_camera(int image_dim, pcmx_camera_t* cam);
+/* z-slab decomposition (parallel/volume3d.py): planes [z_first, z_first + nplanes) of the hash volume (zeros
+ * outside 0..dim-1); slab flood fill over nz owned planes at data/region with read-only halo planes -1 / nz
+ * (halos bit 0 / 1), returns the voxels added; slab ray caster: the reference march restricted to samples with
+ * z >= z0 (all samples on the bottom slab), carried per pixel in state[6] = {pos xyz, colour (f32 bits), steps,
+ * flags}, slab buffers starting at global plane z0 - 1, image written by the bottom slab. */
+void pcmx_create_data_hash_slab(unsigned char* data, int dim, int z_first, int nplanes, unsigned int seed);
+long long pcmx_region3d_slab_host(const unsigned char* data, unsigned char* region, int dim, int nz, int halos, int thr);
+void pcmx_raycast_slab_host(const unsigned char* data, const unsigned char* region, int dim, int z0, int z1,
+                            int image_dim, int* state, int init, int bottom, unsigned char* image);
 /* Serial software ray caster, bit-compatible with the reference value_at() (swapped weights, B21). */
 void pcmx_raycast_serial(const unsigned char* data, const unsigned char* region, int dim, int image_dim,
                          unsigned char* image);

@@ -107,12 +107,26 @@ int pcmx_region2d_grow(const unsigned char* img, unsigned char* region, int H, i
 long long pcmx_region3d_workspace_bytes(int dim);
 int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char* region, int dim, int thr, void* ws, int batch,
                              int max_launches, hipStream_t s, int* launches_out);
+/* z-slab of a distributed volume: dim x dim x nz planes at data/region (plane 0 = first owned plane); halos bit 0 /
+ * bit 1 = plane -1 / plane nz are readable halo planes (read-only seeds, never grown); dim % 16 == 0 */
+long long pcmx_region3d_slab_workspace_bytes(int dim, int nz);
+int pcmx_region3d_grow_slab(const unsigned char* data, unsigned char* region, int dim, int nz, int halos, int thr,
+                            void* ws, int batch, int max_launches, hipStream_t s, int* launches_out);
 /* reference 0/1/2 frontier semantics, one launch per BFS level */
 int pcmx_region3d_grow_naive(const unsigned char* data, unsigned char* region, int dim, int thr, int* flag_ws,
                              int max_launches, hipStream_t s, int* launches_out);
 
 /* ---------------------------------------------------------------- volume + ray casting */
 int pcmx_volume_gen_u8(unsigned char* data, int dim, unsigned seed, hipStream_t s);
+/* planes [z_first, z_first + nplanes) of the same volume (zeros outside 0..dim-1): a z-slab with halo planes */
+int pcmx_volume_gen_slab_u8(unsigned char* data, int dim, int z_first, int nplanes, unsigned seed, hipStream_t s);
+/* z-slab stage of the distributed reference caster (bit-identical to pcmx_raycast_global with f64 colour):
+ * data/region start at global plane z0 - 1 and hold plane z1 when the slab has one above; state = 6 ints per pixel
+ * {pos xyz, colour (f32 bits), steps, flags}, initialised by the first (top) slab when init != 0; the bottom slab
+ * (bottom != 0) marches to the end and writes the image. */
+int pcmx_raycast_slab(const unsigned char* data, const unsigned char* region, int dim, int z0, int* state, int init,
+                      int bottom, unsigned char* image, int image_dim, const float* cam12, float pixel_width,
+                      float step, int max_steps, hipStream_t s);
 int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
                         int image_dim, const float* cam12, float pixel_width, float step, int max_steps, int f64_color,
                         hipStream_t s);

@@ -61,6 +61,19 @@ __global__ __launch_bounds__(256) void volume_gen_kernel(unsigned char* __restri
     data[((size_t)z * dim + y) * dim + x] = (unsigned char)(s >= 0 ? s : (int)(hash3(x, y, z, seed) % 20u));
 }
 
+// planes [z_first, z_first + gridDim.z) of the volume (zeros outside 0..dim-1): a z-slab with its halo planes
+__global__ __launch_bounds__(256) void volume_gen_slab_kernel(unsigned char* __restrict__ data, int dim, int z_first,
+                                                             unsigned seed) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, z = z_first + (int)blockIdx.z;
+    if (x >= dim) return;
+    unsigned char v = 0;
+    if (z >= 0 && z < dim) {
+        const int s = shape_value(x, y, z);
+        v = (unsigned char)(s >= 0 ? s : (int)(hash3(x, y, z, seed) % 20u));
+    }
+    data[((size_t)blockIdx.z * dim + y) * dim + x] = v;
+}
+
 // ---------------------------------------------------------------------------------- reference path
 #pragma clang fp contract(off)
 __device__ __forceinline__ float value_at_ref(float px, float py, float pz, const unsigned char* __restrict__ d, int dim) {
@@ -129,6 +142,81 @@ __global__ __launch_bounds__(256) void raycast_ref_kernel(const unsigned char* _
             color += v * (0.01f + r);
     }
     image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
+}
+
+// value_at_ref on a z-slab buffer whose plane 0 is global plane zoff (identical arithmetic)
+__device__ __forceinline__ float value_at_slab(float px, float py, float pz, const unsigned char* __restrict__ d, int dim,
+                                              int zoff) {
+    if (!(px >= 0 && px < dim - 1 && py >= 0 && py < dim - 1 && pz >= 0 && pz < dim - 1)) return 0.f;
+    const int x = (int)floorf(px), y = (int)floorf(py), z = (int)floorf(pz);
+    const int xu = (int)ceilf(px), yu = (int)ceilf(py), zu = (int)ceilf(pz);
+    const float rx = px - x, ry = py - y, rz = pz - z;
+    const size_t P = (size_t)dim * dim;
+    const unsigned char* zy = d + (size_t)(z - zoff) * P + (size_t)y * dim;
+    const unsigned char* zyu = d + (size_t)(z - zoff) * P + (size_t)yu * dim;
+    const unsigned char* zuy = d + (size_t)(zu - zoff) * P + (size_t)y * dim;
+    const unsigned char* zuyu = d + (size_t)(zu - zoff) * P + (size_t)yu * dim;
+    const float a0 = rx * zy[x] + (1 - rx) * zy[xu];
+    const float a1 = rx * zyu[x] + (1 - rx) * zyu[xu];
+    const float a2 = rx * zuy[x] + (1 - rx) * zuy[xu];
+    const float a3 = rx * zuyu[x] + (1 - rx) * zuyu[xu];
+    const float b0 = ry * a0 + (1 - ry) * a1;
+    const float b1 = ry * a2 + (1 - ry) * a3;
+    return rz * b0 + (1 - rz) * b1;
+}
+
+// z-slab stage of the distributed reference caster (parallel/volume3d.py): the march of raycast_ref_kernel<true>
+// restricted to samples with z >= z0 (every sample on the bottom slab). Rays run towards -z for the reference
+// camera, so the slabs are visited top to bottom; per pixel the state {pos xyz, colour, steps, flags (1 =
+// entered the box, 2 = done)} travels from slab to slab. A slab hands a ray over BEFORE taking a step whose
+// position lies below z0, so the next slab recomputes the very same position: the image is bit-identical to
+// the single-volume caster. data/region start at global plane z0 - 1 (halo below) and hold plane z1 (halo above).
+__global__ __launch_bounds__(256) void raycast_slab_kernel(const unsigned char* __restrict__ data,
+                                                          const unsigned char* __restrict__ region, int dim, int z0,
+                                                          int* __restrict__ state, int init, int bottom,
+                                                          unsigned char* __restrict__ image, int image_dim, Cam c) {
+    const int px = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int py = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (px >= image_dim || py >= image_dim) return;
+    const int half = image_dim / 2;
+    const int x = px - half, y = py - half;
+    float ray[3], pos[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float sc = c.cam[k] + c.fwd[k];
+        const float t = (sc + c.right[k] * (x * c.pw)) + c.up[k] * (y * c.pw);
+        ray[k] = t + c.cam[k] * -1;
+        pos[k] = c.cam[k];
+    }
+    const float l = (float)sqrt((double)(ray[0] * ray[0] + ray[1] * ray[1] + ray[2] * ray[2]));
+    ray[0] /= l, ray[1] /= l, ray[2] /= l;
+    const float sx = ray[0] * c.step, sy = ray[1] * c.step, sz = ray[2] * c.step;
+    const float hi = (float)(dim - 1);
+    int* st = state + 6 * ((size_t)py * image_dim + px);
+    int i = 0, flags = 0;
+    float color = 0.f;
+    if (!init) {
+        pos[0] = __int_as_float(st[0]), pos[1] = __int_as_float(st[1]), pos[2] = __int_as_float(st[2]);
+        color = __int_as_float(st[3]), i = st[4], flags = st[5];
+    }
+    const int zoff = z0 - 1;
+    while (!(flags & 2) && color < 255 && i < c.max_steps) {
+        const float nx = pos[0] + sx, ny = pos[1] + sy, nz = pos[2] + sz;
+        if (!bottom && nz < (float)z0) break;  // the next sample belongs to a lower slab
+        ++i;
+        pos[0] = nx, pos[1] = ny, pos[2] = nz;
+        if (!in_box(pos[0], pos[1], pos[2], hi)) {
+            if (flags & 1) flags |= 2;  // left the convex volume: every later sample is 0
+            continue;
+        }
+        flags |= 1;
+        const int r = (int)value_at_slab(pos[0], pos[1], pos[2], region, dim, zoff);
+        const float v = value_at_slab(pos[0], pos[1], pos[2], data, dim, zoff);
+        color = (float)((double)color + (double)v * (0.01 + r));
+    }
+    st[0] = __float_as_int(pos[0]), st[1] = __float_as_int(pos[1]), st[2] = __float_as_int(pos[2]);
+    st[3] = __float_as_int(color), st[4] = i, st[5] = flags;
+    if (bottom) image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
 }
 #pragma clang fp contract(on)
 
@@ -208,10 +296,18 @@ __device__ __forceinline__ unsigned pair(unsigned a, unsigned an, unsigned b, un
 // permutes slots inside aligned groups of 4, so its groups still cover 16 distinct slots mod 16.
 __device__ __forceinline__ int tex_slot(int j) { return j ^ ((j >> 3) & 3); }
 
+// A block covers 1024 consecutive texels of one z-plane in row-major (y, x) order (rows of several y when
+// dim < 1024; dim % 4 == 0 keeps a thread's 4 texels in one row), so every thread is busy (one block per row
+// left half of each 256-thread block clamped onto duplicate loads at dim 512: 466 -> 392 us). A persistent,
+// software-pipelined variant (next unit's loads in flight, double-buffered 32-KiB stage, 4 blocks/CU) measured
+// 451 us: occupancy matters more here than the pipelining.
 __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* __restrict__ data,
                                                          const unsigned char* __restrict__ region, int dim,
                                                          void* __restrict__ tex, const int* __restrict__ wide_flag) {
-    const int x = min((blockIdx.x * 256 + (int)threadIdx.x) * 4, dim - 4), y = blockIdx.y, z = blockIdx.z;
+    const size_t plane_texels = (size_t)dim * dim;
+    const size_t lin0 = (size_t)blockIdx.x * 1024;  // first texel of this block inside its plane
+    const size_t lin = min(lin0 + (size_t)threadIdx.x * 4, plane_texels - 4);
+    const int y = (int)(lin / dim), x = (int)(lin % dim), z = blockIdx.y;
     const bool wide = *wide_flag != 0;
     const int y1 = min(y + 1, dim - 1), z1 = min(z + 1, dim - 1);
     const size_t P = (size_t)dim * dim;
@@ -228,7 +324,6 @@ __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* _
         rn[q] = rn[q] ? 1u : 0u;
     }
     __shared__ uint4 stage[1024];
-    const int xb = blockIdx.x * 1024;  // first voxel of this block's row segment
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const unsigned r0 = pair(r[0], rn[0], r[1], rn[1], i), r1 = pair(r[2], rn[2], r[3], rn[3], i);
@@ -240,12 +335,81 @@ __global__ __launch_bounds__(256) void brick_pack4_kernel(const unsigned char* _
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int j = i * 256 + threadIdx.x;
-        if (xb + j >= dim) continue;
+        if (lin0 + j >= plane_texels) continue;
         const uint4 t = stage[tex_slot(j)];
+        const size_t o = (size_t)z * plane_texels + lin0 + j;
         if (wide)
-            reinterpret_cast<uint4*>(tex)[rows[0] + xb + j] = t;
+            reinterpret_cast<uint4*>(tex)[o] = t;
         else
-            reinterpret_cast<uint2*>(tex)[rows[0] + xb + j] = make_uint2(t.x, t.y);
+            reinterpret_cast<uint2*>(tex)[o] = make_uint2(t.x, t.y);
+    }
+}
+
+// 8 texels per thread (dim % 8 == 0): one aligned 8-B load per source row; the byte after it (x + 8) is the
+// low byte of the next lane's load (DPP lane shift), and one byte load per row (issued by every lane with the
+// others, used by lane 63 only) covers the wave's last lane — 16 loads per 8 texels instead of 32. 128 threads
+// x 8 texels = the same 1024-texel unit and 16-KiB stage as brick_pack4_kernel.
+__device__ __forceinline__ unsigned pair8(unsigned long long a, unsigned an, unsigned long long b, unsigned bn, int i) {
+    const unsigned a0 = (unsigned)(a >> (8 * i)) & 0xff, a1 = i < 7 ? (unsigned)(a >> (8 * i + 8)) & 0xff : an;
+    const unsigned b0 = (unsigned)(b >> (8 * i)) & 0xff, b1 = i < 7 ? (unsigned)(b >> (8 * i + 8)) & 0xff : bn;
+    return a0 | (a1 << 8) | (b0 << 16) | (b1 << 24);
+}
+
+__device__ __forceinline__ unsigned long long nz_bytes64(unsigned long long w) {  // each byte -> 0/1
+    const unsigned long long t = (((w & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | w) & 0x8080808080808080ull;
+    return t >> 7;
+}
+
+__global__ __launch_bounds__(128) void brick_pack8_kernel(const unsigned char* __restrict__ data,
+                                                         const unsigned char* __restrict__ region, int dim,
+                                                         void* __restrict__ tex, const int* __restrict__ wide_flag) {
+    const int lane = pcmx::lane_id();
+    const size_t P = (size_t)dim * dim;
+    const size_t lin0 = (size_t)blockIdx.x * 1024;
+    const size_t lin = min(lin0 + (size_t)threadIdx.x * 8, P - 8);
+    const int y = (int)(lin / dim), x = (int)(lin % dim), z = blockIdx.y;
+    const bool wide = *wide_flag != 0;
+    const int y1 = min(y + 1, dim - 1), z1 = min(z + 1, dim - 1), xn = min(x + 8, dim - 1);
+    const size_t rows[4] = {(size_t)z * P + (size_t)y * dim, (size_t)z * P + (size_t)y1 * dim,
+                            (size_t)z1 * P + (size_t)y * dim, (size_t)z1 * P + (size_t)y1 * dim};
+    unsigned long long d[4], r[4];
+    unsigned dl[4], rl[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        d[q] = *reinterpret_cast<const unsigned long long*>(data + rows[q] + x);
+        r[q] = *reinterpret_cast<const unsigned long long*>(region + rows[q] + x);
+        dl[q] = data[rows[q] + xn];
+        rl[q] = region[rows[q] + xn];
+    }
+    unsigned dn[4], rn[4];
+    const bool own_next = lane == 63 || x + 8 >= dim;  // the next lane's word is not this row's x + 8
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const unsigned dnb = (unsigned)__float_as_int(pcmx::wave_from_next(__int_as_float((int)(unsigned)d[q]))) & 0xffu;
+        const unsigned rnb = (unsigned)__float_as_int(pcmx::wave_from_next(__int_as_float((int)(unsigned)r[q]))) & 0xffu;
+        dn[q] = own_next ? dl[q] : dnb;
+        rn[q] = (own_next ? rl[q] : rnb) ? 1u : 0u;
+        r[q] = nz_bytes64(r[q]);
+    }
+    __shared__ uint4 stage[1024];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const unsigned r0 = pair8(r[0], rn[0], r[1], rn[1], i), r1 = pair8(r[2], rn[2], r[3], rn[3], i);
+        const unsigned d0 = pair8(d[0], dn[0], d[1], dn[1], i), d1 = pair8(d[2], dn[2], d[3], dn[3], i);
+        stage[tex_slot(threadIdx.x * 8 + i)] =
+            wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int j = i * 128 + threadIdx.x;
+        if (lin0 + j >= P) continue;
+        const uint4 t = stage[tex_slot(j)];
+        const size_t o = (size_t)z * P + lin0 + j;
+        if (wide)
+            reinterpret_cast<uint4*>(tex)[o] = t;
+        else
+            reinterpret_cast<uint2*>(tex)[o] = make_uint2(t.x, t.y);
     }
 }
 
@@ -392,6 +556,23 @@ extern "C" int pcmx_raycast_global(const unsigned char* data, const unsigned cha
     return (int)hipGetLastError();
 }
 
+extern "C" int pcmx_volume_gen_slab_u8(unsigned char* data, int dim, int z_first, int nplanes, unsigned seed,
+                                       hipStream_t s) {
+    if (dim <= 0 || nplanes <= 0) return PCMX_ERR_ARG;
+    volume_gen_slab_kernel<<<dim3((dim + 255) / 256, dim, nplanes), 256, 0, s>>>(data, dim, z_first, seed);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_raycast_slab(const unsigned char* data, const unsigned char* region, int dim, int z0,
+                                 int* state, int init, int bottom, unsigned char* image, int image_dim,
+                                 const float* cam12, float pixel_width, float step, int max_steps, hipStream_t s) {
+    if (dim <= 1 || image_dim <= 0 || z0 < 0 || z0 >= dim || !state) return PCMX_ERR_ARG;
+    const Cam c = make_cam(cam12, pixel_width, step, max_steps);
+    const dim3 grid((image_dim + 15) / 16, (image_dim + 15) / 16);
+    raycast_slab_kernel<<<grid, 256, 0, s>>>(data, region, dim, z0, state, init, bottom, image, image_dim, c);
+    return (int)hipGetLastError();
+}
+
 extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, void* tex,
                                hipStream_t s) {
     if (dim <= 0 || dim > 2048) return -1;
@@ -399,8 +580,12 @@ extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* r
     int* wide = reinterpret_cast<int*>(reinterpret_cast<char*>(tex) + nvox * 16);  // format flag behind the texels
     PCMX_HIP_RET(hipMemsetAsync(wide, 0, sizeof(int), s));
     data_hibit_kernel<<<1024, 256, 0, s>>>(data, nvox, wide);
-    if (dim % 4 == 0 && (reinterpret_cast<size_t>(data) | reinterpret_cast<size_t>(region)) % 4 == 0)
-        brick_pack4_kernel<<<dim3((dim / 4 + 255) / 256, dim, dim), 256, 0, s>>>(data, region, dim, tex, wide);
+    const dim3 units((unsigned)(((size_t)dim * dim + 1023) / 1024), dim);  // 1024-texel units of each z-plane
+    const size_t align = reinterpret_cast<size_t>(data) | reinterpret_cast<size_t>(region);
+    if (dim % 8 == 0 && align % 8 == 0)
+        brick_pack8_kernel<<<units, 128, 0, s>>>(data, region, dim, tex, wide);
+    else if (dim % 4 == 0 && align % 4 == 0)
+        brick_pack4_kernel<<<units, 256, 0, s>>>(data, region, dim, tex, wide);
     else
         brick_pack_kernel<<<dim3((dim + 255) / 256, dim, dim), 256, 0, s>>>(data, region, dim, tex, wide);
     return (int)hipGetLastError();

@@ -303,12 +303,15 @@ __device__ __forceinline__ unsigned long long xflood(unsigned long long R, unsig
 
 // Grows one tile (one wave) to its local fixpoint. Returns the face-change mask of the wave (bit f set if
 // face f = x-, x+, y-, y+, z-, z+ has changed voxels; with seed_faces, voxels already in the region count).
+// Volume = dim (x) x dim (y) x nz (z) planes; with halo_lo / halo_hi the planes -1 / nz are readable (a z-slab's
+// halo planes: read-only external seeds, never grown).
 __device__ unsigned grow_tile3d_bits(const unsigned char* __restrict__ data, unsigned char* __restrict__ region,
-                                     int dim, int thr, int bx, int by, int bz, bool seed_faces) {
+                                     int dim, int nz, bool halo_lo, bool halo_hi, int thr, int bx, int by, int bz,
+                                     bool seed_faces) {
     const int lane = pcmx::lane_id(), ly = lane & 7, lz = lane >> 3;
     const int x0 = bx * kBX, y = by * kBY + ly, z = bz * kBZ + lz;
     const size_t P = (size_t)dim * dim;
-    const bool row_ok = y < dim && z < dim;
+    const bool row_ok = y < dim && z < nz;
     const unsigned long long valid = !row_ok ? 0ull : (dim - x0 >= 64 ? ~0ull : ((1ull << (dim - x0)) - 1));
     unsigned long long R0 = 0, Lx = 0, Lyu = 0, Lzu = 0, ext = 0;
     if (row_ok) {
@@ -336,14 +339,14 @@ __device__ unsigned grow_tile3d_bits(const unsigned char* __restrict__ data, uns
             Lyu = similar64(d, dn, thr) & valid;
             if (ly == kBY - 1) ext |= Lyu & nonzero64(load_row(region + o + dim));
         }
-        if (z + 1 < dim) {
+        if (z + 1 < nz || (halo_hi && z + 1 == nz)) {
             const Row64 dn = load_row(data + o + P);
             Lzu = similar64(d, dn, thr) & valid;
-            if (lz == kBZ - 1) ext |= Lzu & nonzero64(load_row(region + o + P));
+            if (lz == kBZ - 1 || z + 1 == nz) ext |= Lzu & nonzero64(load_row(region + o + P));
         }
         if (ly == 0 && y > 0)
             ext |= similar64(d, load_row(data + o - dim), thr) & nonzero64(load_row(region + o - dim)) & valid;
-        if (lz == 0 && z > 0)
+        if (lz == 0 && (z > 0 || halo_lo))
             ext |= similar64(d, load_row(data + o - P), thr) & nonzero64(load_row(region + o - P)) & valid;
     }
     // links seen from the other side (rows y-1 / z-1 of this tile). The shuffles run on ALL lanes (a lane
@@ -390,8 +393,8 @@ __device__ unsigned grow_tile3d_bits(const unsigned char* __restrict__ data, uns
 }
 
 __global__ __launch_bounds__(256) void region3d_bits_kernel(const unsigned char* __restrict__ data,
-                                                           unsigned char* __restrict__ region, int dim, int thr,
-                                                           int nbx, int nby, int nbz, int epoch,
+                                                           unsigned char* __restrict__ region, int dim, int nz,
+                                                           int halos, int thr, int nbx, int nby, int nbz, int epoch,
                                                            Grow3dWs* __restrict__ ws, int* __restrict__ mark,
                                                            int* __restrict__ lists, int ntiles) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = pcmx::lane_id();
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(256) void region3d_bits_kernel(const unsigned char*
     for (int idx = blockIdx.x * 4 + w; idx < n; idx += gridDim.x * 4) {
         const int t = list_in[idx];
         const int bx = t % nbx, by = (t / nbx) % nby, bz = t / (nbx * nby);
-        const unsigned f = grow_tile3d_bits(data, region, dim, thr, bx, by, bz, epoch == 0);
+        const unsigned f = grow_tile3d_bits(data, region, dim, nz, halos & 1, halos & 2, thr, bx, by, bz, epoch == 0);
         if ((f & 64u) && lane == 0) ws->flag = 1;
         // faces whose voxels changed: the neighbour across sees new halo voxels next launch
         if (lane >= 1 && lane <= 6 && ((f >> (lane - 1)) & 1u)) {
@@ -417,22 +420,28 @@ __global__ __launch_bounds__(256) void region3d_bits_kernel(const unsigned char*
 
 // First work list: every tile holding a region voxel (16 B per thread loads of the region).
 constexpr int kSeedThreads = 256;
+// With halo planes, a tile of the first / last z-layer also scans the halo plane next to it (its region voxels
+// seed that tile); every tile also scans one plane beyond each of its z-faces, which at worst seeds a neighbour
+// of a region tile (harmless extra work).
 template <int TX, int TY, int TZ>
 __global__ __launch_bounds__(kSeedThreads) void region3d_seed_tiles_kernel(const unsigned char* __restrict__ region, int dim,
-                                                                       int nbx, int nby, Grow3dWs* __restrict__ ws,
+                                                                       int nz, int halos, int nbx, int nby,
+                                                                       Grow3dWs* __restrict__ ws,
                                                                        int* __restrict__ mark, int* __restrict__ list0) {
-    // one workgroup per (y-row of tiles, z-slab of tiles): 8 x 8 voxel rows of the full x extent
+    // one workgroup per (y-row of tiles, z-slab of tiles): 8 x (8 + 2) voxel rows of the full x extent
     const int by = blockIdx.x % nby, bz = blockIdx.x / nby;
     const size_t plane = (size_t)dim * dim;
     __shared__ int hit[64];
     if (threadIdx.x < 64) hit[threadIdx.x] = 0;
     __syncthreads();
     const int vecs_per_row = dim / 16;  // dim % 16 == 0 on this path
-    for (int i = threadIdx.x; i < TY * TZ * vecs_per_row; i += kSeedThreads) {
+    const int zmin = (halos & 1) ? -1 : 0, zmax = (halos & 2) ? nz : nz - 1;
+    for (int i = threadIdx.x; i < TY * (TZ + 2) * vecs_per_row; i += kSeedThreads) {
         const int v = i % vecs_per_row, yz = i / vecs_per_row;
-        const int y = by * TY + yz % TY, z = bz * TZ + yz / TY;
-        if (y >= dim || z >= dim) continue;
-        const pcmx::i32x4 w = *reinterpret_cast<const pcmx::i32x4*>(region + (size_t)z * plane + (size_t)y * dim + v * 16);
+        const int y = by * TY + yz % TY, z = bz * TZ - 1 + yz / TY;
+        if (y >= dim || z < zmin || z > zmax) continue;
+        const pcmx::i32x4 w = *reinterpret_cast<const pcmx::i32x4*>(region + (long long)z * (long long)plane +
+                                                                    (size_t)y * dim + v * 16);
         if ((w.x | w.y | w.z | w.w) != 0) hit[(v * 16) / TX] = 1;
     }
     __syncthreads();
@@ -525,36 +534,41 @@ extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* regio
     return h ? PCMX_ERR_NOT_CONVERGED : 0;
 }
 
-extern "C" long long pcmx_region3d_workspace_bytes(int dim) {
-    const long long nt = (long long)((dim + kBX - 1) / kBX) * ((dim + kBY - 1) / kBY) * ((dim + kBZ - 1) / kBZ);
+extern "C" long long pcmx_region3d_slab_workspace_bytes(int dim, int nz) {
+    const long long nt = (long long)((dim + kBX - 1) / kBX) * ((dim + kBY - 1) / kBY) * ((nz + kBZ - 1) / kBZ);
     return (long long)sizeof(Grow3dWs) + 3 * nt * 4;
 }
 
-// Grows `region` (0 = outside, nonzero = inside) to the 6-connected fixpoint. Host syncs once per `batch`
-// launches (a changed-flag read back); launches run on the device-built tile lists in between.
-extern "C" int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char* region, int dim, int thr, void* ws,
-                                        int batch, int max_launches, hipStream_t s, int* launches_out) {
-    if (dim <= 0 || !ws) return -1;
-    if (dim % 16 || (((uintptr_t)region) & 15)) return -1;  // seed scan reads 16-B vectors
-    const int nbx = (dim + kBX - 1) / kBX, nby = (dim + kBY - 1) / kBY, nbz = (dim + kBZ - 1) / kBZ;
-    if (nbx > 64) return -1;  // seed scan keeps one hit flag per x-tile in a 64-entry LDS array
+extern "C" long long pcmx_region3d_workspace_bytes(int dim) { return pcmx_region3d_slab_workspace_bytes(dim, dim); }
+
+// Grows `region` (0 = outside, nonzero = inside) to the 6-connected fixpoint over dim x dim x nz planes. halos bit 0
+// / bit 1: plane -1 / plane nz exist (read-only seeds of a z-slab). Host syncs once per `batch` launches (a
+// changed-flag read back); launches run on the device-built tile lists in between.
+extern "C" int pcmx_region3d_grow_slab(const unsigned char* data, unsigned char* region, int dim, int nz, int halos,
+                                       int thr, void* ws, int batch, int max_launches, hipStream_t s,
+                                       int* launches_out) {
+    if (dim <= 0 || nz <= 0 || !ws || halos < 0 || halos > 3) return PCMX_ERR_ARG;
+    if (dim % 16 || (((uintptr_t)region) & 15) || (((size_t)dim * dim) & 15)) return PCMX_ERR_ARG;  // 16-B seed scan
+    const int nbx = (dim + kBX - 1) / kBX, nby = (dim + kBY - 1) / kBY, nbz = (nz + kBZ - 1) / kBZ;
+    if (nbx > 64) return PCMX_ERR_ARG;  // seed scan keeps one hit flag per x-tile in a 64-entry LDS array
     const long long nt = (long long)nbx * nby * nbz;
-    if (nt > 0x3fffffff) return -1;
+    if (nt > 0x3fffffff) return PCMX_ERR_ARG;
     Grow3dWs* w = reinterpret_cast<Grow3dWs*>(ws);
     int* mark = reinterpret_cast<int*>(w + 1);
     int* lists = mark + nt;
     // marks = -1 (no epoch), counters = 0, then the seed tiles (epoch 0) go to list 0
     PCMX_HIP_RET(hipMemsetAsync(w, 0, sizeof(Grow3dWs), s));
     PCMX_HIP_RET(hipMemsetAsync(mark, 0xff, (size_t)nt * 4, s));
-    region3d_seed_tiles_kernel<kBX, kBY, kBZ><<<nby * nbz, kSeedThreads, 0, s>>>(region, dim, nbx, nby, w, mark, lists);
+    region3d_seed_tiles_kernel<kBX, kBY, kBZ><<<nby * nbz, kSeedThreads, 0, s>>>(region, dim, nz, halos, nbx, nby, w,
+                                                                                mark, lists);
     PCMX_HIP_RET(hipGetLastError());
     const int b = batch < 1 ? 8 : batch;
     int launches = 0, h = 1;
     while (launches < max_launches) {
         PCMX_HIP_RET(hipMemsetAsync(&w->flag, 0, sizeof(int), s));
         for (int i = 0; i < b && launches < max_launches; ++i, ++launches) {
-            region3d_bits_kernel<<<kListGrid, 256, 0, s>>>(data, region, dim, thr, nbx, nby, nbz, launches, w, mark,
-                                                         lists, (int)nt);
+            region3d_bits_kernel<<<kListGrid, 256, 0, s>>>(data, region, dim, nz, halos, thr, nbx, nby, nbz, launches,
+                                                         w, mark, lists, (int)nt);
             PCMX_HIP_RET(hipGetLastError());
         }
         PCMX_HIP_RET(hipMemcpyAsync(&h, &w->flag, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -563,6 +577,11 @@ extern "C" int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char
     }
     if (launches_out) *launches_out = launches;
     return h ? PCMX_ERR_NOT_CONVERGED : 0;
+}
+
+extern "C" int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char* region, int dim, int thr, void* ws,
+                                        int batch, int max_launches, hipStream_t s, int* launches_out) {
+    return pcmx_region3d_grow_slab(data, region, dim, dim, 0, thr, ws, batch, max_launches, s, launches_out);
 }
 
 extern "C" int pcmx_region3d_grow_naive(const unsigned char* data, unsigned char* region, int dim, int thr, int* flag_ws,

@@ -293,6 +293,27 @@ int64_t region3d_grow_(at::Tensor region, const at::Tensor& data, int64_t thr, b
     return launches;
 }
 
+// z-slab with its halo planes: (nz + 2, dim, dim) uint8 tensors; planes 1..nz are grown, plane 0 / nz + 1 are
+// read-only halo seeds when halos bit 0 / bit 1 is set (neighbour ranks' boundary planes)
+int64_t region3d_grow_slab_(at::Tensor region, const at::Tensor& data, int64_t halos, int64_t thr, int64_t batch,
+                            int64_t max_launches) {
+    check_u8_gpu(region, "region"), check_u8_gpu(data, "data");
+    TORCH_CHECK(data.dim() == 3 && data.size(1) == data.size(2) && data.size(0) >= 3 && region.sizes() == data.sizes() &&
+                    region.device() == data.device(),
+                "region3d_grow_slab_: (nz + 2, dim, dim) uint8 slabs with halo planes, on one device");
+    TORCH_CHECK(halos >= 0 && halos <= 3, "region3d_grow_slab_: halos in 0..3");
+    const at::DeviceGuard g(data.device());
+    const int dim = (int)data.size(1), nz = (int)data.size(0) - 2;
+    const size_t plane = (size_t)dim * dim;
+    auto ws = workspace(data, pcmx_region3d_slab_workspace_bytes(dim, nz));
+    int launches = 0;
+    check_rc(pcmx_region3d_grow_slab(data.data_ptr<uint8_t>() + plane, region.data_ptr<uint8_t>() + plane, dim, nz,
+                                     (int)halos, (int)thr, ws.data_ptr(), (int)batch, (int)max_launches, cur_stream(data),
+                                     &launches),
+             "region3d_grow_slab_");
+    return launches;
+}
+
 // ---------------------------------------------------------------- volume + ray casting
 void check_cubic(const at::Tensor& v, const char* what) {
     TORCH_CHECK(v.dim() == 3 && v.size(0) == v.size(1) && v.size(1) == v.size(2) && v.size(0) > 1, what,
@@ -304,6 +325,17 @@ at::Tensor volume_gen_(at::Tensor data, int64_t seed) {
     check_cubic(data, "volume_gen_");
     const at::DeviceGuard g(data.device());
     check_rc(pcmx_volume_gen_u8(data.data_ptr<uint8_t>(), (int)data.size(0), (unsigned)seed, cur_stream(data)), "volume_gen_");
+    return data;
+}
+
+at::Tensor volume_gen_slab_(at::Tensor data, int64_t z_first, int64_t seed) {
+    check_u8_gpu(data, "data");
+    TORCH_CHECK(data.dim() == 3 && data.size(1) == data.size(2) && data.size(0) >= 1,
+                "volume_gen_slab_: (nplanes, dim, dim) uint8");
+    const at::DeviceGuard g(data.device());
+    check_rc(pcmx_volume_gen_slab_u8(data.data_ptr<uint8_t>(), (int)data.size(1), (int)z_first, (int)data.size(0),
+                                     (unsigned)seed, cur_stream(data)),
+             "volume_gen_slab_");
     return data;
 }
 
@@ -328,6 +360,28 @@ at::Tensor raycast_global(const at::Tensor& data, const at::Tensor& region, int6
                                  (int)image_dim, c.data(), (float)pixel_width, (float)step, (int)max_steps, f64_color ? 1 : 0,
                                  cur_stream(data)),
              "raycast_global");
+    return img;
+}
+
+// slab buffers (nz + 2, dim, dim) starting at global plane z0 - 1; state int32 [image_dim^2, 6]
+at::Tensor raycast_slab_(const at::Tensor& data, const at::Tensor& region, int64_t z0, at::Tensor state, bool init,
+                         bool bottom, int64_t image_dim, at::ArrayRef<double> cam12, double pixel_width, double step,
+                         int64_t max_steps) {
+    check_u8_gpu(data, "data"), check_u8_gpu(region, "region");
+    check_gpu(state, "state", at::kInt);
+    TORCH_CHECK(data.dim() == 3 && data.size(1) == data.size(2) && data.size(0) >= 3 && region.sizes() == data.sizes(),
+                "raycast_slab_: (nz + 2, dim, dim) uint8 slabs");
+    TORCH_CHECK(state.is_contiguous() && state.numel() == image_dim * image_dim * 6 && state.device() == data.device(),
+                "raycast_slab_: state int32 [image_dim^2, 6] on data's device");
+    const int dim = (int)data.size(1);
+    TORCH_CHECK(z0 >= 0 && z0 + data.size(0) - 2 <= dim, "raycast_slab_: slab planes inside the volume");
+    const at::DeviceGuard g(data.device());
+    auto img = at::empty({bottom ? image_dim : 0, bottom ? image_dim : 0}, data.options());
+    auto c = cam_vec(cam12);
+    check_rc(pcmx_raycast_slab(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), dim, (int)z0, state.data_ptr<int>(),
+                               init ? 1 : 0, bottom ? 1 : 0, bottom ? img.data_ptr<uint8_t>() : nullptr, (int)image_dim,
+                               c.data(), (float)pixel_width, (float)step, (int)max_steps, cur_stream(data)),
+             "raycast_slab_");
     return img;
 }
 
@@ -509,7 +563,10 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("histeq(Tensor img) -> Tensor");
     m.def("region2d_grow_(Tensor(a!) region, Tensor img, int thr, int batch=4, int max_launches=100000) -> int");
     m.def("region3d_grow_(Tensor(a!) region, Tensor data, int thr, bool tiled=True, int batch=8, int max_launches=1000000) -> int");
+    m.def("region3d_grow_slab_(Tensor(a!) region, Tensor data, int halos, int thr, int batch=8, int max_launches=1000000) -> int");
     m.def("volume_gen_(Tensor(a!) data, int seed) -> Tensor(a!)");
+    m.def("volume_gen_slab_(Tensor(a!) data, int z_first, int seed) -> Tensor(a!)");
+    m.def("raycast_slab_(Tensor data, Tensor region, int z0, Tensor(a!) state, bool init, bool bottom, int image_dim, float[] cam12, float pixel_width, float step, int max_steps) -> Tensor");
     m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True) -> Tensor");
     m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
     m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, int batch=4) -> Tensor");
@@ -542,6 +599,9 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("raycast_global", raycast_global);
     m.impl("brick_pack", brick_pack);
     m.impl("raycast_bricked", raycast_bricked);
+    m.impl("region3d_grow_slab_", region3d_grow_slab_);
+    m.impl("volume_gen_slab_", volume_gen_slab_);
+    m.impl("raycast_slab_", raycast_slab_);
     m.impl("stencil5_", stencil5_);
     m.impl("stencil5xT_", stencil5xT_);
     m.impl("spmv_csr", spmv_csr);

@@ -10,6 +10,7 @@ from .ring import token_ring
 from .spmv import DistributedSpMV, nnz_balanced_cuts
 from .stencil import StencilSlab, reference_run
 from .topology import CartTopology, dims_create, prime_factors, split
+from .volume3d import DistributedVolume, VolumeSlab, emulate_slabs
 
 __all__ = [
     "Context", "init", "finalize", "spawn", "free_port",
@@ -17,4 +18,5 @@ __all__ = [
     "HaloExchanger2D", "global_reduce", "global_scan", "allreduce_buckets", "scatter_rows", "gather_rows",
     "grow_distributed", "scatter_tiles", "gather_tiles", "token_ring",
     "DistributedSpMV", "nnz_balanced_cuts", "StencilSlab", "reference_run",
+    "DistributedVolume", "VolumeSlab", "emulate_slabs",
 ]

@@ -131,7 +131,7 @@ def test_raycast_texture_close(gpu):
     assert abs(a.mean().item() - b.mean().item()) < 3.0
 
 
-@pytest.mark.parametrize("dim", [20, 21, 64])
+@pytest.mark.parametrize("dim", [20, 21, 64, 72])
 @pytest.mark.parametrize("hi", [128, 256])
 def test_brick_pack_texels(gpu, dim, hi):
     # texel = 2x2x2 footprint of data then region, edge-clamped; narrow 8-B texels (region in bit 7) when every

@@ -65,3 +65,34 @@ def test_region_torchrun_rccl_writes_golden(gpu, tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=cli_env())
     assert r.returncode == 0, r.stderr[-3000:]
     assert np.array_equal(bmp.read(tmp_path / "out.bmp"), bmp.read(ASSETS / "region_pic1_golden.bmp"))
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3, 4])
+def test_volume_zslabs_emulated_on_one_gpu(gpu, parts):
+    """Every slab stage of a `parts`-rank z-slab decomposition on one GPU: the slab grower (halo planes as read-only
+    seeds) and the pipelined slab caster reproduce the single-volume region and the f64 global caster bit for bit."""
+    from parallel_c_programs_amd import ops
+    from parallel_c_programs_amd.parallel import emulate_slabs
+
+    vol = ops.create_volume(512, device=gpu, seed=0)
+    reg_ref, _ = ops.region3d(vol)
+    reg_ref = (reg_ref != 0).to(torch.uint8)
+    img_ref = ops.raycast(vol, reg_ref, 64, method="global")
+    reg, img, outer = emulate_slabs(512, parts, gpu, image_dim=64)
+    assert int(reg.sum()) == 2197899 and torch.equal(reg, reg_ref)
+    assert torch.equal(img, img_ref)
+    assert outer == 1 if parts == 1 else outer >= 2
+
+
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 visible GPUs")
+def test_volume3d_torchrun_rccl(gpu, tmp_path):
+    from parallel_c_programs_amd.parallel import free_port
+
+    n = min(_ngpu(), 8)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "parallel_c_programs_amd.cli.run_volume3d",
+           "--image-dim", "64"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=cli_env(), cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["region_voxels"] == 2197899 and out["image_sum"] == 127183
