@@ -360,56 +360,75 @@ __device__ __forceinline__ unsigned long long nz_bytes64(unsigned long long w) {
     return t >> 7;
 }
 
+template <int ZP>
 __global__ __launch_bounds__(128) void brick_pack8_kernel(const unsigned char* __restrict__ data,
                                                          const unsigned char* __restrict__ region, int dim,
                                                          void* __restrict__ tex, const int* __restrict__ wide_flag) {
+    // ZP consecutive output planes per block: their ZP + 1 source planes are loaded once, all up front (ZP times
+    // the loads in flight of one plane per block, (ZP+1)/(2 ZP) of the row loads). The pack is latency-bound, not
+    // VALU- or bandwidth-bound: 1 GiB of texels took ~370 us with ZP = 1 against a 155-us 1-GiB fill (counters:
+    // 130 MB fetched); a byte-transpose (v_perm) assembly and an XCD-contiguous unit order changed nothing.
+    // Measured at 512^3: ZP 1 / 2 / 4 / 8 = 367 / 301 / 285 / 283 us (LDS-free direct stores: 537 us).
     const int lane = pcmx::lane_id();
     const size_t P = (size_t)dim * dim;
     const size_t lin0 = (size_t)blockIdx.x * 1024;
     const size_t lin = min(lin0 + (size_t)threadIdx.x * 8, P - 8);
-    const int y = (int)(lin / dim), x = (int)(lin % dim), z = blockIdx.y;
+    const int y = (int)(lin / dim), x = (int)(lin % dim), zb = blockIdx.y * ZP;
     const bool wide = *wide_flag != 0;
-    const int y1 = min(y + 1, dim - 1), z1 = min(z + 1, dim - 1), xn = min(x + 8, dim - 1);
-    const size_t rows[4] = {(size_t)z * P + (size_t)y * dim, (size_t)z * P + (size_t)y1 * dim,
-                            (size_t)z1 * P + (size_t)y * dim, (size_t)z1 * P + (size_t)y1 * dim};
-    unsigned long long d[4], r[4];
-    unsigned dl[4], rl[4];
+    const int y1 = min(y + 1, dim - 1), xn = min(x + 8, dim - 1);
+    unsigned long long d[ZP + 1][2], r[ZP + 1][2];
+    unsigned dl[ZP + 1][2], rl[ZP + 1][2];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        d[q] = *reinterpret_cast<const unsigned long long*>(data + rows[q] + x);
-        r[q] = *reinterpret_cast<const unsigned long long*>(region + rows[q] + x);
-        dl[q] = data[rows[q] + xn];
-        rl[q] = region[rows[q] + xn];
+    for (int j = 0; j <= ZP; ++j) {
+        const size_t pl = (size_t)min(zb + j, dim - 1) * P;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const size_t row = pl + (size_t)(e ? y1 : y) * dim;
+            d[j][e] = *reinterpret_cast<const unsigned long long*>(data + row + x);
+            r[j][e] = *reinterpret_cast<const unsigned long long*>(region + row + x);
+            dl[j][e] = data[row + xn];
+            rl[j][e] = region[row + xn];
+        }
     }
-    unsigned dn[4], rn[4];
+    unsigned dn[ZP + 1][2], rn[ZP + 1][2];
     const bool own_next = lane == 63 || x + 8 >= dim;  // the next lane's word is not this row's x + 8
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const unsigned dnb = (unsigned)__float_as_int(pcmx::wave_from_next(__int_as_float((int)(unsigned)d[q]))) & 0xffu;
-        const unsigned rnb = (unsigned)__float_as_int(pcmx::wave_from_next(__int_as_float((int)(unsigned)r[q]))) & 0xffu;
-        dn[q] = own_next ? dl[q] : dnb;
-        rn[q] = (own_next ? rl[q] : rnb) ? 1u : 0u;
-        r[q] = nz_bytes64(r[q]);
-    }
+    for (int j = 0; j <= ZP; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const unsigned dnb = (unsigned)__float_as_int(pcmx::wave_from_next(__int_as_float((int)(unsigned)d[j][e]))) & 0xffu;
+            const unsigned rnb = (unsigned)__float_as_int(pcmx::wave_from_next(__int_as_float((int)(unsigned)r[j][e]))) & 0xffu;
+            dn[j][e] = own_next ? dl[j][e] : dnb;
+            rn[j][e] = (own_next ? rl[j][e] : rnb) ? 1u : 0u;
+            r[j][e] = nz_bytes64(r[j][e]);
+        }
     __shared__ uint4 stage[1024];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const unsigned r0 = pair8(r[0], rn[0], r[1], rn[1], i), r1 = pair8(r[2], rn[2], r[3], rn[3], i);
-        const unsigned d0 = pair8(d[0], dn[0], d[1], dn[1], i), d1 = pair8(d[2], dn[2], d[3], dn[3], i);
-        stage[tex_slot(threadIdx.x * 8 + i)] =
-            wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
-    }
-    __syncthreads();
+    for (int k = 0; k < ZP; ++k) {
+        const int z = zb + k;
+        if (z >= dim) break;  // block-uniform
+        if (k) __syncthreads();  // the previous plane's stage has been read back
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int j = i * 128 + threadIdx.x;
-        if (lin0 + j >= P) continue;
-        const uint4 t = stage[tex_slot(j)];
-        const size_t o = (size_t)z * P + lin0 + j;
-        if (wide)
-            reinterpret_cast<uint4*>(tex)[o] = t;
-        else
-            reinterpret_cast<uint2*>(tex)[o] = make_uint2(t.x, t.y);
+        for (int i = 0; i < 8; ++i) {
+            const unsigned r0 = pair8(r[k][0], rn[k][0], r[k][1], rn[k][1], i);
+            const unsigned r1 = pair8(r[k + 1][0], rn[k + 1][0], r[k + 1][1], rn[k + 1][1], i);
+            const unsigned d0 = pair8(d[k][0], dn[k][0], d[k][1], dn[k][1], i);
+            const unsigned d1 = pair8(d[k + 1][0], dn[k + 1][0], d[k + 1][1], dn[k + 1][1], i);
+            stage[tex_slot(threadIdx.x * 8 + i)] =
+                wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = i * 128 + threadIdx.x;
+            if (lin0 + j >= P) continue;
+            const uint4 t = stage[tex_slot(j)];
+            const size_t o = (size_t)z * P + lin0 + j;
+            if (wide)
+                reinterpret_cast<uint4*>(tex)[o] = t;
+            else
+                reinterpret_cast<uint2*>(tex)[o] = make_uint2(t.x, t.y);
+        }
     }
 }
 
@@ -583,7 +602,7 @@ extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* r
     const dim3 units((unsigned)(((size_t)dim * dim + 1023) / 1024), dim);  // 1024-texel units of each z-plane
     const size_t align = reinterpret_cast<size_t>(data) | reinterpret_cast<size_t>(region);
     if (dim % 8 == 0 && align % 8 == 0)
-        brick_pack8_kernel<<<units, 128, 0, s>>>(data, region, dim, tex, wide);
+        brick_pack8_kernel<4><<<dim3(units.x, (dim + 3) / 4), 128, 0, s>>>(data, region, dim, tex, wide);
     else if (dim % 4 == 0 && align % 4 == 0)
         brick_pack4_kernel<<<units, 256, 0, s>>>(data, region, dim, tex, wide);
     else
