@@ -745,7 +745,12 @@ __global__ __launch_bounds__(C::kThreads, 1) void sgemm_rs_kernel(const float* _
             for (int i = 0; i < C::MT; ++i) {
 #pragma unroll
                 for (int j = 0; j < C::NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[s][j], acc[i][j], 0, 0, 0);
+                {
+                    if constexpr (SCHED == 4)  // accumulators forced into AGPRs (AGPR-form MFMA)
+                        asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[i][s]), "v"(b[s][j]));
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[s][j], acc[i][j], 0, 0, 0);
+                }
                 filler(s * C::MT + i);
             }
     };
@@ -833,6 +838,7 @@ __global__ __launch_bounds__(C::kThreads, 1) void sgemm_rs_kernel(const float* _
     if (t + 1 < nk) stage(t++, std::true_type{}, std::false_type{});
     stage(t, std::false_type{}, std::false_type{});
 
+    if constexpr (SCHED == 4) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> accvgpr_read
     // epilogue: tile j holds columns 4c+j, so a lane's 4 tiles form one contiguous 16-B store
 #pragma unroll
     for (int i = 0; i < C::MT; ++i)
@@ -1291,6 +1297,8 @@ extern "C" int pcmx_sgemm_lab_variant(const float* A, const float* B, float* C, 
         case 20: return launch_rs<3, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 21: return launch_rs<3, true, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 22: return launch_rs<2, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 23: return launch_rs<4, true, CfgRS8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 24: return launch_rs<4, true>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         default: return -1;
     }
 }
