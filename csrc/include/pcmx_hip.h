@@ -78,6 +78,10 @@ int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const 
 /* same with an explicit tile shape: rows = f32x4 rows per lane, 16 (8 waves, the default) or 8 (16 waves) */
 int pcmx_scan_f32_rows(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
                        unsigned* err_flag, int rows, hipStream_t s);
+/* schedule A/B entry (csrc/kernels/scan.hip): 0 persistent R16xW8, 1 persistent R8xW16, 2 parked-tile R16xW8,
+ * 3 parked-tile R8xW16, 4 parked-tile R16xW8 with early polls (pcmx_scan_f32) */
+int pcmx_scan_f32_variant(const float* x, float* out, long long n, int exclusive, const float* init_dev,
+                          void* workspace, unsigned* err_flag, int variant, hipStream_t s);
 /* synchronises s; PCMX_ERR_TIMEOUT if the last scan on this workspace gave up a look-back, else 0 */
 int pcmx_scan_check(const void* workspace, hipStream_t s);
 

@@ -2,21 +2,24 @@
 // "prefix-scan 1e9 f32" kernel. Reference ancestor: the histogram CDF (ref 4-histogram-equalization-
 // openmp-pthreads/histogram_serial.c:29-34) generalised to 1e9 elements.
 //
-// MI355X design (measured in scripts/scan_lab.hip; 1e9 f32 on one MI355X):
+// MI355X design (measured in scripts/scan_lab.hip and scripts/scan_tune.py; 1e9 f32 on one MI355X):
 //  * HBM traffic is one read + one write of the array (8 B/element); the roofline is a tiled copy
 //    (~1.28 ms = 6.2 TB/s for 128-KiB tiles; 64-KiB tiles stream markedly worse on this part).
 //  * Tile = 128 KiB: 8 waves x 16 f32x4 rows per lane (or 16 waves x 8 rows), in-register wave scans.
 //  * PERSISTENT + SOFTWARE-PIPELINED: one 512-thread block per CU walks tiles in ticket order and keeps
-//    the NEXT tile's loads in flight (second register buffer) while the current tile's look-back polls its
-//    predecessors, so the look-back latency (agent-scope polls cross the 8 XCD L2s) hides behind HBM
-//    traffic. A one-tile-per-block grid pays that latency in the open: 1.9 ms -> 1.55 ms here.
+//    the NEXT tile's loads in flight (second register buffer) while a look-back polls predecessors.
+//  * PRODUCTION = the PARKED-TILE schedule (scan_parked_kernel, kEarly): tile t is scanned and its aggregate
+//    published, its tile-local results are parked in LDS, and it is looked back and written out during the
+//    block's NEXT tile, with the first round of polls sent before that tile's scan. Every predecessor then
+//    published an iteration ago and the look-back round trip overlaps the scan: 1.47 ms (persistent schedule,
+//    look-back right after the scan, scan_persistent_kernel) -> 1.41 ms (parked) -> 1.27 ms = 6.29 TB/s
+//    (parked + early polls); the look-back-free structure bound is 1.23 ms.
 //  * Tiles come from an atomic ticket, so a tile is only ever owned by a RUNNING block and every predecessor
 //    of the oldest unfinished tile has published: the look-back cannot deadlock whatever the dispatcher does.
 //  * Hand-off = 8-byte {flag, value} granules written with ONE agent-scope relaxed atomic store and polled
-//    with agent-scope relaxed loads (cdna_hip_programming.md G16 recipe R2); one wave looks back 64 tiles per
-//    poll (wider per-lane windows measured slower). Status words and the ticket are zeroed by a
-//    hipMemsetAsync on the same stream before every launch. Spins are bounded: a look-back that gives up
-//    marks its result invalid in the workspace (ws->timeout) AND in the caller's sticky error word
+//    with agent-scope relaxed loads (cdna_hip_programming.md G16 recipe R2). Status words and the ticket are
+//    zeroed by a hipMemsetAsync on the same stream before every launch. Spins are bounded: a look-back that
+//    gives up marks its result invalid in the workspace (ws->timeout) AND in the caller's sticky error word
 //    (err_flag, system-scope atomic OR: it may live in host-mapped pinned memory), which pcmx_scan_check /
 //    the torch op turn into an error instead of a silently wrong prefix.
 #include "pcmx_common.h"
@@ -225,6 +228,219 @@ __global__ __launch_bounds__(W * kWave) void scan_persistent_kernel(const float*
     }
 }
 
+// ---- PARKED-TILE schedule (look-back one iteration late).
+// The persistent schedule above looks tile t back right after scanning it, while its neighbours t-1, t-2, ...
+// are being scanned by other blocks at the same moment: each look-back waits for aggregates that are still
+// being produced, and that publication chain cost ~17% (1.23 ms without a look-back vs 1.46 ms, see
+// profiles/r1_workloads/scan_lookback_ab.txt). Here a block scans tile t (publishing its aggregate), parks the
+// tile-local results in LDS (128 KiB of the 160 KiB) and only looks t back and writes it out during its NEXT
+// tile: by then every predecessor published its aggregate an iteration ago, so the look-back is one round of
+// polls. The inclusive prefixes now trail by one iteration (~grid tiles), so one wave polls 8 windows of 64
+// predecessors with all loads issued at once and combines them newest-first. Each thread parks and later reads
+// back only its own f32x4 slots (no barrier guards the park buffer).
+constexpr int kParkWindows = 8;
+
+using ParkPoll = unsigned long long[kParkWindows];
+
+// One round of polls: lane l of window k reads the status of tile look - l - 64k (all loads in flight at once).
+__device__ __forceinline__ void parked_poll(long long tile, long long look, ScanWs* ws, ParkPoll& sv) {
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
+    const int lane = pcmx::lane_id();
+#pragma unroll
+    for (int k = 0; k < kParkWindows; ++k) {
+        const long long idx = look - lane - (long long)k * kWave;
+        sv[k] = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : pack(kFlagIncl, 0.f);
+#ifdef PCMX_FAULT_INJECT
+        if (tile == kFaultTile) sv[k] = 0ull;
+#endif
+    }
+    (void)tile;
+}
+
+// Exclusive prefix of `tile` from its predecessors' granules; `polled` = sv already holds the first round.
+__device__ __forceinline__ float parked_lookback(long long tile, ScanWs* ws, unsigned* err_flag, ParkPoll& sv,
+                                                bool polled) {
+    const int lane = pcmx::lane_id();
+    float acc = 0.f;  // lane-partial sum of the predecessors accounted for so far
+    long long look = tile - 1;
+    unsigned spins = 0;
+    while (true) {
+        if (!polled) parked_poll(tile, look, ws, sv);
+        polled = false;
+        bool done = false, stall = false;
+#pragma unroll
+        for (int k = 0; k < kParkWindows; ++k) {
+            if (done || stall) break;  // wave-uniform
+            const unsigned flag = (unsigned)(sv[k] >> 32);
+            const float val = __uint_as_float((unsigned)sv[k]);
+            const unsigned long long m_incl = __ballot(flag == kFlagIncl);
+            const unsigned long long m_zero = __ballot(flag == 0u);
+            if (m_incl != 0ull) {
+                const int first = __builtin_ctzll(m_incl);
+                const unsigned long long need = (first == 63) ? ~0ull : ((1ull << (first + 1)) - 1ull);
+                if ((m_zero & need) == 0ull) {
+                    acc += lane <= first ? val : 0.f;
+                    done = true;
+                } else {
+                    stall = true;
+                }
+            } else if (m_zero == 0ull) {
+                acc += val;
+                look -= kWave;
+            } else {
+                stall = true;
+            }
+        }
+        if (done) break;
+        if (stall) {
+            if (++spins > kSpinLimit) {  // bounded spin, reported as in the persistent schedule
+                if (lane == 0) {
+                    atomicExch(&ws->timeout, 1u);
+                    if (err_flag) __hip_atomic_fetch_or(err_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return pcmx::wave_reduce<float, 0>(acc);
+}
+
+// Looks back `prev` (wave 0), publishes its inclusive prefix and writes it out from the park buffer.
+template <int R, int W>
+__device__ __forceinline__ void parked_flush(float* __restrict__ out, long long n, long long prev, float agg_prev,
+                                             float init, ScanWs* ws, unsigned* err_flag, const f32x4* park,
+                                             float* s_prefix, unsigned* s_next, unsigned ticket, ParkPoll& sv,
+                                             bool polled) {
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
+    const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
+    if (prev >= 0 && wave == 0) {
+        const float prefix = prev == 0 ? 0.f : parked_lookback(prev, ws, err_flag, sv, polled);
+        if (lane == 0) {
+            if (prev != 0)
+                __hip_atomic_store(&status[prev], pack(kFlagIncl, prefix + agg_prev), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            *s_prefix = init + prefix;
+        }
+    }
+    if (threadIdx.x == 0) *s_next = ticket;
+    __syncthreads();
+    if (prev < 0) return;
+    const float off = *s_prefix;
+    const long long base = prev * Tile<R, W>::kElems + (long long)wave * Tile<R, W>::kWaveItems;
+    const bool full = (prev + 1) * Tile<R, W>::kElems <= n;  // block-uniform
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const f32x4 o = park[(wave * R + r) * kWave + lane] + off;
+        const long long e = base + r * 256 + lane * 4;
+        if (full || e + 3 < n) {
+            __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + e));
+        } else {
+            if (e < n) out[e] = o.x;
+            if (e + 1 < n) out[e + 1] = o.y;
+            if (e + 2 < n) out[e + 2] = o.z;
+        }
+    }
+}
+
+// One iteration: scan `cur` (in v) and publish its aggregate, issue the loads of `next` into vn, take a ticket,
+// flush `prev` from the park buffer, park `cur`. Returns cur's aggregate (thread 0 needs it one iteration later).
+template <int R, int W, bool kEarly>
+__device__ __forceinline__ float parked_step(const float* __restrict__ in, float* __restrict__ out, long long n,
+                                             long long cur, f32x4 (&v)[R], long long next, f32x4 (&vn)[R],
+                                             long long prev, float agg_prev, long long ntiles, int exclusive, float init,
+                                             ScanWs* ws, unsigned* err_flag, f32x4* park, float* s_wave_tot,
+                                             float* s_prefix, unsigned* s_next) {
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
+    const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
+    // kEarly: wave 0 sends prev's first round of polls BEFORE this tile's scan, so their round trip overlaps it
+    ParkPoll sv;
+    const bool polled = kEarly && wave == 0 && prev > 0;
+    if (polled) parked_poll(prev, prev - 1, ws, sv);
+    float carry = 0.f;
+    float lane_excl[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        v[r].y += v[r].x;
+        v[r].z += v[r].y;
+        v[r].w += v[r].z;
+        const float incl = pcmx::wave_inclusive_scan(v[r].w);
+        float excl = __shfl_up(incl, 1, kWave);
+        if (lane == 0) excl = 0.f;
+        lane_excl[r] = carry + excl;
+        carry += __shfl(incl, kWave - 1, kWave);
+    }
+    if (lane == 0) s_wave_tot[wave] = carry;
+    __syncthreads();
+    float agg = 0.f, wexcl = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const float t = s_wave_tot[w];
+        wexcl += w < wave ? t : 0.f;
+        agg += t;
+    }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&status[cur], pack(cur == 0 ? kFlagIncl : kFlagAgg, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (next < ntiles) load_tile<R, W>(in, n, next, vn);
+    const unsigned ticket = threadIdx.x == 0 ? atomicAdd(&ws->ticket, 1u) : 0u;
+    parked_flush<R, W>(out, n, prev, agg_prev, init, ws, err_flag, park, s_prefix, s_next, ticket, sv, polled);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const float b = wexcl + lane_excl[r];
+        f32x4 o;
+        if (exclusive) {
+            o.x = b;
+            o.y = b + v[r].x;
+            o.z = b + v[r].y;
+            o.w = b + v[r].z;
+        } else {
+            o = v[r] + b;
+        }
+        park[(wave * R + r) * kWave + lane] = o;
+    }
+    return agg;
+}
+
+template <int R, int W, bool kEarly>
+__global__ __launch_bounds__(W * kWave) void scan_parked_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                long long n, long long ntiles, int exclusive,
+                                                                const float* init_dev, ScanWs* ws, unsigned* err_flag) {
+    __shared__ f32x4 park[W * R * kWave];
+    __shared__ float s_wave_tot[W];
+    __shared__ float s_prefix;
+    __shared__ unsigned s_tile[2];
+    const float init = init_dev ? *init_dev : 0.f;
+    f32x4 va[R], vb[R];
+    if (threadIdx.x == 0) {
+        s_tile[0] = atomicAdd(&ws->ticket, 1u);
+        s_tile[1] = atomicAdd(&ws->ticket, 1u);
+    }
+    __syncthreads();
+    long long ta = s_tile[0], tb = s_tile[1], prev = -1;
+    if (ta >= ntiles) return;
+    float agg_prev = 0.f;
+    load_tile<R, W>(in, n, ta, va);
+    // unrolled by two so both register buffers are statically named; every exit is block-uniform and ends with
+    // the flush of the last parked tile
+    while (true) {
+        agg_prev = parked_step<R, W, kEarly>(in, out, n, ta, va, tb, vb, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
+                                     park, s_wave_tot, &s_prefix, &s_tile[0]);
+        prev = ta;
+        ta = s_tile[0];
+        if (tb >= ntiles) break;
+        agg_prev = parked_step<R, W, kEarly>(in, out, n, tb, vb, ta, va, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
+                                     park, s_wave_tot, &s_prefix, &s_tile[0]);
+        prev = tb;
+        tb = s_tile[0];
+        if (ta >= ntiles) break;
+    }
+    __syncthreads();  // every wave has read s_prefix of the last step before wave 0 rewrites it
+    ParkPoll sv;
+    parked_flush<R, W>(out, n, prev, agg_prev, init, ws, err_flag, park, &s_prefix, &s_tile[1], 0u, sv, false);
+}
+
 inline long long num_tiles(long long n) { return (n + kTileElems - 1) / kTileElems; }
 
 int device_cus() {
@@ -239,26 +455,35 @@ int device_cus() {
 
 extern "C" long long pcmx_scan_workspace_bytes(long long n) { return (long long)sizeof(ScanWs) + num_tiles(n) * 8; }
 
-extern "C" int pcmx_scan_f32_rows(const float* x, float* out, long long n, int exclusive, const float* init_dev,
-                                  void* workspace, unsigned* err_flag, int rows, hipStream_t s) {
+extern "C" int pcmx_scan_f32_variant(const float* x, float* out, long long n, int exclusive, const float* init_dev,
+                                     void* workspace, unsigned* err_flag, int variant, hipStream_t s) {
     if (n <= 0) return 0;
-    if (rows != 8 && rows != 16) return PCMX_ERR_ARG;
+    if (variant < 0 || variant > 4) return PCMX_ERR_ARG;
     if ((((uintptr_t)x) & 15u) || (((uintptr_t)out) & 15u) || !workspace) return PCMX_ERR_ARG;
     const long long tiles = num_tiles(n);
     if (tiles > 0x7fffffffLL) return PCMX_ERR_ARG;
     PCMX_HIP_RET(hipMemsetAsync(workspace, 0, sizeof(ScanWs) + (size_t)tiles * 8, s));
     ScanWs* ws = reinterpret_cast<ScanWs*>(workspace);
     const unsigned grid = (unsigned)(tiles < device_cus() ? tiles : device_cus());  // one resident block per CU
-    if (rows == 8)
-        scan_persistent_kernel<8, 16><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag);
-    else
-        scan_persistent_kernel<16, 8><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag);
+    switch (variant) {
+        case 0: scan_persistent_kernel<16, 8><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        case 1: scan_persistent_kernel<8, 16><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        case 2: scan_parked_kernel<16, 8, false><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        case 3: scan_parked_kernel<8, 16, false><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        default: scan_parked_kernel<16, 8, true><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+    }
     return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_scan_f32_rows(const float* x, float* out, long long n, int exclusive, const float* init_dev,
+                                  void* workspace, unsigned* err_flag, int rows, hipStream_t s) {
+    if (rows != 8 && rows != 16) return PCMX_ERR_ARG;
+    return pcmx_scan_f32_variant(x, out, n, exclusive, init_dev, workspace, err_flag, rows == 16 ? 4 : 1, s);
 }
 
 extern "C" int pcmx_scan_f32(const float* x, float* out, long long n, int exclusive, const float* init_dev, void* workspace,
                              unsigned* err_flag, hipStream_t s) {
-    return pcmx_scan_f32_rows(x, out, n, exclusive, init_dev, workspace, err_flag, 16, s);
+    return pcmx_scan_f32_variant(x, out, n, exclusive, init_dev, workspace, err_flag, 4, s);
 }
 
 extern "C" int pcmx_scan_check(const void* workspace, hipStream_t s) {

@@ -100,6 +100,34 @@ def test_scan_integer_exact(gpu):
     assert torch.equal(out.long(), torch.cumsum(x.long(), 0))
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_scan_schedules_exact(gpu, variant):
+    """Every scan schedule (persistent / parked-tile / parked + early polls) on ragged sizes, exclusive, a device
+    init and in place; small integers keep every prefix exact in f32."""
+    import ctypes
+
+    from parallel_c_programs_amd._native import hip_lib
+
+    lib = hip_lib()
+    lib.pcmx_scan_workspace_bytes.restype = ctypes.c_longlong
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for m in (1, 5, 32768, 32769, 300_001, 32768 * 700 + 13):
+        x = torch.randint(-8, 9, (m,), device=gpu).float()
+        ws = torch.empty(lib.pcmx_scan_workspace_bytes(ctypes.c_longlong(m)), dtype=torch.uint8, device=gpu)
+        init = torch.tensor([3.0], device=gpu)
+        ref = torch.cumsum(x.double(), 0)
+        for exclusive, y, src, want in ((0, torch.empty_like(x), x, ref + 3.0),
+                                        (1, torch.empty_like(x), x, torch.cat([ref.new_zeros(1), ref[:-1]]) + 3.0),
+                                        (0, None, x.clone(), ref + 3.0)):
+            y = src if y is None else y  # in place
+            rc = lib.pcmx_scan_f32_variant(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                           ctypes.c_longlong(m), exclusive, ctypes.c_void_p(init.data_ptr()),
+                                           ctypes.c_void_p(ws.data_ptr()), None, variant, stream)
+            assert rc == 0
+            assert lib.pcmx_scan_check(ctypes.c_void_p(ws.data_ptr()), stream) == 0
+            assert torch.equal(y.double(), want), (m, exclusive)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 16])
 def test_sgemm_identity_asymmetric(gpu, variant):
     # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
