@@ -101,7 +101,7 @@ int main(int argc, char** argv) {
                                   cam.max_steps, 1, s));
     } else {
         CHECK(pcmx_brick_pack(data, region, dim, tex, s));
-        CHECK(pcmx_raycast_bricked(tex, dim, image, image_dim, cam12, cam.pixel_width, cam.step_size, cam.max_steps, 0, s));
+        CHECK(pcmx_raycast_bricked(tex, dim, image, image_dim, cam12, cam.pixel_width, cam.step_size, cam.max_steps, 0, 0, s));
     }
     CHECK(hipStreamSynchronize(s));
     t1 = pcmx_wtime();

@@ -138,9 +138,11 @@ int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, 
  * (8-byte texels when every data value < 128, else 16-byte; the format flag is stored behind the texels),
  * dim <= 2048 */
 int pcmx_brick_pack(const unsigned char* data, const unsigned char* region, int dim, void* tex, hipStream_t s);
-/* texture ray caster; batch = steps per prefetch batch (1, 4, 8, 16; 0 = 4, the measured best) */
+/* texture ray caster; batch = steps per prefetch batch (1, 4, 8, 16; 0 = 16, the measured best); segments = waves
+ * marching one ray patch, each a contiguous share of the step range (1, 2, 4; 0 = the measured best) */
 int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* image, int image_dim,
-                         const float* cam12, float pixel_width, float step, int max_steps, int batch, hipStream_t s);
+                         const float* cam12, float pixel_width, float step, int max_steps, int batch, int segments,
+                         hipStream_t s);
 
 /* ---------------------------------------------------------------- stencil */
 int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, int ld, int r0, int r1, long long global_row0,

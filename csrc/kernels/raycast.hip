@@ -11,7 +11,9 @@
 //    trilinear sample of both volumes is ONE load instead of 16 byte loads; texel-centre addressing,
 //    clamp-to-edge and 8-bit fixed-point weights emulate cudaFilterModeLinear + cudaReadModeNormalizedFloat.
 //    Rays are clipped analytically to the volume and only the steps inside are visited (prefetched in
-//    batches). 512^2 image of the 512^3 reference volume: 3.18 -> 1.66 ms per frame including the pack.
+//    batches of 16 steps; only the raw texels stay live across a batch) and every 16x4 ray patch is split over
+//    4 waves by step range (partial colours composed in ray order). 512^2 image of the 512^3 reference volume:
+//    march 2.7 -> 1.16 -> 0.83 ms; frame (pack + march) 3.18 -> 1.66 -> ~1.14 ms.
 //  * raycast_global marches positions by repeated f32 adds exactly like the reference, but skips sampling
 //    while the ray is outside the volume's bounding box (the adds still run, so positions are unchanged)
 //    and stops once the ray has left it (a convex box cannot be re-entered): identical images, far fewer
@@ -19,6 +21,8 @@
 //  * 16x16 pixel workgroups (4 wave64s of 16x4 pixels): neighbouring rays share cache lines.
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -450,12 +454,17 @@ __device__ __forceinline__ float q8(float f) { return rintf(f * 256.f) * (1.f / 
 // per batch (2*D texel loads in flight) and consumed in order with the reference's termination tests (stop at
 // colour >= 255, stop when the ray leaves the convex box). Positions differ from the reference's repeated
 // f32 adds by rounding only (~1e-3 voxel), below the 8-bit weight quantum of the emulated texture filter.
-template <int D, bool WIDE>
+template <int D, bool WIDE, int SEG>
 __device__ __forceinline__ void raycast_tex_march(const void* __restrict__ texv, int dim,
-                                                  unsigned char* __restrict__ image, int image_dim, const Cam& c) {
-    const int px = blockIdx.x * 16 + (threadIdx.x & 15);  // (8x8-pixel waves measured no faster)
-    const int py = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (px >= image_dim || py >= image_dim) return;
+                                                  unsigned char* __restrict__ image, int image_dim, const Cam& c,
+                                                  float* s_part) {
+    // SEG waves share one 16x4 ray patch, each marching 1/SEG of the clipped step range (see raycast_tex_kernel)
+    constexpr int kRows = 16 / SEG;  // pixel rows per 4-wave block
+    const int lane = pcmx::lane_id(), wave = threadIdx.x / pcmx::kWave, g = wave / SEG, seg = wave % SEG;
+    const int px = blockIdx.x * 16 + (lane & 15);  // (8x8-pixel waves measured no faster)
+    const int py = blockIdx.y * kRows + g * 4 + (lane >> 4);
+    const bool valid = px < image_dim && py < image_dim;
+    if (SEG == 1 && !valid) return;
     const int half = image_dim / 2;
     const int x = px - half, y = py - half;
     float ray[3];
@@ -481,63 +490,93 @@ __device__ __forceinline__ void raycast_tex_march(const void* __restrict__ texv,
     }
     const size_t P = (size_t)dim * dim;
     float color = 0.f;
-    if (k_lo <= k_hi) {
-        const int k0 = max(1, (int)floorf(k_lo) - 1);
-        const int k1 = min(c.max_steps, (int)ceilf(k_hi) + 1);
+    if (valid && k_lo <= k_hi) {
+        int k0 = max(1, (int)floorf(k_lo) - 1);
+        int k1 = min(c.max_steps, (int)ceilf(k_hi) + 1);
+        if (SEG > 1) {  // this wave's share of [k0, k1]; the in-box steps of a convex box are contiguous
+            const int len = (k1 - k0 + SEG) / SEG;
+            k0 += seg * len;
+            k1 = min(k1, k0 + len - 1);
+        }
+        // texel-centre addressing (sample at p - 0.5), clamp-to-edge, 8-bit fractional weights
+        auto tap = [&](int step, float& ax, float& ay, float& az, bool& inb, bool opaque) -> size_t {
+            float kk = (float)step;
+            if (opaque) asm volatile("" : "+v"(kk));  // recompute at use: keeps the compiler from holding the
+                                                     // issue-time values live across the batch
+            const float p0 = fmaf(kk, sv[0], c.cam[0]), p1 = fmaf(kk, sv[1], c.cam[1]), p2 = fmaf(kk, sv[2], c.cam[2]);
+            inb = in_box(p0, p1, p2, hi);
+            const float fx = p0 - 0.5f, fy = p1 - 0.5f, fz = p2 - 0.5f;
+            int x0 = (int)floorf(fx), y0 = (int)floorf(fy), z0 = (int)floorf(fz);
+            ax = q8(fx - x0), ay = q8(fy - y0), az = q8(fz - z0);
+            if (x0 < 0) x0 = 0, ax = 0.f;
+            if (y0 < 0) y0 = 0, ay = 0.f;
+            if (z0 < 0) z0 = 0, az = 0.f;
+            x0 = min(x0, dim - 1), y0 = min(y0, dim - 1), z0 = min(z0, dim - 1);
+            return (size_t)z0 * P + ((unsigned)y0 * (unsigned)dim + (unsigned)x0);  // row part < 2^32 (dim <= 2048)
+        };
+        using Texel = typename std::conditional<WIDE, uint4, uint2>::type;
         bool entered = false, active = true;
         for (int i = k0; active && i <= k1 && color < 255.f; i += D) {
-            uint4 t[D];  // data z, data z+1, region z, region z+1 (4 corners each)
-            float ax[D], ay[D], az[D];
-            bool inb[D];
+            // only the raw texels stay live across the batch (2 or 4 VGPRs per step in flight); the weights are
+            // recomputed at use, so deep batches keep the occupancy
+            Texel q[D];
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                const float kk = (float)(i + k);
-                const float p0 = fmaf(kk, sv[0], c.cam[0]), p1 = fmaf(kk, sv[1], c.cam[1]), p2 = fmaf(kk, sv[2], c.cam[2]);
-                inb[k] = i + k <= k1 && in_box(p0, p1, p2, hi);
-                // texel-centre addressing: sample at p - 0.5, clamp-to-edge
-                const float fx = p0 - 0.5f, fy = p1 - 0.5f, fz = p2 - 0.5f;
-                int x0 = (int)floorf(fx), y0 = (int)floorf(fy), z0 = (int)floorf(fz);
-                ax[k] = q8(fx - x0), ay[k] = q8(fy - y0), az[k] = q8(fz - z0);
-                if (x0 < 0) x0 = 0, ax[k] = 0.f;
-                if (y0 < 0) y0 = 0, ay[k] = 0.f;
-                if (z0 < 0) z0 = 0, az[k] = 0.f;
-                x0 = min(x0, dim - 1), y0 = min(y0, dim - 1), z0 = min(z0, dim - 1);
-                const unsigned o = (unsigned)y0 * (unsigned)dim + (unsigned)x0;  // < 2^32 for dim <= 2048
-                // unconditional, always in-bounds load (no masked-load branch); unused when !inb
-                if constexpr (WIDE) {
-                    t[k] = reinterpret_cast<const uint4*>(texv)[(size_t)z0 * P + o];
-                } else {
-                    const uint2 q = reinterpret_cast<const uint2*>(texv)[(size_t)z0 * P + o];
-                    t[k] = make_uint4(q.x & 0x7f7f7f7fu, q.y & 0x7f7f7f7fu, (q.x >> 7) & 0x01010101u, (q.y >> 7) & 0x01010101u);
-                }
+                float ax, ay, az;
+                bool inb;
+                q[k] = reinterpret_cast<const Texel*>(texv)[tap(i + k, ax, ay, az, inb, false)];  // always in bounds
             }
 #pragma unroll
             for (int k = 0; k < D; ++k) {
                 const bool live = active && i + k <= k1 && color < 255.f;
                 active = live;
                 if (!live) continue;
-                if (!inb[k]) {  // texture fetches outside never add colour; a convex box is never re-entered
+                float ax, ay, az;
+                bool inb;
+                (void)tap(i + k, ax, ay, az, inb, true);
+                if (!inb) {  // texture fetches outside never add colour; a convex box is never re-entered
                     if (entered) active = false;
                     continue;
                 }
                 entered = true;
-                const float d = (1.f - az[k]) * bilerp4(t[k].x, ax[k], ay[k]) + az[k] * bilerp4(t[k].y, ax[k], ay[k]);
-                const float rr = (1.f - az[k]) * bilerp4(t[k].z, ax[k], ay[k]) + az[k] * bilerp4(t[k].w, ax[k], ay[k]);
+                uint4 t;  // data z, data z+1, region z, region z+1 (4 corners each)
+                if constexpr (WIDE)
+                    t = q[k];
+                else
+                    t = make_uint4(q[k].x & 0x7f7f7f7fu, q[k].y & 0x7f7f7f7fu, (q[k].x >> 7) & 0x01010101u,
+                                   (q[k].y >> 7) & 0x01010101u);
+                const float d = (1.f - az) * bilerp4(t.x, ax, ay) + az * bilerp4(t.y, ax, ay);
+                const float rr = (1.f - az) * bilerp4(t.z, ax, ay) + az * bilerp4(t.w, ax, ay);
                 const int r = (int)rr;  // 255 * normalised region tap, region voxels hold 1
                 color += d * (0.01f + r);
             }
         }
     }
+    if (SEG > 1) {  // segment partial colours compose in ray order; a saturated prefix ends the ray
+        s_part[threadIdx.x] = color;
+        __syncthreads();
+        if (seg != 0 || !valid) return;
+        color = 0.f;
+#pragma unroll
+        for (int q = 0; q < SEG; ++q)
+            if (color < 255.f) color += s_part[(g * SEG + q) * pcmx::kWave + lane];
+    }
     image[py * image_dim + px] = (unsigned char)(color > 255.f ? 255.f : color);
 }
 
-template <int D>
+// 256-thread blocks of 4 waves. SEG = 1: each wave marches a 16x4 pixel patch (a block covers 16x16). SEG > 1:
+// SEG waves take the SAME 16x4 patch and each marches a contiguous 1/SEG of every ray's clipped step range; the
+// partial colours are summed in ray order through LDS (a ray whose earlier segments reach 255 is saturated, as
+// the sequential march's stop at colour >= 255 gives after the final clamp). A 512^2 image is only 4096 waves,
+// 4 per SIMD: splitting the rays gives the march SEG times the waves to hide its texel-load latency.
+template <int D, int SEG>
 __global__ __launch_bounds__(256) void raycast_tex_kernel(const void* __restrict__ tex, const int* __restrict__ wide,
                                                          int dim, unsigned char* __restrict__ image, int image_dim, Cam c) {
+    __shared__ float s_part[SEG > 1 ? 256 : 1];
     if (*wide)
-        raycast_tex_march<D, true>(tex, dim, image, image_dim, c);
+        raycast_tex_march<D, true, SEG>(tex, dim, image, image_dim, c, s_part);
     else
-        raycast_tex_march<D, false>(tex, dim, image, image_dim, c);
+        raycast_tex_march<D, false, SEG>(tex, dim, image, image_dim, c, s_part);
 }
 
 Cam make_cam(const float* cam12, float pw, float step, int max_steps) {
@@ -610,21 +649,33 @@ extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* r
     return (int)hipGetLastError();
 }
 
-// batch = steps per prefetch batch (1, 4, 8, 16; 0 = 4, the measured best)
+// batch = steps per prefetch batch (1, 4, 8, 16; 0 = 16, the measured best); segments = waves per ray patch
+// (1, 2, 4; 0 = the measured best)
+template <int D>
+void launch_tex(const void* tex, const int* wide, int dim, unsigned char* image, int image_dim, const Cam& c,
+                int segments, hipStream_t s) {
+    const unsigned gx = (unsigned)(image_dim + 15) / 16;
+    switch (segments) {
+        case 1: raycast_tex_kernel<D, 1><<<dim3(gx, (image_dim + 15) / 16), 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
+        case 2: raycast_tex_kernel<D, 2><<<dim3(gx, (image_dim + 7) / 8), 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
+        default: raycast_tex_kernel<D, 4><<<dim3(gx, (image_dim + 3) / 4), 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
+    }
+}
+
 extern "C" int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* image, int image_dim,
                                     const float* cam12, float pixel_width, float step, int max_steps, int batch,
-                                    hipStream_t s) {
+                                    int segments, hipStream_t s) {
     if (dim <= 1 || dim > 2048 || image_dim <= 0) return PCMX_ERR_ARG;
     if (batch != 0 && batch != 1 && batch != 4 && batch != 8 && batch != 16) return PCMX_ERR_ARG;
+    if (segments != 0 && segments != 1 && segments != 2 && segments != 4) return PCMX_ERR_ARG;
+    if (segments == 0) segments = 4;
     const Cam c = make_cam(cam12, pixel_width, step, max_steps);
-    dim3 grid((image_dim + 15) / 16, (image_dim + 15) / 16);
     const int* wide = reinterpret_cast<const int*>(reinterpret_cast<const char*>(tex) + (size_t)dim * dim * dim * 16);
     switch (batch) {
-        case 1: raycast_tex_kernel<1><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
-        case 16: raycast_tex_kernel<16><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
-        case 8: raycast_tex_kernel<8><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
-        default: raycast_tex_kernel<4><<<grid, 256, 0, s>>>(tex, wide, dim, image, image_dim, c); break;
+        case 1: launch_tex<1>(tex, wide, dim, image, image_dim, c, segments, s); break;
+        case 4: launch_tex<4>(tex, wide, dim, image, image_dim, c, segments, s); break;
+        case 8: launch_tex<8>(tex, wide, dim, image, image_dim, c, segments, s); break;
+        default: launch_tex<16>(tex, wide, dim, image, image_dim, c, segments, s); break;
     }
     return (int)hipGetLastError();
 }
-

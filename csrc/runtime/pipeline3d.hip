@@ -104,7 +104,7 @@ unsigned char* cast(const unsigned char* host_data, const unsigned char* host_re
         if (!rc) rc = pcmx_brick_pack(d.data, d.region, dim, d.ws, d.s);
         if (!rc)
             rc = pcmx_raycast_bricked(d.ws, dim, d.image, image_dim, cam12, cam.pixel_width, cam.step_size,
-                                      cam.max_steps, 0, d.s);
+                                      cam.max_steps, 0, 0, d.s);
     } else if (!rc) {
         rc = pcmx_raycast_global(d.data, d.region, dim, d.image, image_dim, cam12, cam.pixel_width, cam.step_size,
                                  cam.max_steps, 1, d.s);

@@ -399,7 +399,7 @@ at::Tensor brick_pack(const at::Tensor& data, const at::Tensor& region) {
 }
 
 at::Tensor raycast_bricked(const at::Tensor& tex, int64_t image_dim, at::ArrayRef<double> cam12, double pixel_width,
-                           double step, int64_t max_steps, int64_t batch) {
+                           double step, int64_t max_steps, int64_t batch, int64_t segments) {
     check_gpu(tex, "tex", at::kLong);
     TORCH_CHECK(tex.dim() == 1 && tex.numel() >= 18 && tex.is_contiguous(), "raycast_bricked: tex from brick_pack");
     const int64_t nvox = (tex.numel() - 2) / 2;
@@ -410,7 +410,7 @@ at::Tensor raycast_bricked(const at::Tensor& tex, int64_t image_dim, at::ArrayRe
     auto c = cam_vec(cam12);
     check_rc(pcmx_raycast_bricked(tex.data_ptr(), (int)dim,
                                   img.data_ptr<uint8_t>(), (int)image_dim, c.data(), (float)pixel_width, (float)step,
-                                  (int)max_steps, (int)batch, cur_stream(tex)),
+                                  (int)max_steps, (int)batch, (int)segments, cur_stream(tex)),
              "raycast_bricked");
     return img;
 }
@@ -569,7 +569,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("raycast_slab_(Tensor data, Tensor region, int z0, Tensor(a!) state, bool init, bool bottom, int image_dim, float[] cam12, float pixel_width, float step, int max_steps) -> Tensor");
     m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True) -> Tensor");
     m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
-    m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, int batch=4) -> Tensor");
+    m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, int batch=0, int segments=0) -> Tensor");
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");

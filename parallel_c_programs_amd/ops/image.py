@@ -182,13 +182,15 @@ def default_camera(image_dim: int) -> Camera:
 
 
 def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, method: str = "global",
-            cam: Camera | None = None, batch: int = 4) -> torch.Tensor:
+            cam: Camera | None = None, batch: int = 0, segments: int = 0) -> torch.Tensor:
     """Render the volume (ray marching, trilinear sampling of data and region).
 
     method: "global" — bit-compatible with the reference's serial/global-memory caster (f64 colour update);
             "global_f32" — f32 colour update like the CUDA kernel; "texture" — the texture path
             (texel-centre addressing, correct weights, 8-bit fractional weights) on a packed brick volume;
-            `batch` = its march steps per prefetch batch (1, 4, 8, 16: same image, 4 is fastest).
+            `batch` = its march steps per prefetch batch (1, 4, 8, 16: same image; 0 = 16, the fastest);
+            `segments` = waves sharing one ray patch, each marching a contiguous share of the steps (1, 2, 4;
+            0 = the fastest; partial colours are composed in ray order, so images agree up to f32 rounding).
     """
     cam = cam or default_camera(image_dim)
     if not data.is_cuda:
@@ -205,5 +207,5 @@ def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, meth
     if method == "texture":
         tex = o.brick_pack(data, region)
         return o.raycast_bricked(tex, int(image_dim), cam.cam12(), float(cam.pixel_width), float(cam.step_size),
-                                 int(cam.max_steps), int(batch))
+                                 int(cam.max_steps), int(batch), int(segments))
     raise ValueError(f"unknown raycast method {method!r}")

@@ -1,4 +1,5 @@
-"""Ray-cast lab: time the texture ray marcher (brick-packed volume) at each prefetch batch size, 512^2 image.
+"""Ray-cast lab: time the texture ray marcher (brick-packed volume) at each segment split and prefetch batch size,
+512^2 image.
 Usage: python scripts/raycast_lab.py"""
 import sys
 
@@ -16,9 +17,9 @@ tex = native().brick_pack(vol, (reg != 0).to(torch.uint8))
 cam = default_camera(512)
 
 
-def run(max_steps=None, batch=4):
+def run(max_steps=None, batch=0, segments=0):
     return native().raycast_bricked(tex, 512, cam.cam12(), float(cam.pixel_width), float(cam.step_size),
-                                    int(max_steps or cam.max_steps), batch)
+                                    int(max_steps or cam.max_steps), batch, segments)
 
 
 def timeit(fn, reps=10):
@@ -40,14 +41,11 @@ for ms in (1000, 2000, 3000, 4000, 5000):
 
 
 ref = None
-for b in (1, 4, 8, 16):
-    for _ in range(2):
-        img = run(batch=b)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        run(batch=b)
-    e1.record()
-    torch.cuda.synchronize()
-    ref = img if ref is None else ref
-    print(f"batch {b:2d}: {e0.elapsed_time(e1) / 10:.3f} ms  identical={torch.equal(img, ref)}")
+for rnd in range(2):
+    for b, seg in ((4, 1), (16, 1), (16, 2), (8, 4), (16, 4)):
+        img = run(batch=b, segments=seg)
+        ms = timeit(lambda: run(batch=b, segments=seg))
+        ref = img if ref is None else ref
+        diff = (img.float() - ref.float()).abs()
+        print(f"batch {b:2d} segments {seg}: {ms:.3f} ms  max|diff| vs batch 4 x 1 segment {diff.max().item():.0f}  "
+              f"pixels differing {int((diff > 0).sum())}", flush=True)

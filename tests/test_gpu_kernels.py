@@ -173,6 +173,20 @@ def test_raycast_texture_batches_identical(gpu):
         assert torch.equal(im, imgs[0])
 
 
+def test_raycast_texture_segments_agree(gpu):
+    # splitting every ray's steps over 1 / 2 / 4 waves composes the same colour up to f32 summation order
+    vol = ops.create_volume(512, device=gpu, seed=0)
+    reg, _ = ops.region3d(vol, threshold=1)
+    reg = (reg != 0).to(torch.uint8)
+    imgs = [ops.raycast(vol, reg, 128, method="texture", segments=s).int() for s in (1, 2, 4)]
+    for im in imgs[1:]:
+        d = (im - imgs[0]).abs()
+        assert d.max().item() <= 1 and int((d > 0).sum()) <= 16
+    wide = ops.raycast(vol | 128, reg, 64, method="texture", segments=4).int()  # 16-B texel path, same split
+    wide1 = ops.raycast(vol | 128, reg, 64, method="texture", segments=1).int()
+    assert (wide - wide1).abs().max().item() <= 1
+
+
 @pytest.mark.parametrize("shape", [(256, 512), (1000, 1024), (515, 4096)])
 def test_stencil_bit_exact(gpu, shape):
     rows, cols = shape
