@@ -106,7 +106,21 @@ void r_destroy(pcmx_comm_t* c) {
     free(c);
 }
 
-const pcmx_comm_ops_t kRcclOps = {r_group_start, r_group_end, r_send, r_recv, r_allreduce, r_bcast, r_sync, r_destroy};
+int r_allgather(pcmx_comm_t* c, const void* s, void* r, size_t n) {
+    return rc_of(ncclAllGather(s, r, n, ncclUint8, impl(c)->comm, impl(c)->stream));
+}
+int r_gather(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) {
+    return rc_of(ncclGather(s, r, n, ncclUint8, root, impl(c)->comm, impl(c)->stream));
+}
+int r_scatter(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) {
+    return rc_of(ncclScatter(s, r, n, ncclUint8, root, impl(c)->comm, impl(c)->stream));
+}
+int r_alltoall(pcmx_comm_t* c, const void* s, void* r, size_t n) {
+    return rc_of(ncclAllToAll(s, r, n, ncclUint8, impl(c)->comm, impl(c)->stream));
+}
+
+const pcmx_comm_ops_t kRcclOps = {r_group_start, r_group_end, r_send,      r_recv,     r_allreduce, r_bcast,
+                                  r_sync,        r_destroy,   r_allgather, r_gather,   r_scatter,   r_alltoall};
 
 // ---------------------------------------------------------------- staged TCP transport (device buffers)
 // Device buffers moved through host memory over the TCP transport: lets P ranks share ONE GPU (RCCL refuses
@@ -203,7 +217,18 @@ void s_destroy(pcmx_comm_t* c) {
     if (c->host && c->host != c) pcmx_comm_destroy(c->host);
     free(c);
 }
-const pcmx_comm_ops_t kStagedOps = {s_group_start, s_group_end, s_send, s_recv, s_allreduce, s_bcast, s_sync, s_destroy};
+int s_copy(pcmx_comm_t* c, void* d, const void* src, size_t n) {
+    int rc = (int)hipMemcpyAsync(d, src, n, hipMemcpyDeviceToDevice, simpl(c)->stream);
+    return rc ? rc : (int)hipStreamSynchronize(simpl(c)->stream);
+}
+int s_allgather(pcmx_comm_t* c, const void* s, void* r, size_t n) { return pcmx_p2p_allgather(c, s, r, n, s_copy); }
+int s_gather(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) { return pcmx_p2p_gather(c, s, r, n, root, s_copy); }
+int s_scatter(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) {
+    return pcmx_p2p_scatter(c, s, r, n, root, s_copy);
+}
+int s_alltoall(pcmx_comm_t* c, const void* s, void* r, size_t n) { return pcmx_p2p_alltoall(c, s, r, n, s_copy); }
+const pcmx_comm_ops_t kStagedOps = {s_group_start, s_group_end, s_send,      s_recv,   s_allreduce, s_bcast,
+                                    s_sync,        s_destroy,   s_allgather, s_gather, s_scatter,   s_alltoall};
 
 // ---------------------------------------------------------------- device backend
 struct DevCtx {
@@ -336,4 +361,63 @@ extern "C" int pcmx_comm_init_env_rccl(pcmx_comm_t** out) {
     c->ops = &kRcclOps, c->impl = r, c->host = host, c->stream = r->stream;
     *out = c;
     return 0;
+}
+
+// ---------------------------------------------------------------- distributed reduce / scan (north-star NS3)
+// Global reduce and prefix scan of a vector split over the ranks (rank r holds elements [sum_{q<r} n_q, ...)),
+// device buffers, everything stream-ordered on the communicator's stream (no host round trip): a local HBM-speed
+// reduce, then ONE all-reduce of a scalar (never the 4 GB vector: ancestor ref 2-mpi-region-growing/region.c:
+// 435-440); the scan all-gathers the per-rank totals (world floats), a one-thread kernel forms the exclusive
+// prefix of the ranks below, and the local single-pass scan starts from it (its init operand is device memory).
+namespace {
+__global__ void rank_prefix_kernel(const float* __restrict__ totals, int rank, float* __restrict__ init) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        float s = 0.f;
+        for (int q = 0; q < rank; ++q) s += totals[q];
+        *init = s;
+    }
+}
+long long align256(long long b) { return (b + 255) & ~255LL; }
+}  // namespace
+
+extern "C" long long pcmx_dist_workspace_bytes(long long n_local, int world) {
+    const long long red = align256(pcmx_reduce_workspace_bytes(n_local > 0 ? n_local : 1));
+    const long long scan = align256(pcmx_scan_workspace_bytes(n_local > 0 ? n_local : 1));
+    return red + scan + align256(4LL * (world + 2));
+}
+
+extern "C" int pcmx_reduce_distributed(pcmx_comm_t* c, const float* x, long long n_local, int op, float* out,
+                                       void* ws) {
+    if (!c || !c->stream || !ws || !out || n_local < 0) return PCMX_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(c->stream);
+    int rc = 0;
+    if (n_local > 0) {
+        rc = pcmx_reduce_f32(x, n_local, op, out, ws, s);
+    } else {  // an empty rank contributes the identity of op
+        const float id = op == PCMX_OP_MIN ? __builtin_huge_valf() : op == PCMX_OP_MAX ? -__builtin_huge_valf() : 0.f;
+        rc = (int)hipMemcpyAsync(out, &id, 4, hipMemcpyHostToDevice, s);
+        if (!rc) rc = (int)hipStreamSynchronize(s);  // the host source must outlive the copy
+    }
+    if (rc) return rc;
+    return c->ops->allreduce(c, out, 1, PCMX_F32, op == PCMX_OP_MIN ? PCMX_MIN : op == PCMX_OP_MAX ? PCMX_MAX : PCMX_SUM);
+}
+
+extern "C" int pcmx_scan_distributed(pcmx_comm_t* c, const float* x, float* out, long long n_local, int exclusive,
+                                     void* ws, unsigned* err_flag) {
+    if (!c || !c->stream || !ws || n_local < 0) return PCMX_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(c->stream);
+    char* base = static_cast<char*>(ws);
+    void* red_ws = base;
+    void* scan_ws = base + align256(pcmx_reduce_workspace_bytes(n_local > 0 ? n_local : 1));
+    float* totals = reinterpret_cast<float*>(static_cast<char*>(scan_ws) +
+                                             align256(pcmx_scan_workspace_bytes(n_local > 0 ? n_local : 1)));
+    float* mine = totals + c->world;  // this rank's total, then its exclusive offset
+    float* init = mine + 1;
+    int rc = n_local > 0 ? pcmx_reduce_f32(x, n_local, PCMX_OP_SUM, mine, red_ws, s)
+                         : (int)hipMemsetAsync(mine, 0, 4, s);
+    if (!rc) rc = c->ops->allgather(c, mine, totals, 4);
+    if (rc) return rc;
+    rank_prefix_kernel<<<1, 64, 0, s>>>(totals, c->rank, init);
+    if ((rc = (int)hipGetLastError())) return rc;
+    return n_local > 0 ? pcmx_scan_f32(x, out, n_local, exclusive, init, scan_ws, err_flag, s) : 0;
 }

@@ -325,8 +325,80 @@ static void tcp_destroy(pcmx_comm_t* c) {
     free(c);
 }
 
-static const pcmx_comm_ops_t kTcpOps = {tcp_group_start, tcp_group_end, tcp_send, tcp_recv,
-                                        tcp_allreduce,   tcp_bcast,     tcp_sync, tcp_destroy};
+/* ------------------------------------------------------------------ collectives over point-to-point */
+/* One grouped round: every peer's block moves at once (TCP: all sockets progress together in tcp_progress; staged:
+ * one host round trip for the whole group). `copy` handles the rank's own block. */
+static char* blk(const void* base, size_t i, size_t bytes) { return (char*)base + i * bytes; }
+
+int pcmx_p2p_allgather(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, pcmx_copy_fn copy) {
+    int rc = 0;
+    if (send != blk(recv, c->rank, bytes)) rc = copy(c, blk(recv, c->rank, bytes), send, bytes);
+    if (rc || c->world == 1) return rc;
+    c->ops->group_start(c);
+    for (int p = 0; p < c->world && !rc; ++p) {
+        if (p == c->rank) continue;
+        rc = c->ops->send(c, blk(recv, c->rank, bytes), bytes, p);
+        if (!rc) rc = c->ops->recv(c, blk(recv, p, bytes), bytes, p);
+    }
+    const int rc2 = c->ops->group_end(c);
+    return rc ? rc : rc2;
+}
+
+int pcmx_p2p_gather(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, int root, pcmx_copy_fn copy) {
+    if (root < 0 || root >= c->world) return -1;
+    if (c->rank != root) return c->ops->send(c, send, bytes, root);
+    int rc = send != blk(recv, root, bytes) ? copy(c, blk(recv, root, bytes), send, bytes) : 0;
+    if (rc || c->world == 1) return rc;
+    c->ops->group_start(c);
+    for (int p = 0; p < c->world && !rc; ++p)
+        if (p != root) rc = c->ops->recv(c, blk(recv, p, bytes), bytes, p);
+    const int rc2 = c->ops->group_end(c);
+    return rc ? rc : rc2;
+}
+
+int pcmx_p2p_scatter(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, int root, pcmx_copy_fn copy) {
+    if (root < 0 || root >= c->world) return -1;
+    if (c->rank != root) return c->ops->recv(c, recv, bytes, root);
+    int rc = recv != blk(send, root, bytes) ? copy(c, recv, blk(send, root, bytes), bytes) : 0;
+    if (rc || c->world == 1) return rc;
+    c->ops->group_start(c);
+    for (int p = 0; p < c->world && !rc; ++p)
+        if (p != root) rc = c->ops->send(c, blk(send, p, bytes), bytes, p);
+    const int rc2 = c->ops->group_end(c);
+    return rc ? rc : rc2;
+}
+
+int pcmx_p2p_alltoall(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, pcmx_copy_fn copy) {
+    if (send == recv) return -1; /* out of place only */
+    int rc = copy(c, blk(recv, c->rank, bytes), blk(send, c->rank, bytes), bytes);
+    if (rc || c->world == 1) return rc;
+    c->ops->group_start(c);
+    for (int p = 0; p < c->world && !rc; ++p) {
+        if (p == c->rank) continue;
+        rc = c->ops->send(c, blk(send, p, bytes), bytes, p);
+        if (!rc) rc = c->ops->recv(c, blk(recv, p, bytes), bytes, p);
+    }
+    const int rc2 = c->ops->group_end(c);
+    return rc ? rc : rc2;
+}
+
+static int host_copy(pcmx_comm_t* c, void* dst, const void* src, size_t bytes) {
+    (void)c;
+    memmove(dst, src, bytes);
+    return 0;
+}
+static int tcp_allgather(pcmx_comm_t* c, const void* s, void* r, size_t n) { return pcmx_p2p_allgather(c, s, r, n, host_copy); }
+static int tcp_gather(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) {
+    return pcmx_p2p_gather(c, s, r, n, root, host_copy);
+}
+static int tcp_scatter(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) {
+    return pcmx_p2p_scatter(c, s, r, n, root, host_copy);
+}
+static int tcp_alltoall(pcmx_comm_t* c, const void* s, void* r, size_t n) { return pcmx_p2p_alltoall(c, s, r, n, host_copy); }
+
+static const pcmx_comm_ops_t kTcpOps = {tcp_group_start, tcp_group_end, tcp_send,      tcp_recv,
+                                        tcp_allreduce,   tcp_bcast,     tcp_sync,      tcp_destroy,
+                                        tcp_allgather,   tcp_gather,    tcp_scatter,   tcp_alltoall};
 
 /* ------------------------------------------------------------------ bootstrap */
 
@@ -440,6 +512,12 @@ int pcmx_comm_recv(pcmx_comm_t* c, void* b, size_t n, int p) { return c->ops->re
 int pcmx_comm_allreduce(pcmx_comm_t* c, void* b, size_t n, int dt, int op) { return c->ops->allreduce(c, b, n, dt, op); }
 int pcmx_comm_bcast(pcmx_comm_t* c, void* b, size_t n, int root) { return c->ops->bcast(c, b, n, root); }
 int pcmx_comm_sync(pcmx_comm_t* c) { return c->ops->sync(c); }
+int pcmx_comm_allgather(pcmx_comm_t* c, const void* s, void* r, size_t n) { return c->ops->allgather(c, s, r, n); }
+int pcmx_comm_gather(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) { return c->ops->gather(c, s, r, n, root); }
+int pcmx_comm_scatter(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) {
+    return c->ops->scatter(c, s, r, n, root);
+}
+int pcmx_comm_alltoall(pcmx_comm_t* c, const void* s, void* r, size_t n) { return c->ops->alltoall(c, s, r, n); }
 int pcmx_comm_barrier(pcmx_comm_t* c) {
     int rc = c->ops->sync(c);
     if (rc) return rc;

@@ -36,6 +36,13 @@ typedef struct pcmx_comm_ops {
     int (*bcast)(pcmx_comm_t*, void* buf, size_t bytes, int root);
     int (*sync)(pcmx_comm_t*);
     void (*destroy)(pcmx_comm_t*);
+    /* collectives over equal byte blocks (`bytes` per rank; recv/send of the root-side buffers hold world
+     * blocks in rank order). RCCL: ncclAllGather / ncclGather / ncclScatter / ncclAllToAll; TCP and staged:
+     * one grouped round of point-to-point messages (every peer on its own socket / link at once). */
+    int (*allgather)(pcmx_comm_t*, const void* send, void* recv, size_t bytes);
+    int (*gather)(pcmx_comm_t*, const void* send, void* recv, size_t bytes, int root);
+    int (*scatter)(pcmx_comm_t*, const void* send, void* recv, size_t bytes, int root);
+    int (*alltoall)(pcmx_comm_t*, const void* send, void* recv, size_t bytes);
 } pcmx_comm_ops_t;
 
 struct pcmx_comm {
@@ -65,6 +72,22 @@ int pcmx_comm_allreduce(pcmx_comm_t* c, void* buf, size_t count, int dtype, int 
 int pcmx_comm_bcast(pcmx_comm_t* c, void* buf, size_t bytes, int root);
 int pcmx_comm_sync(pcmx_comm_t* c);
 int pcmx_comm_barrier(pcmx_comm_t* c); /* host side-channel barrier (after sync) */
+/* MPI_Allgather / Gather / Scatter / Alltoall of `bytes` per rank (recv of allgather/gather/alltoall and send
+ * of scatter/alltoall hold world blocks in rank order; the root-only buffers may be NULL elsewhere). In place:
+ * allgather with send == recv + rank * bytes, scatter with recv == send + root * bytes on the root. */
+int pcmx_comm_allgather(pcmx_comm_t* c, const void* send, void* recv, size_t bytes);
+int pcmx_comm_gather(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, int root);
+int pcmx_comm_scatter(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, int root);
+int pcmx_comm_alltoall(pcmx_comm_t* c, const void* send, void* recv, size_t bytes);
+
+/* point-to-point implementations of the collectives above for transports without native ones; `copy` moves a
+ * block between two of the transport's own buffers (memmove for host memory, a device copy for the staged
+ * transport) */
+typedef int (*pcmx_copy_fn)(pcmx_comm_t* c, void* dst, const void* src, size_t bytes);
+int pcmx_p2p_allgather(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, pcmx_copy_fn copy);
+int pcmx_p2p_gather(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, int root, pcmx_copy_fn copy);
+int pcmx_p2p_scatter(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, int root, pcmx_copy_fn copy);
+int pcmx_p2p_alltoall(pcmx_comm_t* c, const void* send, void* recv, size_t bytes, pcmx_copy_fn copy);
 
 /* ---- Cartesian topology (MPI_Dims_create / Cart_create(reorder=0) / Cart_coords / Cart_shift) */
 typedef struct {
@@ -112,6 +135,15 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
 /* Token chain of ref 1-introduction/mpi.c (prints "Rank %d received %d \n" / "Rank %d sent %d \n");
  * token_buf: 4 bytes in the transport's memory space. Returns the final token value on this rank. */
 int pcmx_token_ring(pcmx_comm_t* c, void* token_buf, const pcmx_region_backend_t* be, int verbose);
+
+/* ---- distributed reduce / scan over device vectors split across the ranks (libpcmx_hip; RCCL or staged
+ * transport, stream-ordered on c->stream). ws: pcmx_dist_workspace_bytes(n_local, world) bytes of device memory.
+ * reduce: *out (device) = op over every rank's x (op = PCMX_OP_SUM / MIN / MAX of pcmx_hip.h).
+ * scan: out = inclusive/exclusive prefix of the GLOBAL vector (rank order); err_flag as in pcmx_scan_f32. */
+long long pcmx_dist_workspace_bytes(long long n_local, int world);
+int pcmx_reduce_distributed(pcmx_comm_t* c, const float* x, long long n_local, int op, float* out, void* ws);
+int pcmx_scan_distributed(pcmx_comm_t* c, const float* x, float* out, long long n_local, int exclusive, void* ws,
+                          unsigned* err_flag);
 
 /* host flood fill on a padded tile (CPU backend of `grow`) */
 void pcmx_region2d_padded_host(unsigned char* region_p, const unsigned char* img_p, int h, int w, int threshold);

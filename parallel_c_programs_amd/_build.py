@@ -179,6 +179,7 @@ BIN_TOOLS = {
     "device_info": ("bin/device_info_main.cpp", "hip"),
     "region": ("bin/region_main.cpp", "hip"),
     "mpi_ring": ("bin/mpi_ring_main.cpp", "hip"),
+    "collectives": ("bin/collectives_main.cpp", "hip"),
     "vmul": ("bin/vmul_main.cpp", "hip"),
     "pcmx_launch": ("bin/launch_main.c", "c"),
     # C programs written only against the reference 3-D entry points (pcmx_pipeline3d.h): host C, linked with

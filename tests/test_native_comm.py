@@ -121,3 +121,34 @@ def test_native_mpi_ring_staged(gpu):
     r = _launch(3, BIN / "mpi_ring", "--staged")
     assert r.returncode == 0, r.stderr
     assert "Rank 0 received 3 " in r.stdout.splitlines()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
+def test_native_collectives_tcp(n):
+    """MPI_Allgather / Gather / Scatter / Alltoall equivalents (pcmx_comm_allgather ...) over the TCP transport:
+    every rank checks its blocks byte for byte (odd block size, in-place all-gather, non-zero gather root)."""
+    r = _launch(n, BIN / "collectives", "--cpu", "--bytes", "4099")
+    assert r.returncode == 0, r.stderr
+    assert f"collectives ok world={n}" in r.stdout
+    assert sum("alltoall ok" in ln for ln in r.stdout.splitlines()) == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_native_collectives_staged(gpu, n):
+    """Device buffers, P ranks on the one GPU: the collectives plus the distributed reduce and prefix scan
+    (local gfx950 reduce/scan kernels, per-rank totals all-gathered, exact on small integers, ragged ranks)."""
+    r = _launch(n, BIN / "collectives", "--staged")
+    assert r.returncode == 0, r.stderr
+    assert f"collectives ok world={n}" in r.stdout
+    assert sum("reduce scan ok" in ln for ln in r.stdout.splitlines()) == n
+
+
+@pytest.mark.gpu
+def test_native_collectives_rccl(gpu):
+    import torch
+
+    n = min(torch.cuda.device_count(), 8)
+    r = _launch(n, BIN / "collectives")
+    assert r.returncode == 0, r.stderr
+    assert f"collectives ok world={n}" in r.stdout
