@@ -299,6 +299,10 @@ __device__ __forceinline__ unsigned pair(unsigned a, unsigned an, unsigned b, un
 // 512^3). The read-back (texel j by lane j, ds_read_b128 groups of 16 lanes made of aligned 4-lane blocks) only
 // permutes slots inside aligned groups of 4, so its groups still cover 16 distinct slots mod 16.
 __device__ __forceinline__ int tex_slot(int j) { return j ^ ((j >> 3) & 3); }
+// the same for 8 texels per lane (lane t writes 8t+i): XOR with t mod 8 spreads an 8-lane write group over 8
+// distinct 16-B slots (t mod 4 left 2-way conflicts: 2.1e7 per 512^3 pack, r2_pmc/raycast.md); the read-back
+// still only permutes slots inside aligned groups of 8
+__device__ __forceinline__ int tex_slot8(int j) { return j ^ ((j >> 3) & 7); }
 
 // A block covers 1024 consecutive texels of one z-plane in row-major (y, x) order (rows of several y when
 // dim < 1024; dim % 4 == 0 keeps a thread's 4 texels in one row), so every thread is busy (one block per row
@@ -418,7 +422,7 @@ __global__ __launch_bounds__(128) void brick_pack8_kernel(const unsigned char* _
             const unsigned r1 = pair8(r[k + 1][0], rn[k + 1][0], r[k + 1][1], rn[k + 1][1], i);
             const unsigned d0 = pair8(d[k][0], dn[k][0], d[k][1], dn[k][1], i);
             const unsigned d1 = pair8(d[k + 1][0], dn[k + 1][0], d[k + 1][1], dn[k + 1][1], i);
-            stage[tex_slot(threadIdx.x * 8 + i)] =
+            stage[tex_slot8(threadIdx.x * 8 + i)] =
                 wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
         }
         __syncthreads();
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(128) void brick_pack8_kernel(const unsigned char* _
         for (int i = 0; i < 8; ++i) {
             const int j = i * 128 + threadIdx.x;
             if (lin0 + j >= P) continue;
-            const uint4 t = stage[tex_slot(j)];
+            const uint4 t = stage[tex_slot8(j)];
             const size_t o = (size_t)z * P + lin0 + j;
             if (wide)
                 reinterpret_cast<uint4*>(tex)[o] = t;
@@ -454,6 +458,111 @@ __device__ __forceinline__ float q8(float f) { return rintf(f * 256.f) * (1.f / 
 // per batch (2*D texel loads in flight) and consumed in order with the reference's termination tests (stop at
 // colour >= 255, stop when the ray leaves the convex box). Positions differ from the reference's repeated
 // f32 adds by rounding only (~1e-3 voxel), below the 8-bit weight quantum of the emulated texture filter.
+// Ray of pixel (px, py): step vector and the analytic clip of its march against the sampled box [0, dim-1)^3,
+// in units of steps with one step of margin each side. k0 > k1 = the ray misses the volume.
+struct TexRay {
+    float sv[3];
+    int k0, k1;
+};
+__device__ __forceinline__ TexRay tex_ray(int px, int py, int image_dim, int dim, const Cam& c) {
+    const int half = image_dim / 2;
+    const int x = px - half, y = py - half;
+    float ray[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float sc = c.cam[k] + c.fwd[k];
+        ray[k] = (sc + c.right[k] * (x * c.pw)) + c.up[k] * (y * c.pw) - c.cam[k];
+    }
+    const float l = sqrtf(ray[0] * ray[0] + ray[1] * ray[1] + ray[2] * ray[2]);
+    TexRay r;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.sv[k] = ray[k] / l * c.step;
+    const float hi = (float)(dim - 1);
+    // slab clip in units of steps: inside <=> 0 <= cam + k*sv < hi on every axis
+    float k_lo = 1.f, k_hi = (float)c.max_steps;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (r.sv[a] == 0.f) {
+            if (!(c.cam[a] >= 0.f && c.cam[a] < hi)) k_hi = -1.f;
+            continue;
+        }
+        const float t0 = (0.f - c.cam[a]) / r.sv[a], t1 = (hi - c.cam[a]) / r.sv[a];
+        k_lo = fmaxf(k_lo, fminf(t0, t1));
+        k_hi = fminf(k_hi, fmaxf(t0, t1));
+    }
+    if (k_lo <= k_hi) {
+        r.k0 = max(1, (int)floorf(k_lo) - 1);
+        r.k1 = min(c.max_steps, (int)ceilf(k_hi) + 1);
+    } else {
+        r.k0 = 1, r.k1 = 0;
+    }
+    return r;
+}
+
+// Colour accumulated over steps [k0, k1] of the ray (reference termination tests: stop at colour >= 255, stop
+// when the ray leaves the convex box after entering it).
+template <int D, bool WIDE>
+__device__ __forceinline__ float tex_march(const void* __restrict__ texv, int dim, const Cam& c, const float (&sv)[3],
+                                           int k0, int k1) {
+    const size_t P = (size_t)dim * dim;
+    const float hi = (float)(dim - 1);
+    float color = 0.f;
+    // texel-centre addressing (sample at p - 0.5), clamp-to-edge, 8-bit fractional weights
+    auto tap = [&](int step, float& ax, float& ay, float& az, bool& inb, bool opaque) -> size_t {
+        float kk = (float)step;
+        if (opaque) asm volatile("" : "+v"(kk));  // recompute at use: keeps the compiler from holding the
+                                                 // issue-time values live across the batch
+        const float p0 = fmaf(kk, sv[0], c.cam[0]), p1 = fmaf(kk, sv[1], c.cam[1]), p2 = fmaf(kk, sv[2], c.cam[2]);
+        inb = in_box(p0, p1, p2, hi);
+        const float fx = p0 - 0.5f, fy = p1 - 0.5f, fz = p2 - 0.5f;
+        int x0 = (int)floorf(fx), y0 = (int)floorf(fy), z0 = (int)floorf(fz);
+        ax = q8(fx - x0), ay = q8(fy - y0), az = q8(fz - z0);
+        if (x0 < 0) x0 = 0, ax = 0.f;
+        if (y0 < 0) y0 = 0, ay = 0.f;
+        if (z0 < 0) z0 = 0, az = 0.f;
+        x0 = min(x0, dim - 1), y0 = min(y0, dim - 1), z0 = min(z0, dim - 1);
+        return (size_t)z0 * P + ((unsigned)y0 * (unsigned)dim + (unsigned)x0);  // row part < 2^32 (dim <= 2048)
+    };
+    using Texel = typename std::conditional<WIDE, uint4, uint2>::type;
+    bool entered = false, active = true;
+    for (int i = k0; active && i <= k1 && color < 255.f; i += D) {
+        // only the raw texels stay live across the batch (2 or 4 VGPRs per step in flight); the weights are
+        // recomputed at use, so deep batches keep the occupancy
+        Texel q[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            float ax, ay, az;
+            bool inb;
+            q[k] = reinterpret_cast<const Texel*>(texv)[tap(i + k, ax, ay, az, inb, false)];  // always in bounds
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const bool live = active && i + k <= k1 && color < 255.f;
+            active = live;
+            if (!live) continue;
+            float ax, ay, az;
+            bool inb;
+            (void)tap(i + k, ax, ay, az, inb, true);
+            if (!inb) {  // texture fetches outside never add colour; a convex box is never re-entered
+                if (entered) active = false;
+                continue;
+            }
+            entered = true;
+            uint4 t;  // data z, data z+1, region z, region z+1 (4 corners each)
+            if constexpr (WIDE)
+                t = q[k];
+            else
+                t = make_uint4(q[k].x & 0x7f7f7f7fu, q[k].y & 0x7f7f7f7fu, (q[k].x >> 7) & 0x01010101u,
+                               (q[k].y >> 7) & 0x01010101u);
+            const float d = (1.f - az) * bilerp4(t.x, ax, ay) + az * bilerp4(t.y, ax, ay);
+            const float rr = (1.f - az) * bilerp4(t.z, ax, ay) + az * bilerp4(t.w, ax, ay);
+            const int r = (int)rr;  // 255 * normalised region tap, region voxels hold 1
+            color += d * (0.01f + r);
+        }
+    }
+    return color;
+}
+
 template <int D, bool WIDE, int SEG>
 __device__ __forceinline__ void raycast_tex_march(const void* __restrict__ texv, int dim,
                                                   unsigned char* __restrict__ image, int image_dim, const Cam& c,
@@ -465,92 +574,16 @@ __device__ __forceinline__ void raycast_tex_march(const void* __restrict__ texv,
     const int py = blockIdx.y * kRows + g * 4 + (lane >> 4);
     const bool valid = px < image_dim && py < image_dim;
     if (SEG == 1 && !valid) return;
-    const int half = image_dim / 2;
-    const int x = px - half, y = py - half;
-    float ray[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float sc = c.cam[k] + c.fwd[k];
-        ray[k] = (sc + c.right[k] * (x * c.pw)) + c.up[k] * (y * c.pw) - c.cam[k];
-    }
-    const float l = sqrtf(ray[0] * ray[0] + ray[1] * ray[1] + ray[2] * ray[2]);
-    const float sv[3] = {ray[0] / l * c.step, ray[1] / l * c.step, ray[2] / l * c.step};
-    const float hi = (float)(dim - 1);
-    // slab clip in units of steps: inside <=> 0 <= cam + k*sv < hi on every axis
-    float k_lo = 1.f, k_hi = (float)c.max_steps;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        if (sv[a] == 0.f) {
-            if (!(c.cam[a] >= 0.f && c.cam[a] < hi)) k_hi = -1.f;
-            continue;
-        }
-        const float t0 = (0.f - c.cam[a]) / sv[a], t1 = (hi - c.cam[a]) / sv[a];
-        k_lo = fmaxf(k_lo, fminf(t0, t1));
-        k_hi = fminf(k_hi, fmaxf(t0, t1));
-    }
-    const size_t P = (size_t)dim * dim;
+    const TexRay r = tex_ray(px, py, image_dim, dim, c);
     float color = 0.f;
-    if (valid && k_lo <= k_hi) {
-        int k0 = max(1, (int)floorf(k_lo) - 1);
-        int k1 = min(c.max_steps, (int)ceilf(k_hi) + 1);
+    if (valid && r.k0 <= r.k1) {
+        int k0 = r.k0, k1 = r.k1;
         if (SEG > 1) {  // this wave's share of [k0, k1]; the in-box steps of a convex box are contiguous
             const int len = (k1 - k0 + SEG) / SEG;
             k0 += seg * len;
             k1 = min(k1, k0 + len - 1);
         }
-        // texel-centre addressing (sample at p - 0.5), clamp-to-edge, 8-bit fractional weights
-        auto tap = [&](int step, float& ax, float& ay, float& az, bool& inb, bool opaque) -> size_t {
-            float kk = (float)step;
-            if (opaque) asm volatile("" : "+v"(kk));  // recompute at use: keeps the compiler from holding the
-                                                     // issue-time values live across the batch
-            const float p0 = fmaf(kk, sv[0], c.cam[0]), p1 = fmaf(kk, sv[1], c.cam[1]), p2 = fmaf(kk, sv[2], c.cam[2]);
-            inb = in_box(p0, p1, p2, hi);
-            const float fx = p0 - 0.5f, fy = p1 - 0.5f, fz = p2 - 0.5f;
-            int x0 = (int)floorf(fx), y0 = (int)floorf(fy), z0 = (int)floorf(fz);
-            ax = q8(fx - x0), ay = q8(fy - y0), az = q8(fz - z0);
-            if (x0 < 0) x0 = 0, ax = 0.f;
-            if (y0 < 0) y0 = 0, ay = 0.f;
-            if (z0 < 0) z0 = 0, az = 0.f;
-            x0 = min(x0, dim - 1), y0 = min(y0, dim - 1), z0 = min(z0, dim - 1);
-            return (size_t)z0 * P + ((unsigned)y0 * (unsigned)dim + (unsigned)x0);  // row part < 2^32 (dim <= 2048)
-        };
-        using Texel = typename std::conditional<WIDE, uint4, uint2>::type;
-        bool entered = false, active = true;
-        for (int i = k0; active && i <= k1 && color < 255.f; i += D) {
-            // only the raw texels stay live across the batch (2 or 4 VGPRs per step in flight); the weights are
-            // recomputed at use, so deep batches keep the occupancy
-            Texel q[D];
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                float ax, ay, az;
-                bool inb;
-                q[k] = reinterpret_cast<const Texel*>(texv)[tap(i + k, ax, ay, az, inb, false)];  // always in bounds
-            }
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                const bool live = active && i + k <= k1 && color < 255.f;
-                active = live;
-                if (!live) continue;
-                float ax, ay, az;
-                bool inb;
-                (void)tap(i + k, ax, ay, az, inb, true);
-                if (!inb) {  // texture fetches outside never add colour; a convex box is never re-entered
-                    if (entered) active = false;
-                    continue;
-                }
-                entered = true;
-                uint4 t;  // data z, data z+1, region z, region z+1 (4 corners each)
-                if constexpr (WIDE)
-                    t = q[k];
-                else
-                    t = make_uint4(q[k].x & 0x7f7f7f7fu, q[k].y & 0x7f7f7f7fu, (q[k].x >> 7) & 0x01010101u,
-                                   (q[k].y >> 7) & 0x01010101u);
-                const float d = (1.f - az) * bilerp4(t.x, ax, ay) + az * bilerp4(t.y, ax, ay);
-                const float rr = (1.f - az) * bilerp4(t.z, ax, ay) + az * bilerp4(t.w, ax, ay);
-                const int r = (int)rr;  // 255 * normalised region tap, region voxels hold 1
-                color += d * (0.01f + r);
-            }
-        }
+        color = tex_march<D, WIDE>(texv, dim, c, r.sv, k0, k1);
     }
     if (SEG > 1) {  // segment partial colours compose in ray order; a saturated prefix ends the ray
         s_part[threadIdx.x] = color;
@@ -679,3 +712,4 @@ extern "C" int pcmx_raycast_bricked(const void* tex, int dim, unsigned char* ima
     }
     return (int)hipGetLastError();
 }
+

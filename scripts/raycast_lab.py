@@ -40,6 +40,8 @@ for ms in (1000, 2000, 3000, 4000, 5000):
     print(f"max_steps {ms}: {timeit(lambda: run(ms)):.3f} ms")
 
 
+
+
 ref = None
 for rnd in range(2):
     for b, seg in ((4, 1), (16, 1), (16, 2), (8, 4), (16, 4)):
