@@ -160,6 +160,14 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
     const int h = tile[1] - tile[0], w = tile[3] - tile[2];
     const size_t tbytes = (size_t)(h + 2) * (w + 2);
     const int nedge = 2 * w + 2 * h;
+    /* every rank derives the same answer: equal tiles (1/2/4/8 ranks on a 512^2 image) use the scatter / gather
+     * collectives (one ncclScatter / ncclGather), uneven ones one grouped message per rank */
+    int equal = 1;
+    for (int r = 0; r < c->world; ++r) {
+        int t[4];
+        pcmx_cart_tile(&topo, r, H, W, t);
+        equal &= t[1] - t[0] == h && t[3] - t[2] == w;
+    }
     unsigned char *img_p = NULL, *reg_p = NULL, *full_p = NULL, *stage = NULL, *sendb = NULL, *recvb = NULL;
     unsigned char* full_reg = NULL;
     int* flag = NULL;
@@ -174,7 +182,7 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
         goto done;
     }
 
-    /* ---- scatter padded image tiles (one message per rank) */
+    /* ---- scatter padded image tiles (one scatter collective, or one message per rank for uneven tiles) */
     if (root) {
         const size_t pw = (size_t)W + 2;
         unsigned char* padded = (unsigned char*)calloc((size_t)(H + 2) * pw, 1);
@@ -196,23 +204,34 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
         free(padded);
         if (rc) goto done;
         size_t off = 0;
-        TRY(pcmx_comm_group_start(c));
-        for (int r = 0; r < c->world; ++r) {
-            int t[4];
-            pcmx_cart_tile(&topo, r, H, W, t);
-            const size_t th = (size_t)(t[1] - t[0] + 2), tw = (size_t)(t[3] - t[2] + 2);
-            unsigned char* dst = r == 0 ? img_p : stage + off;
-            TRY(be->copy2d(dst, tw, full_p + (size_t)t[0] * pw + t[2], pw, tw, th, ctx));
-            if (r) {
-                TRY(be->sync(ctx));
-                TRY(pcmx_comm_send(c, dst, th * tw, r));
+        if (equal) { /* every padded tile staged in rank order, then ONE scatter collective (ncclScatter) */
+            for (int r = 0; r < c->world; ++r) {
+                int t[4];
+                pcmx_cart_tile(&topo, r, H, W, t);
+                TRY(be->copy2d(stage + (size_t)r * tbytes, (size_t)w + 2, full_p + (size_t)t[0] * pw + t[2], pw,
+                               (size_t)w + 2, (size_t)h + 2, ctx));
             }
-            off += th * tw;
+            TRY(be->sync(ctx));
+        } else { /* uneven tiles: one grouped message per rank */
+            TRY(pcmx_comm_group_start(c));
+            for (int r = 0; r < c->world; ++r) {
+                int t[4];
+                pcmx_cart_tile(&topo, r, H, W, t);
+                const size_t th = (size_t)(t[1] - t[0] + 2), tw = (size_t)(t[3] - t[2] + 2);
+                unsigned char* dst = r == 0 ? img_p : stage + off;
+                TRY(be->copy2d(dst, tw, full_p + (size_t)t[0] * pw + t[2], pw, tw, th, ctx));
+                if (r) {
+                    TRY(be->sync(ctx));
+                    TRY(pcmx_comm_send(c, dst, th * tw, r));
+                }
+                off += th * tw;
+            }
+            TRY(pcmx_comm_group_end(c));
         }
-        TRY(pcmx_comm_group_end(c));
-    } else {
+    } else if (!equal) {
         TRY(pcmx_comm_recv(c, img_p, tbytes, 0));
     }
+    if (equal) TRY(pcmx_comm_scatter(c, root ? stage : NULL, img_p, tbytes, 0));
 
     /* ---- seeds: the reference's four corner seeds (region.c:450-490) in global coordinates */
     TRY(be->memset0(reg_p, tbytes, ctx));
@@ -261,8 +280,27 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
         TRY(be->memset0(flag, sizeof(int), ctx));
     }
 
-    /* ---- gather interiors to root (one message per rank) */
-    if (root) {
+    /* ---- gather interiors to root (ONE gather collective for equal tiles, else one message per rank) */
+    if (equal) {
+        const size_t pw = (size_t)W + 2, n = (size_t)w * h;
+        /* contiguous interior, staged through img_p (no longer needed) */
+        TRY(be->copy2d(img_p, (size_t)w, reg_p + (w + 2) + 1, (size_t)w + 2, (size_t)w, (size_t)h, ctx));
+        TRY(be->sync(ctx));
+        TRY(pcmx_comm_gather(c, img_p, root ? stage : NULL, n, 0));
+        TRY(pcmx_comm_sync(c));
+        if (root) {
+            full_reg = (unsigned char*)calloc((size_t)(H + 2) * pw, 1);
+            for (int r = 0; r < c->world; ++r) {
+                int t[4];
+                pcmx_cart_tile(&topo, r, H, W, t);
+                TRY(be->copy2d(full_p + (size_t)(t[0] + 1) * pw + t[2] + 1, pw, stage + (size_t)r * n, (size_t)w,
+                               (size_t)w, (size_t)h, ctx));
+            }
+            TRY(be->d2h(full_reg, full_p, (size_t)(H + 2) * pw, ctx));
+            for (int r = 0; r < H; ++r)
+                memcpy(region_out + (size_t)r * W, full_reg + (size_t)(r + 1) * pw + 1, (size_t)W);
+        }
+    } else if (root) {
         const size_t pw = (size_t)W + 2;
         full_reg = (unsigned char*)calloc((size_t)(H + 2) * pw, 1);
         /* reuse full_p as the padded device region image */
