@@ -9,8 +9,9 @@
 //    rows and, by shuffles, along columns), 4x4 tiles per workgroup exchanging borders through LDS. 3-D:
 //    BIT-PARALLEL one-wave tiles of 64x8x8 — a lane holds one 64-voxel row as
 //    a 64-bit mask, similarity to the x / y / z neighbours as link masks, and a sweep is a few 64-bit ops
-//    plus cross-lane shuffles (a front crosses a whole row per sweep; no LDS, no barriers): 0.73 ms per
-//    512^3 grow (the 32x8x8 LDS-tile version took 1.47 ms).
+//    plus cross-lane shuffles (a front crosses a whole row per sweep; no LDS, no barriers): 0.52 ms of
+//    kernels per 512^3 grow (the 32x8x8 LDS-tile version took 1.47 ms), 0.63 ms with the host loop
+//    (fixpoint_pipelined: the changed-flag check of a batch overlaps the next batch).
 //  * Active-tile worklist: a tile only runs if a face neighbour changed in the previous launch. 2-D:
 //    act_in -> act_out flags over the block grid (self-cleaning, no memset between launches). 3-D (32k tiles at 512^3): a compacted device-built list
 //    walked by a persistent grid, so a launch costs the frontier, not a full-volume dispatch.
@@ -205,8 +206,9 @@ __global__ __launch_bounds__(kThreads2) void region2d_bits_kernel(u64* __restric
 constexpr int kListGrid = 2048;  // persistent grid of the list kernel (8 workgroups per CU)
 
 struct Grow3dWs {
-    int flag;
+    int flags[4];  // "a tile changed" flag of each batch in flight (fixpoint_pipelined ring)
     int count[3];
+    int pad;
     // followed by: int mark[ntiles]; int list[2][ntiles]
 };
 
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(256) void region3d_bits_kernel(const unsigned char*
                                                            unsigned char* __restrict__ region, int dim, int nz,
                                                            int halos, int thr, int nbx, int nby, int nbz, int epoch,
                                                            Grow3dWs* __restrict__ ws, int* __restrict__ mark,
-                                                           int* __restrict__ lists, int ntiles) {
+                                                           int* __restrict__ lists, int ntiles, int* __restrict__ flag) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = pcmx::lane_id();
     const int* list_in = lists + (epoch & 1) * ntiles;
     int* list_out = lists + ((epoch + 1) & 1) * ntiles;
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(256) void region3d_bits_kernel(const unsigned char*
         const int t = list_in[idx];
         const int bx = t % nbx, by = (t / nbx) % nby, bz = t / (nbx * nby);
         const unsigned f = grow_tile3d_bits(data, region, dim, nz, halos & 1, halos & 2, thr, bx, by, bz, epoch == 0);
-        if ((f & 64u) && lane == 0) ws->flag = 1;
+        if ((f & 64u) && lane == 0) *flag = 1;
         // faces whose voxels changed: the neighbour across sees new halo voxels next launch
         if (lane >= 1 && lane <= 6 && ((f >> (lane - 1)) & 1u)) {
             const int d = lane;
@@ -479,6 +481,72 @@ __global__ __launch_bounds__(256) void region3d_step_kernel(const unsigned char*
 }  // namespace
 
 namespace {
+
+// Host side of the iterate-to-fixpoint loops. A batch of launches sets a device flag when anything changed; the
+// fixpoint is the first batch that changed nothing. Instead of a blocking read-back per batch (the GPU idled
+// ~40 us per batch behind the host's copy + sync round trip), the NEXT batch is enqueued before the host waits
+// for the current one's flag: each batch owns a flag slot (ring of kFixRing), its flag is copied into pinned
+// host memory and an event is recorded; the GPU always has the next batch queued, and after convergence at most
+// one speculative batch runs, whose launches find an empty worklist and exit.
+constexpr int kFixRing = 4;
+struct FixpointHost {
+    int* pinned = nullptr;
+    hipEvent_t ev[kFixRing] = {};
+    unsigned pending = 0;  // slots whose copy may still be in flight from an earlier call
+    bool ready = false;
+};
+FixpointHost* fixpoint_host() {
+    constexpr int kMaxDev = 64;
+    thread_local FixpointHost hosts[kMaxDev];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+    FixpointHost& h = hosts[dev];
+    if (!h.ready) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&h.pinned), kFixRing * sizeof(int), hipHostMallocPortable) != hipSuccess)
+            return nullptr;
+        for (int i = 0; i < kFixRing; ++i)
+            if (hipEventCreateWithFlags(&h.ev[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+        h.ready = true;
+    }
+    for (int i = 0; i < kFixRing; ++i)  // a speculative batch of the previous call may still be copying
+        if (h.pending & (1u << i)) (void)hipEventSynchronize(h.ev[i]);
+    h.pending = 0;
+    return &h;
+}
+
+// launch(n, dflag, first) enqueues n launches (global launch indices first..first+n-1) that raise *dflag on a
+// change; dflags: kFixRing device ints. Returns 0 at the fixpoint, PCMX_ERR_NOT_CONVERGED when max_launches ran
+// out with the last batch still changing; *launches_out = launches up to the confirming batch.
+template <class Launch>
+int fixpoint_pipelined(hipStream_t s, int* dflags, int batch, int max_launches, Launch&& launch, int* launches_out) {
+    FixpointHost* H = fixpoint_host();
+    if (!H) return PCMX_ERR_ARG;
+    int launched = 0, confirmed = 0, head = 0, tail = 0, len[kFixRing] = {};
+    bool converged = false;
+    while (true) {
+        while (head - tail < 2 && launched < max_launches) {  // keep two batches queued
+            const int slot = head % kFixRing, n = batch < max_launches - launched ? batch : max_launches - launched;
+            PCMX_HIP_RET(hipMemsetAsync(&dflags[slot], 0, sizeof(int), s));
+            if (const int lrc = launch(n, &dflags[slot], launched)) return lrc;
+            PCMX_HIP_RET(hipMemcpyAsync(&H->pinned[slot], &dflags[slot], sizeof(int), hipMemcpyDeviceToHost, s));
+            PCMX_HIP_RET(hipEventRecord(H->ev[slot], s));
+            H->pending |= 1u << slot;
+            launched += n, len[slot] = n, ++head;
+        }
+        if (tail == head) break;
+        const int slot = tail % kFixRing;
+        PCMX_HIP_RET(hipEventSynchronize(H->ev[slot]));
+        H->pending &= ~(1u << slot);
+        confirmed += len[slot], ++tail;
+        if (H->pinned[slot] == 0) {
+            converged = true;
+            break;
+        }
+    }
+    if (launches_out) *launches_out = confirmed;
+    return converged ? 0 : PCMX_ERR_NOT_CONVERGED;
+}
+
 struct Region2dGeom {
     int R, C, nw, nbx, nby;
     long long words, nblocks;
@@ -497,7 +565,7 @@ extern "C" long long pcmx_region2d_workspace_bytes(int H, int W) {
     return 64 + ((2 * g.nblocks * 4 + 7) / 8) * 8 + 3 * g.words * 8;
 }
 
-// ws: [flag | act0 | act1 | rb | hl | vl]. Host reads the changed flag once per `batch` launches.
+// ws: [flag ring (16 ints) | act0 | act1 | rb | hl | vl]. Batches of `batch` launches, pipelined fixpoint check.
 extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* region, int H, int W, int ld, int thr,
                                   void* ws, int batch, int max_launches, hipStream_t s, int* launches_out) {
     if (H <= 0 || W <= 0 || ld < W + 2 || !ws || ((uintptr_t)ws & 7)) return PCMX_ERR_ARG;
@@ -515,23 +583,21 @@ extern "C" int pcmx_region2d_grow(const unsigned char* img, unsigned char* regio
     PCMX_HIP_RET(hipMemsetAsync(act[1], 0, g.nblocks * sizeof(int), s));
     const dim3 grid(g.nbx, g.nby);
     if (batch < 1) batch = 4;
-    int launches = 0, cur = 0, h = 1;
-    while (launches < max_launches) {
-        PCMX_HIP_RET(hipMemsetAsync(flag, 0, sizeof(int), s));
-        for (int b = 0; b < batch && launches < max_launches; ++b, ++launches) {
-            region2d_bits_kernel<<<grid, kThreads2, 0, s>>>(rb, hl, vl, g.R, H, W, g.nw, act[cur], act[cur ^ 1], flag);
-            PCMX_HIP_RET(hipGetLastError());
-            cur ^= 1;
-        }
-        PCMX_HIP_RET(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-        PCMX_HIP_RET(hipStreamSynchronize(s));
-        if (!h) break;
-    }
+    const int rc = fixpoint_pipelined(
+        s, flag, batch, max_launches,
+        [&](int n, int* f, int first) {
+            for (int b = 0; b < n; ++b) {  // act lists alternate by global launch index
+                const int cur = (first + b) & 1;
+                region2d_bits_kernel<<<grid, kThreads2, 0, s>>>(rb, hl, vl, g.R, H, W, g.nw, act[cur], act[cur ^ 1], f);
+            }
+            return (int)hipGetLastError();
+        },
+        launches_out);
+    if (rc != 0 && rc != PCMX_ERR_NOT_CONVERGED) return rc;
     region2d_bits_store_kernel<<<(unsigned)(((long long)H * W + 255) / 256), 256, 0, s>>>(region, H, W, ld, g.nw, rb);
     PCMX_HIP_RET(hipGetLastError());
-    if (launches_out) *launches_out = launches;
-    // the last launch still changed something: the fixpoint was not confirmed (the region stored is partial)
-    return h ? PCMX_ERR_NOT_CONVERGED : 0;
+    // NOT_CONVERGED: the last batch still changed something, the fixpoint was not confirmed (the region is partial)
+    return rc;
 }
 
 extern "C" long long pcmx_region3d_slab_workspace_bytes(int dim, int nz) {
@@ -542,8 +608,8 @@ extern "C" long long pcmx_region3d_slab_workspace_bytes(int dim, int nz) {
 extern "C" long long pcmx_region3d_workspace_bytes(int dim) { return pcmx_region3d_slab_workspace_bytes(dim, dim); }
 
 // Grows `region` (0 = outside, nonzero = inside) to the 6-connected fixpoint over dim x dim x nz planes. halos bit 0
-// / bit 1: plane -1 / plane nz exist (read-only seeds of a z-slab). Host syncs once per `batch` launches (a
-// changed-flag read back); launches run on the device-built tile lists in between.
+// / bit 1: plane -1 / plane nz exist (read-only seeds of a z-slab). Launches run on the device-built tile lists
+// in batches of `batch`; the changed-flag check of batch k overlaps batch k+1 (fixpoint_pipelined).
 extern "C" int pcmx_region3d_grow_slab(const unsigned char* data, unsigned char* region, int dim, int nz, int halos,
                                        int thr, void* ws, int batch, int max_launches, hipStream_t s,
                                        int* launches_out) {
@@ -563,20 +629,15 @@ extern "C" int pcmx_region3d_grow_slab(const unsigned char* data, unsigned char*
                                                                                 mark, lists);
     PCMX_HIP_RET(hipGetLastError());
     const int b = batch < 1 ? 8 : batch;
-    int launches = 0, h = 1;
-    while (launches < max_launches) {
-        PCMX_HIP_RET(hipMemsetAsync(&w->flag, 0, sizeof(int), s));
-        for (int i = 0; i < b && launches < max_launches; ++i, ++launches) {
-            region3d_bits_kernel<<<kListGrid, 256, 0, s>>>(data, region, dim, nz, halos, thr, nbx, nby, nbz, launches,
-                                                         w, mark, lists, (int)nt);
-            PCMX_HIP_RET(hipGetLastError());
-        }
-        PCMX_HIP_RET(hipMemcpyAsync(&h, &w->flag, sizeof(int), hipMemcpyDeviceToHost, s));
-        PCMX_HIP_RET(hipStreamSynchronize(s));
-        if (!h) break;
-    }
-    if (launches_out) *launches_out = launches;
-    return h ? PCMX_ERR_NOT_CONVERGED : 0;
+    return fixpoint_pipelined(
+        s, w->flags, b, max_launches,
+        [&](int n, int* f, int first) {
+            for (int i = 0; i < n; ++i)  // launch index = list epoch
+                region3d_bits_kernel<<<kListGrid, 256, 0, s>>>(data, region, dim, nz, halos, thr, nbx, nby, nbz,
+                                                             first + i, w, mark, lists, (int)nt, f);
+            return (int)hipGetLastError();
+        },
+        launches_out);
 }
 
 extern "C" int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char* region, int dim, int thr, void* ws,
