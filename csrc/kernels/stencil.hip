@@ -224,7 +224,7 @@ __device__ __forceinline__ u32x4 update_pairs(const Row8& n, const Row8& c, cons
 // fully unrolled prefetch loop turns into compile-time register names (no window-shifting moves). Rings hold
 // PACKED bf16 rows (4 VGPRs each): the kernel is latency-bound, so unpacking a row per use (ALU) is cheaper
 // than the occupancy lost to 8-VGPR float rows (T=4: 187 -> ~110 VGPRs, 2 -> 4 waves per SIMD).
-template <int T, int kAhead>
+template <int T, int kAhead, int RPW = kRowsPerWave>
 __global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned short* __restrict__ u,
                                                                  unsigned short* __restrict__ out, int rows, int cols,
                                                                  int ld, int halo, int r0, int r1, long long grow0,
@@ -233,8 +233,8 @@ __global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned 
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c0 = (int)blockIdx.x * kOutCols - 8 + lane * 8;  // first column of this lane (may be < 0)
-    const int rs = max(r0, (int)(blockIdx.y * (kWaves * kRowsPerWave) + wave * kRowsPerWave));
-    const int re = min(r1, (int)(blockIdx.y * (kWaves * kRowsPerWave) + (wave + 1) * kRowsPerWave));
+    const int rs = max(r0, (int)(blockIdx.y * (kWaves * RPW) + wave * RPW));
+    const int re = min(r1, (int)(blockIdx.y * (kWaves * RPW) + (wave + 1) * RPW));
     if (rs >= re) return;
     const bool in_grid = c0 >= 0 && c0 + 8 <= cols;  // cols % 8 == 0
     const bool store_lane = in_grid && lane >= 1 && lane <= 62;
