@@ -225,10 +225,9 @@ __device__ __forceinline__ u32x4 update_pairs(const Row8& n, const Row8& c, cons
 // PACKED bf16 rows (4 VGPRs each): the kernel is latency-bound, so unpacking a row per use (ALU) is cheaper
 // than the occupancy lost to 8-VGPR float rows (T=4: 187 -> ~110 VGPRs, 2 -> 4 waves per SIMD).
 template <int T, int kAhead, int RPW = kRowsPerWave>
-__global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned short* __restrict__ u,
-                                                                 unsigned short* __restrict__ out, int rows, int cols,
-                                                                 int ld, int halo, int r0, int r1, long long grow0,
-                                                                 long long grows, float k) {
+__device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict__ u, unsigned short* __restrict__ out,
+                                                int rows, int cols, int ld, int halo, int r0, int r1, long long grow0,
+                                                long long grows, float k) {
     static_assert(T >= 1 && T <= 8, "lanes 1..62 stay exact for at most 8 levels");
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -286,6 +285,151 @@ __global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned 
         }
     }
 }
+template <int T, int kAhead, int RPW = kRowsPerWave>
+__global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned short* __restrict__ u,
+                                                                 unsigned short* __restrict__ out, int rows, int cols,
+                                                                 int ld, int halo, int r0, int r1, long long grow0,
+                                                                 long long grows, float k) {
+    stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, r0, r1, grow0, grows, k);
+}
+
+// ---- v2: the same T-level row pipeline with ~30% fewer VALU ops per level (the kernel is VALU-issue bound):
+//  * wave-uniform row bookkeeping: the wave index is read as a scalar, so the Dirichlet-row test, row clamps
+//    and addressing are SALU work and `fixed_row` is a scalar branch (v1 spent ~4 VALU ops + exec-mask
+//    juggling per level on 64-bit row compares);
+//  * buffer loads/stores with a per-wave descriptor: the row offset is an SGPR soffset, a lane's column offset
+//    a constant voffset, and lanes outside the grid get an out-of-range voffset, so the hardware returns 0 /
+//    drops the store (no per-row address VALU, no select);
+//  * the two lane-edge neighbours enter as DPP-sourced scalar adds (w + e of pair 0 and pair 3 built directly
+//    in their packed registers: no DPP move + pair-forming moves + packed add);
+//  * an intermediate level is rounded to bf16 AS FLOATS with one v_cvt_pk_bf16_f32 per value (low half 0),
+//    instead of pack (4) + unpack (8); only the stored last level is packed;
+//  * no Dirichlet handling on the fast path: the few waves that hold column 0 / cols-1 or compute a level row on
+//    global row 0 / grows-1 (a block column at each side, a wave or two at the top and bottom of the grid) run
+//    the v1 pipeline instead (kept as a separate loop: one kernel, two code paths chosen per wave).
+// Same arithmetic, same order: bit-identical to v1 and to T single steps. Measured (scripts/stencil_lab.hip,
+// 16384^2): T=4 0.29-0.35 -> 0.235-0.24 ms, T=6 0.43-0.49 -> 0.31-0.32 ms (5.1 TGLUP/s).
+__device__ __forceinline__ float round_bf16(float x) {  // x rounded to bf16 (RNE), kept as f32
+    const f32x2 v = {0.f, x};
+    return __uint_as_float(__builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2)));
+}
+
+// Sum of a lane-edge neighbour and an own-lane value as ONE scalar add: keeps the SLP vectoriser from forming a
+// pair (DPP move + pair move + packed add) so the DPP move can fold into the add (v_add_f32_dpp).
+__device__ __forceinline__ float add_scalar(float a, float b) {
+    float r = a + b;
+    asm volatile("" : "+v"(r));
+    return r;
+}
+
+template <bool kLast>
+__device__ __forceinline__ void level_pairs(const Row8& n, const Row8& c, const Row8& s, float k, Row8& nx, u32x4& pk) {
+    const f2 kk = f2{k, k}, m4 = f2{-4.f, -4.f};
+    f2 we[4];
+    const float em1 = pcmx::wave_from_prev(c.p[3].y);  // e_{-1}: previous lane's e7
+    const float e8 = pcmx::wave_from_next(c.p[0].x);   // e_8: next lane's e0
+    we[0] = f2{add_scalar(em1, c.p[1].x), add_scalar(c.p[3].x, c.p[1].y)};  // (e_{-1} + e1, e3 + e5)
+    we[1] = c.p[0] + c.p[2];
+    we[2] = c.p[1] + c.p[3];
+    we[3] = f2{add_scalar(c.p[2].x, c.p[0].y), add_scalar(c.p[2].y, e8)};   // (e2 + e4, e6 + e8)
+    Row8 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const f2 t3 = (n.p[q] + s.p[q]) + we[q];
+        const f2 lap = __builtin_elementwise_fma(c.p[q], m4, t3);
+        o.p[q] = c.p[q] + kk * lap;
+    }
+    if constexpr (kLast) {
+        pk = pack_pairs(o);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx.p[q] = f2{round_bf16(o.p[q].x), round_bf16(o.p[q].y)};
+    }
+}
+
+// The row pipeline of one interior wave (no Dirichlet row or column in reach).
+template <int T, int kAhead>
+__device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, const __amdgpu_buffer_rsrc_t ro, unsigned vld,
+                                            unsigned vst, int sr0, int pitch, int slab_rows, int halo, int rs, int i0,
+                                            int i1, float k) {
+    auto fetch = [&](int r) __attribute__((always_inline)) {  // local row r, clamped into the slab
+        const int sr = min(max(r + halo, 0), slab_rows - 1);
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, vld, (sr - sr0) * pitch, 0));
+    };
+    // ring[t][slot]: level t (0 = u) row with (row index - first) % 3 == slot, as exact floats in pair layout
+    Row8 ring[T][3];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) ring[t][q].p[p] = f2{0.f, 0.f};
+    u32x4 pre[kAhead];
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) pre[j] = fetch(min(i0 + j, i1 - 1));
+    for (int ib = i0; ib < i1; ib += kAhead) {
+#pragma unroll
+        for (int j = 0; j < kAhead; ++j) {
+            const int i = ib + j;
+            if (i < i1) {
+                const int m0 = j % 3, m1 = (j + 2) % 3, m2 = (j + 1) % 3;  // slots of rows i, i-1, i-2
+                ring[0][m0] = unpack_pairs(pre[j]);
+                pre[j] = fetch(min(i + kAhead, i1 - 1));
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const int r = i - t - 1;
+                    if (t + 1 < T) {
+                        u32x4 unused;
+                        level_pairs<false>(ring[t][m2], ring[t][m1], ring[t][m0], k, ring[t + 1 < T ? t + 1 : 0][m0],
+                                           unused);
+                    } else if (r >= rs) {
+                        u32x4 pk;
+                        Row8 unused;
+                        level_pairs<true>(ring[t][m2], ring[t][m1], ring[t][m0], k, unused, pk);
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pcmx::i32x4, pk), ro, vst,
+                                                               (r + halo - sr0) * pitch, 2);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int T, int kAhead, int RPW = kRowsPerWave>
+__global__ __launch_bounds__(kWaves * 64) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
+                                                                  unsigned short* __restrict__ out, int rows, int cols,
+                                                                  int ld, int halo, int r0, int r1, long long grow0,
+                                                                  long long grows, float k) {
+    static_assert(T >= 1 && T <= 8, "lanes 1..62 stay exact for at most 8 levels");
+    static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int c0 = (int)blockIdx.x * kOutCols - 8 + lane * 8;  // first column of this lane (may be < 0)
+    const int rs = max(r0, (int)(blockIdx.y * (kWaves * RPW)) + wave * RPW);
+    const int re = min(r1, (int)(blockIdx.y * (kWaves * RPW)) + (wave + 1) * RPW);
+    if (rs >= re) return;
+    const bool in_grid = c0 >= 0 && c0 + 8 <= cols;  // cols % 8 == 0
+    const bool store_lane = in_grid && lane >= 1 && lane <= 62;
+    const bool fix0 = c0 == 0, fix7 = c0 + 8 == cols;
+    const int slab_rows = rows + 2 * halo;
+    const int i0 = rs - T, i1 = re + T;  // u rows consumed: [i0, i1); level rows computed: [i0 - T, i1 - 1)
+    // the wave's slab rows [sr0, sr1) (clamped like the fetch); one descriptor per buffer over exactly them
+    const int sr0 = min(max(i0 + halo, 0), slab_rows - 1), sr1 = min(max(i1 - 1 + halo, 0), slab_rows - 1) + 1;
+    const int pitch = ld * 2;
+    const unsigned bytes = (unsigned)((size_t)(sr1 - sr0) * (size_t)pitch);
+    const auto ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(u) + (size_t)sr0 * ld, (short)0,
+                                                      (int)bytes, 0x00020000);
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(out + (size_t)sr0 * ld, (short)0, (int)bytes, 0x00020000);
+    const unsigned vld = in_grid ? (unsigned)c0 * 2 : 0x80000000u;     // out of range: the load returns 0
+    const unsigned vst = store_lane ? (unsigned)c0 * 2 : 0x80000000u;  // out of range: the store is dropped
+    const long long g0 = grow0 + i0 - T, g1 = grow0 + i1 - 2;          // global rows of computed level rows
+    const bool edge_rows = (g0 <= 0 && 0 <= g1) || (g0 <= grows - 1 && grows - 1 <= g1);
+    const bool slow = edge_rows || __builtin_amdgcn_ballot_w64(fix0 || fix7) != 0;
+    if (slow)  // a few waves per grid: the v1 pipeline (per-column selects, per-row Dirichlet test; same results)
+        stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, r0, r1, grow0, grows, k);
+    else
+        pipeline_v2<T, kAhead>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
+}
 #pragma clang fp contract(on)
 }  // namespace
 
@@ -315,17 +459,34 @@ extern "C" int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols
     // rows that read `steps` rows beyond the local range need that deep a halo unless the side is a global edge
     const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
     if (halo < steps && ((r0 < steps && !top_global) || (r1 > rows - steps && !bot_global))) return -1;
-    dim3 grid((cols + kOutCols - 1) / kOutCols, (rows + kWaves * kRowsPerWave - 1) / (kWaves * kRowsPerWave));
     const unsigned short* ui = (const unsigned short*)u;
     unsigned short* uo = (unsigned short*)out;
+    // T = 2 is HBM-bound: the v1 kernel. T >= 3 is VALU-bound: v2 with 48 rows per wave, or 32 on short ranges
+    // (a rank's slab at N = 8 is 2048 rows: shorter waves give 2x the waves at 2T/RPW more redundant rows;
+    // measured 2.6 vs 2.0 TGLUP/s at T = 6 on a 2048 x 16384 slab, scripts/stencil_lab.hip)
+    const bool short_range = r1 - r0 < 8192;
+    auto grid_for = [&](int rpw) {
+        return dim3((cols + kOutCols - 1) / kOutCols, (rows + kWaves * rpw - 1) / (kWaves * rpw));
+    };
+#define PCMX_STENCIL_V2(T)                                                                                          \
+    if (short_range)                                                                                                \
+        stencil5xT2_kernel<T, 6, 32><<<grid_for(32), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,     \
+                                                                          global_row0, global_rows, k);             \
+    else                                                                                                            \
+        stencil5xT2_kernel<T, 6, 48><<<grid_for(48), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,     \
+                                                                          global_row0, global_rows, k);
     switch (steps) {
-        case 2: stencil5xT_kernel<2, 6><<<grid, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1, global_row0, global_rows, k); break;
-        case 3: stencil5xT_kernel<3, 6><<<grid, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1, global_row0, global_rows, k); break;
-        case 4: stencil5xT_kernel<4, 6><<<grid, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1, global_row0, global_rows, k); break;
-        case 6: stencil5xT_kernel<6, 6><<<grid, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1, global_row0, global_rows, k); break;
-        case 8: stencil5xT_kernel<8, 6><<<grid, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1, global_row0, global_rows, k); break;
+        case 2:
+            stencil5xT_kernel<2, 6><<<grid_for(kRowsPerWave), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,
+                                                                                 global_row0, global_rows, k);
+            break;
+        case 3: PCMX_STENCIL_V2(3) break;
+        case 4: PCMX_STENCIL_V2(4) break;
+        case 6: PCMX_STENCIL_V2(6) break;
+        case 8: PCMX_STENCIL_V2(8) break;
         default: return -1;
     }
+#undef PCMX_STENCIL_V2
     return (int)hipGetLastError();
 }
 

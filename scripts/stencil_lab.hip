@@ -1,39 +1,34 @@
-// Stencil lab: rows per wave of the fused T=4 kernel on the 16384^2 bf16 grid (one HBM pass per 4 updates).
-// A wave recomputes 2T rows beyond its RPW output rows (12.5% extra at RPW 64) and the grid has
-// 34 x rows/(4 RPW) workgroups at ~3 resident waves per SIMD: RPW trades redundant rows against the last-round
-// tail. Checks every variant's output bit for bit against RPW 64.
+// Stencil lab: fused T-step kernels on the 16384^2 bf16 grid (one HBM pass per T updates).
+//   v1 = stencil5xT_kernel (packed-f32 pairs, VALU row bookkeeping), v2 = stencil5xT2_kernel (scalar row
+//   bookkeeping, buffer loads/stores, DPP-sourced edge adds, cvt-only intermediate rounding); RPW variants of v2.
+// Every variant is checked bit for bit against v1 at the same T. Data: bf16 values in [0.5, 1) plus the
+// Dirichlet rows / columns of a full grid (global rows = rows).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/kernels -Icsrc/runtime \
-//          scripts/stencil_lab.hip -o bin/stencil_lab
+//          scripts/stencil_lab.hip -o bin/stencil_lab ;  run: bin/stencil_lab [T...]
 #include "../csrc/kernels/stencil.hip"
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
-template <int RPW>
+static int g_rows = 16384;  // rows of the slab (STENCIL_ROWS: 2048 = one rank's slab of the 16384^2 grid at N=8)
+
+template <int V, int T, int RPW, int AH = 6>
 void launch(const unsigned short* u, unsigned short* o, int n, int ld, int halo, float k) {
-    dim3 grid((n + kOutCols - 1) / kOutCols, (n + kWaves * RPW - 1) / (kWaves * RPW));
-    stencil5xT_kernel<4, 6, RPW><<<grid, kWaves * 64>>>(u, o, n, n, ld, halo, 0, n, 0, n, k);
+    const int rows = g_rows;
+    dim3 grid((n + kOutCols - 1) / kOutCols, (rows + kWaves * RPW - 1) / (kWaves * RPW));
+    if constexpr (V == 1)
+        stencil5xT_kernel<T, 6, RPW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, 0, rows, 0, rows, k);
+    else
+        stencil5xT2_kernel<T, AH, RPW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, 0, rows, 0, rows, k);
 }
 
-int main() {
-    const int n = 16384, halo = 4, ld = n;
-    const size_t elems = (size_t)(n + 2 * halo) * ld;
-    std::vector<unsigned short> h(elems);
-    unsigned s = 12345;
-    for (auto& v : h) {
-        s = s * 1664525u + 1013904223u;
-        v = (unsigned short)(0x3f00 + ((s >> 16) & 0xff));  // bf16 values in [0.5, 1)
-    }
-    unsigned short *u, *o, *ref;
-    CK(hipMalloc(&u, elems * 2));
-    CK(hipMalloc(&o, elems * 2));
-    CK(hipMalloc(&ref, elems * 2));
-    CK(hipMemcpy(u, h.data(), elems * 2, hipMemcpyHostToDevice));
-    CK(hipMemset(o, 0, elems * 2));
-    CK(hipMemset(ref, 0, elems * 2));
+template <int T>
+int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, int ld, size_t elems) {
+    const int halo = 8;
     const float k = 0.1f;
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
@@ -47,28 +42,72 @@ int main() {
         float ms = 0;
         hipEventElapsedTime(&ms, e0, e1);
         ms /= 20;
-        printf("%-8s %.4f ms  %.0f GLUP/s\n", name, ms, (double)n * n * 4 / (ms * 1e-3) / 1e9);
+        printf("T=%d rows=%d %-10s %.4f ms  %.0f GLUP/s\n", T, g_rows, name, ms, (double)g_rows * n * T / (ms * 1e-3) / 1e9);
         fflush(stdout);
     };
-    launch<64>(u, ref, n, ld, halo, k);
-    CK(hipDeviceSynchronize());
     std::vector<unsigned short> a(elems), b(elems);
+    CK(hipMemset(ref, 0, elems * 2));
+    launch<1, T, 64>(u, ref, n, ld, halo, k);
+    CK(hipDeviceSynchronize());
     CK(hipMemcpy(a.data(), ref, elems * 2, hipMemcpyDeviceToHost));
-    for (int rnd = 0; rnd < 2; ++rnd) {
-        time("rpw64", [&] { launch<64>(u, o, n, ld, halo, k); });
-        time("rpw96", [&] { launch<96>(u, o, n, ld, halo, k); });
-        time("rpw128", [&] { launch<128>(u, o, n, ld, halo, k); });
-        time("rpw48", [&] { launch<48>(u, o, n, ld, halo, k); });
-    }
-    const int rpws[3] = {96, 128, 48};
-    for (int i = 0; i < 3; ++i) {
+    auto same = [&](const char* name, auto fn) -> int {
         CK(hipMemset(o, 0, elems * 2));
-        if (rpws[i] == 96) launch<96>(u, o, n, ld, halo, k);
-        if (rpws[i] == 128) launch<128>(u, o, n, ld, halo, k);
-        if (rpws[i] == 48) launch<48>(u, o, n, ld, halo, k);
+        fn();
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(b.data(), o, elems * 2, hipMemcpyDeviceToHost));
-        printf("rpw%d identical to rpw64: %s\n", rpws[i], memcmp(a.data(), b.data(), elems * 2) == 0 ? "yes" : "NO");
+        size_t bad = 0, first = 0;
+        for (size_t i = 0; i < elems; ++i)
+            if (a[i] != b[i] && !bad++) first = i;
+        printf("T=%d %-10s identical to v1: %s", T, name, bad == 0 ? "yes\n" : "NO");
+        if (bad) printf(" (%zu cells differ, first at slab row %zu col %zu: %04x vs %04x)\n", bad, first / ld, first % ld, a[first], b[first]);
+        return 0;
+    };
+    same("v2", [&] { launch<2, T, 64>(u, o, n, ld, halo, k); });
+    same("v2rpw96", [&] { launch<2, T, 96>(u, o, n, ld, halo, k); });
+
+    same("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
+    same("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
+    same("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
+    for (int rnd = 0; rnd < 2; ++rnd) {
+        time("v1", [&] { launch<1, T, 64>(u, o, n, ld, halo, k); });
+        time("v2", [&] { launch<2, T, 64>(u, o, n, ld, halo, k); });
+        time("v2rpw96", [&] { launch<2, T, 96>(u, o, n, ld, halo, k); });
+
+        time("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
+        time("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
+        time("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
+    }
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    const int n = 16384, halo = 8, ld = n;
+    if (const char* r = getenv("STENCIL_ROWS")) g_rows = atoi(r);
+    const size_t elems = (size_t)(n + 2 * halo) * ld;
+    std::vector<unsigned short> h(elems);
+    unsigned s = 12345;
+    for (auto& v : h) {
+        s = s * 1664525u + 1013904223u;
+        v = (unsigned short)(0x3f00 + ((s >> 16) & 0xff));  // bf16 values in [0.5, 1)
+    }
+    unsigned short *u, *o, *ref;
+    CK(hipMalloc(&u, elems * 2));
+    CK(hipMalloc(&o, elems * 2));
+    CK(hipMalloc(&ref, elems * 2));
+    CK(hipMemcpy(u, h.data(), elems * 2, hipMemcpyHostToDevice));
+    std::vector<int> ts;
+    for (int i = 1; i < argc; ++i) ts.push_back(atoi(argv[i]));
+    if (ts.empty()) ts = {4};
+    for (int T : ts) {
+        int rc = 0;
+        switch (T) {
+            case 2: rc = run<2>(u, o, ref, n, ld, elems); break;
+            case 4: rc = run<4>(u, o, ref, n, ld, elems); break;
+            case 6: rc = run<6>(u, o, ref, n, ld, elems); break;
+            case 8: rc = run<8>(u, o, ref, n, ld, elems); break;
+            default: printf("T=%d not built\n", T);
+        }
+        if (rc) return rc;
     }
     return 0;
 }

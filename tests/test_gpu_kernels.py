@@ -215,11 +215,12 @@ def test_stencil_row_range_split(gpu):
     assert torch.equal(full, part)
 
 
-@pytest.mark.parametrize("steps", [2, 3, 4, 8])
-@pytest.mark.parametrize("shape", [(256, 512), (1000, 1000), (515, 4096), (9, 2000)])
+@pytest.mark.parametrize("steps", [2, 3, 4, 6, 8])
+@pytest.mark.parametrize("shape", [(256, 512), (1000, 1000), (515, 4096), (9, 2000), (8300, 1000)])
 def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
     """Temporal-blocking kernel == `steps` single steps (bf16 bits); random data so every lane/strip-overlap
-    path counts; column counts that are not multiples of the 496-column output strip."""
+    path counts; column counts that are not multiples of the 496-column output strip; >= 8192 rows takes the
+    48-rows-per-wave launch, fewer the 32-row one (interior waves: v2 fast path, edge waves: v1 pipeline)."""
     rows, cols = shape
     g = torch.Generator().manual_seed(rows + steps)
     u = (torch.rand(rows + 2, cols, generator=g) * 4 - 2).to(torch.bfloat16)
@@ -232,7 +233,7 @@ def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
     assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16))
 
 
-@pytest.mark.parametrize("steps", [2, 4])
+@pytest.mark.parametrize("steps", [2, 4, 6])
 @pytest.mark.parametrize("global_row0,global_rows", [(0, 300), (40, 340), (40, 300)])
 def test_stencil_fused_deep_halo_slab_and_row_split(gpu, global_row0, global_rows, steps):
     """A rank's slab with `steps` halo rows (neighbour rows present) and the interior/boundary split used for
