@@ -157,19 +157,27 @@ int pcmx_stencil5x2_bf16(const void* u, void* out, int rows, int cols, int ld, i
 
 /* ---------------------------------------------------------------- SpMV */
 long long pcmx_spmv_csr_plan(const long long* row_ptr_host, int n_rows, void* items_host, long long max_items);
+/* the same cut with items of at most item_nnz (64..1024, multiple of 64) nonzeros */
+long long pcmx_spmv_csr_plan_nnz(const long long* row_ptr_host, int n_rows, void* items_host, long long max_items,
+                                 int item_nnz);
 int pcmx_spmv_csr(const long long* row_ptr, const int* col, const float* val, const float* x, float* y, int n_rows,
                   const void* items, long long n_items, hipStream_t s);
 /* XCD-sliced CSR (ops/sparse.py SlicedCSR): n_slices = 8 * phases <= PCMX_SPMV_MAX_SLICES; per nonzero col, val
- * and lrow (u16 row offset inside its item); per slice nnz-balanced items (a later piece of a split long row
- * has row1 == row0). Slice s runs on the blocks b with b % 8 == s % 8 (one XCD), writes ypart[s][0, n_rows);
- * a combine pass sums the partials into y and a fix-up adds extra[fix[k].item] to y[fix[k].row].
- * slice_nz0 / slice_item0 are HOST arrays (n_slices and n_slices + 1 entries).
- * mode: 0 = production; bit 0 = skip the x gathers (lab measurement only); mode >> 8 (if nonzero) = resident
+ * and lrow (u16 offset of its row inside its item, rows counted among the rows the slice touches); per slice
+ * nnz-balanced items over the slice's touched rows (a later piece of a split long row has row1 == row0).
+ * Slice s runs on the blocks b with b % 8 == s % 8 (one XCD) and writes one compact partial per touched row to
+ * ypart[slice_out0[s] + touched-row index]; a combine pass sums each row's partials into y (row_mask[r] bit s:
+ * slice s touches row r; chunk_base[c * n_slices + s]: touched rows of slice s before row 64c) and a fix-up adds
+ * extra[fix[k].item] to y[fix[k].row]. slice_nz0 / slice_item0 / slice_out0 are HOST arrays (n_slices,
+ * n_slices + 1 and n_slices + 1 entries).
+ * mode: bit 1 = items planned with item_nnz 512 (else 1024); bit 0 = skip the x gathers (lab measurement
+ * only); mode >> 8 (if nonzero) = resident
  * blocks per CU (default 2). */
 #define PCMX_SPMV_MAX_SLICES 32
 int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x, float* ypart,
                      float* extra, float* y, int n_rows, int n_cols, int n_slices, const long long* slice_nz0,
-                     const long long* slice_item0, const void* items, const void* fix, int n_fix, int mode,
+                     const long long* slice_item0, const long long* slice_out0, const void* items,
+                     const unsigned* row_mask, const int* chunk_base, const void* fix, int n_fix, int mode,
                      hipStream_t s);
 int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                      const float* x, float* y, hipStream_t s);

@@ -15,8 +15,11 @@
 // measured chip-wide by scripts/gather_lab.hip, vs ~270 G/s when each XCD gathers from its own <= 4 MiB).
 // So the columns are cut into S = 8 * phases slices (a small, hot head of columns is dealt by rows instead,
 // so every XCD keeps its own copy of it); workgroups are dealt round-robin over the 8 XCDs, so block b runs
-// slice (b % 8) + 8 * phase and all of a slice's gathers stay inside ONE L2. Each slice writes a partial-y
-// row, a combine pass sums the S partials, a fix-up adds the later pieces of split long rows.
+// slice (b % 8) + 8 * phase and all of a slice's gathers stay inside ONE L2. Each slice writes a COMPACT
+// partial y: one value per row the slice touches (36% of the S x n_rows pairs on the 1e8-nnz power-law graph;
+// the dense S x n_rows partials cost 640 MB of writes + 640 MB of combine reads per product). A combine pass
+// sums every row's partials (per-row slice mask + per-64-row-chunk base offsets, ranks from wave ballots), a
+// fix-up adds the later pieces of split long rows.
 //
 // Banded (implicit column indices): one wave per row; the 5 bands are contiguous slices of x and of the
 // value array, so all loads are unit-stride and no column index is ever read.
@@ -123,31 +126,34 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_csr_items_kernel(
 struct SliceMeta {
     long long nz0[kMaxSlices];    // first nonzero of slice s in the slice-major col/val/lrow
     long long item0[kMaxSlices + 1];
+    long long out0[kMaxSlices];   // first compact partial of slice s
 };
 
+template <int kPL>
 struct StreamRegs {
-    int c[kPerLane];
-    float v[kPerLane];
-    unsigned short r[kPerLane];
+    int c[kPL];
+    float v[kPL];
+    unsigned short r[kPL];
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
+template <int kPL>
 __device__ __forceinline__ void load_item_stream(const int* __restrict__ col, const float* __restrict__ val,
-                                                 const unsigned short* __restrict__ lrow, const Item& it, StreamRegs& q,
-                                                 int lane) {
+                                                 const unsigned short* __restrict__ lrow, const Item& it,
+                                                 StreamRegs<kPL>& q, int lane) {
     const unsigned n = (unsigned)(it.nz1 - it.nz0);
     const auto rc = rsrc(col + it.nz0, n * 4), rv = rsrc(val + it.nz0, n * 4), rr = rsrc(lrow + it.nz0, n * 2);
 #pragma unroll
-    for (int j = 0; j < kPerLane; ++j) {  // aux 2 = nt: streamed once
+    for (int j = 0; j < kPL; ++j) {  // aux 2 = nt: streamed once
         const unsigned i = j * kWave + lane;
         q.c[j] = __builtin_amdgcn_raw_buffer_load_b32(rc, i * 4, 0, 2);
         q.v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, i * 4, 0, 2));
     }
 #pragma unroll
-    for (int j = 0; j < kPerLane; ++j) q.r[j] = __builtin_amdgcn_raw_buffer_load_b16(rr, (j * kWave + lane) * 2, 0, 2);
+    for (int j = 0; j < kPL; ++j) q.r[j] = __builtin_amdgcn_raw_buffer_load_b16(rr, (j * kWave + lane) * 2, 0, 2);
 }
 
 struct SlicedCtx {
@@ -166,13 +172,13 @@ struct SlicedCtx {
 // One pipeline step: gathers of the current item, stream loads of the next item, then the current item's
 // LDS scatter and stores. Called alternately with the two register sets swapped (a register copy would make
 // the compiler wait for the prefetch).
-template <int kMode>
-__device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, const Item& cur, const StreamRegs& q,
-                                            Item& nitem, StreamRegs& nq) {
+template <int kMode, int kPL>
+__device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, const Item& cur, const StreamRegs<kPL>& q,
+                                            Item& nitem, StreamRegs<kPL>& nq) {
     const int lane = k.lane;
-    float g[kPerLane];
+    float g[kPL];
 #pragma unroll
-    for (int j = 0; j < kPerLane; ++j)
+    for (int j = 0; j < kPL; ++j)
         g[j] = (kMode & 1) ? __int_as_float(q.c[j])
                            : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(k.rx, q.c[j] * 4, 0, 0));
     const long long nxt = it + k.stride;
@@ -186,21 +192,21 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
     if (nrows <= 1) {  // whole short row or a piece of a long row (later piece: row1 == row0 -> extra[it])
         float acc = 0.f;
 #pragma unroll
-        for (int j = 0; j < kPerLane; ++j) acc += q.v[j] * g[j];
+        for (int j = 0; j < kPL; ++j) acc += q.v[j] * g[j];
         acc = pcmx::wave_reduce<float, 0>(acc);
         if (lane == 0) k.yw[0] = acc;
         dst = nrows == 1 ? k.yp + cur.row0 : k.extra + it;
         nstore = 1;
     } else {
 #pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
+        for (int j = 0; j < kPL; ++j) {  // compact rows: every row of an item holds >= 1 of its <= 64 kPL nonzeros
             const int i = j * kWave + lane;
             if (i < nrows) k.yw[i] = 0.f;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
+        for (int j = 0; j < kPL; ++j) {
             const int i = j * kWave + lane;
             if (i < n) atomicAdd(&k.yw[q.r[j]], q.v[j] * g[j]);
         }
@@ -211,7 +217,7 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const auto ry = rsrc(dst, (unsigned)nstore * 4);
 #pragma unroll
-    for (int j = 0; j < kPerLane; ++j) {
+    for (int j = 0; j < kPL; ++j) {
         const int i = j * kWave + lane;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(k.yw[i]), ry, i * 4, 0, 2);
     }
@@ -221,11 +227,11 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
     return more;
 }
 
-template <int kMode>
+template <int kMode, int kPL>
 __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     const unsigned short* __restrict__ lrow, const int* __restrict__ col, const float* __restrict__ val,
     const float* __restrict__ x, int n_cols, float* __restrict__ ypart, float* __restrict__ extra,
-    const Item* __restrict__ items, SliceMeta meta, int n_rows, int blocks_per_slice) {
+    const Item* __restrict__ items, SliceMeta meta, int blocks_per_slice) {
     __shared__ float yl[kWavesPerBlock][kItemRows + 1];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int b = blockIdx.x;
@@ -239,36 +245,52 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     const long long base = meta.nz0[s];
     k.col = col + base, k.val = val + base, k.lrow = lrow + base;
     k.rx = rsrc(x, (unsigned)n_cols * 4);
-    k.items = items, k.extra = extra, k.yp = ypart + (size_t)s * n_rows, k.yw = yl[w];
+    k.items = items, k.extra = extra, k.yp = ypart + meta.out0[s], k.yw = yl[w];
     k.lane = pcmx::lane_id();
     Item ia = items[it], ib;
-    StreamRegs qa, qb;
-    load_item_stream(k.col, k.val, k.lrow, ia, qa, k.lane);
-    while (sliced_step<kMode>(k, it, ia, qa, ib, qb) && sliced_step<kMode>(k, it, ib, qb, ia, qa)) {
+    StreamRegs<kPL> qa, qb;
+    load_item_stream<kPL>(k.col, k.val, k.lrow, ia, qa, k.lane);
+    while (sliced_step<kMode, kPL>(k, it, ia, qa, ib, qb) && sliced_step<kMode, kPL>(k, it, ib, qb, ia, qa)) {
     }
 }
 
+// y[r] = sum over the slices touching row r (bit k of mask[r]) of that slice's compact partial, in slice order.
+// One wave per 64-row chunk c: the partial of slice k for lane l sits at out0[k] + base[c][k] + (number of lower
+// lanes whose row slice k also touches) — a ballot + popcount; base[c][*] is wave-uniform (scalar loads).
+struct SliceOut {
+    long long out0[kMaxSlices + 1];
+};
 template <int S>
-__global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restrict__ ypart, float* __restrict__ y,
+__global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restrict__ comp, const unsigned* __restrict__ mask,
+                                                           const int* __restrict__ base, SliceOut so, float* __restrict__ y,
                                                            int n_rows) {
-    using pcmx::f32x4;
-    const int n4 = n_rows / 4;
-    if (n_rows % 4 == 0) {  // partial rows are 16-B aligned
-        for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
-            f32x4 acc = pcmx::ld_nt(reinterpret_cast<const f32x4*>(ypart) + i);
+    // XCD-aware chunk order: workgroups are dealt round-robin over the 8 XCDs, so block b takes chunk group
+    // (b % 8) * (gridDim.x / 8) + b / 8 and each XCD walks ONE contiguous row range (a slice's partial runs of
+    // neighbouring chunks share cache lines in that XCD's L2 instead of being fetched by two XCDs)
+    const int g = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    const int c = __builtin_amdgcn_readfirstlane(g * 4 + (int)threadIdx.x / kWave);
+    const int lane = pcmx::lane_id();
+    const int r = c * kWave + lane;
+    if (c * kWave >= n_rows) return;
+    const unsigned m = r < n_rows ? __builtin_nontemporal_load(mask + r) : 0u;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int* bc = base + (size_t)c * S;
+    // every slice's load is issued unconditionally (a lane whose row the slice does not touch reads out of its
+    // descriptor's range and gets 0), so the S gathers overlap instead of serialising behind branches
+    float v[S];
 #pragma unroll
-            for (int s = 1; s < S; ++s)
-                acc += pcmx::ld_nt(reinterpret_cast<const f32x4*>(ypart + (size_t)s * n_rows) + i);
-            reinterpret_cast<f32x4*>(y)[i] = acc;
-        }
-        return;
+    for (int k = 0; k < S; ++k) {
+        const bool bit = (m >> k) & 1u;
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(bit);
+        const auto rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(comp) + so.out0[k], (short)0,
+                                                          (int)((so.out0[k + 1] - so.out0[k]) * 4), 0x00020000);
+        const unsigned off = bit ? (unsigned)(bc[k] + (int)__popcll(bal & below)) * 4u : 0xffffffffu;
+        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rk, off, 0, 0));
     }
-    for (int r = blockIdx.x * 256 + threadIdx.x; r < n_rows; r += gridDim.x * 256) {
-        float acc = 0.f;
+    float acc = 0.f;
 #pragma unroll
-        for (int s = 0; s < S; ++s) acc += ypart[(size_t)s * n_rows + r];
-        y[r] = acc;
-    }
+    for (int k = 0; k < S; ++k) acc += v[k];  // slice order; untouched slices add +0
+    if (r < n_rows) y[r] = acc;
 }
 
 // later pieces of split long rows: fix[k] = {item index, row}
@@ -310,28 +332,34 @@ __global__ __launch_bounds__(256) void spmv_banded_kernel(const float* __restric
 // Host-side analysis: row_ptr is a HOST array (n_rows+1, int64). Writes up to max_items items into
 // `items_host` (4 x int64 words each: row0, row1, nz0, nz1 packed as in Item) and returns the count, or
 // -1 if max_items is too small. pcmx_spmv_csr_plan_count() gives the exact count first.
-extern "C" long long pcmx_spmv_csr_plan(const long long* row_ptr, int n_rows, void* items_host, long long max_items) {
+extern "C" long long pcmx_spmv_csr_plan_nnz(const long long* row_ptr, int n_rows, void* items_host,
+                                           long long max_items, int item_nnz) {
+    if (item_nnz < 64 || item_nnz > kItemNnz || item_nnz % 64) return -1;
     Item* items = reinterpret_cast<Item*>(items_host);
     long long k = 0;
     int r = 0;
     while (r < n_rows) {
         const long long len = row_ptr[r + 1] - row_ptr[r];
-        if (len > kItemNnz) {  // long row: split into pieces
-            for (long long p = row_ptr[r]; p < row_ptr[r + 1]; p += kItemNnz) {
-                if (items && k < max_items) items[k] = Item{r, r + 1, p, p + kItemNnz < row_ptr[r + 1] ? p + kItemNnz : row_ptr[r + 1]};
+        if (len > item_nnz) {  // long row: split into pieces
+            for (long long p = row_ptr[r]; p < row_ptr[r + 1]; p += item_nnz) {
+                if (items && k < max_items) items[k] = Item{r, r + 1, p, p + item_nnz < row_ptr[r + 1] ? p + item_nnz : row_ptr[r + 1]};
                 ++k;
             }
             ++r;
             continue;
         }
         int r1 = r + 1;
-        while (r1 < n_rows && row_ptr[r1 + 1] - row_ptr[r] <= kItemNnz && r1 - r < kItemRows) ++r1;
+        while (r1 < n_rows && row_ptr[r1 + 1] - row_ptr[r] <= item_nnz && r1 - r < kItemRows) ++r1;
         if (items && k < max_items) items[k] = Item{r, r1, row_ptr[r], row_ptr[r1]};
         ++k;
         r = r1;
     }
     if (items && k > max_items) return -1;
     return k;
+}
+
+extern "C" long long pcmx_spmv_csr_plan(const long long* row_ptr, int n_rows, void* items_host, long long max_items) {
+    return pcmx_spmv_csr_plan_nnz(row_ptr, n_rows, items_host, max_items, kItemNnz);
 }
 
 extern "C" int pcmx_spmv_csr(const long long* row_ptr, const int* col, const float* val, const float* x, float* y,
@@ -348,20 +376,24 @@ extern "C" int pcmx_spmv_csr(const long long* row_ptr, const int* col, const flo
 
 extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x,
                                 float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
-                                const long long* slice_nz0, const long long* slice_item0, const void* items,
-                                const void* fix, int n_fix, int mode, hipStream_t s) {
+                                const long long* slice_nz0, const long long* slice_item0, const long long* slice_out0,
+                                const void* items, const unsigned* row_mask, const int* chunk_base, const void* fix,
+                                int n_fix, int mode, hipStream_t s) {
     if (n_rows <= 0) return 0;
     if (n_slices <= 0 || n_slices % 8 || n_slices > kMaxSlices) return (int)hipErrorInvalidValue;
     const int persist_blocks = (mode >> 8) ? (mode >> 8) : kPersistBlocks;
     SliceMeta meta{};
+    SliceOut so{};
     long long most = 0;
     for (int k = 0; k < n_slices; ++k) {
         meta.nz0[k] = slice_nz0[k];
         meta.item0[k] = slice_item0[k];
+        meta.out0[k] = so.out0[k] = slice_out0[k];
         if (slice_item0[k + 1] < slice_item0[k]) return (int)hipErrorInvalidValue;
         most = slice_item0[k + 1] - slice_item0[k] > most ? slice_item0[k + 1] - slice_item0[k] : most;
     }
     meta.item0[n_slices] = slice_item0[n_slices];
+    so.out0[n_slices] = slice_out0[n_slices];
     if (most > 0) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -371,20 +403,21 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         const long long per = (long long)(cus / 8) * persist_blocks;  // resident blocks per XCD
         const int bp = (int)(need < per ? need : per);
         const unsigned nb = (unsigned)(bp * n_slices);
-        if (mode & 1)
-            spmv_sliced_kernel<1><<<nb, kWavesPerBlock * kWave, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra,
-                                                                        reinterpret_cast<const Item*>(items), meta, n_rows, bp);
-        else
-            spmv_sliced_kernel<0><<<nb, kWavesPerBlock * kWave, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra,
-                                                                        reinterpret_cast<const Item*>(items), meta, n_rows, bp);
+        const Item* it = reinterpret_cast<const Item*>(items);
+        const dim3 blk(kWavesPerBlock * kWave);
+        switch (mode & 3) {  // bit 0: skip the x gathers (lab), bit 1: items of 512 nonzeros (8 per lane)
+            case 0: spmv_sliced_kernel<0, 16><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
+            case 1: spmv_sliced_kernel<1, 16><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
+            case 2: spmv_sliced_kernel<0, 8><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
+            default: spmv_sliced_kernel<1, 8><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
+        }
     }
-    const long long want = (n_rows / 4 + 255) / 256;
-    const int cb = want > 2048 ? 2048 : (want < 1 ? 1 : (int)want);
+    const unsigned cb = (unsigned)((n_rows + 2047) / 2048) * 8;  // 4 waves of 64 rows per block, 8k blocks
     switch (n_slices) {
-        case 8: spmv_combine_kernel<8><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
-        case 16: spmv_combine_kernel<16><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
-        case 24: spmv_combine_kernel<24><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
-        case 32: spmv_combine_kernel<32><<<cb, 256, 0, s>>>(ypart, y, n_rows); break;
+        case 8: spmv_combine_kernel<8><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
+        case 16: spmv_combine_kernel<16><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
+        case 24: spmv_combine_kernel<24><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
+        case 32: spmv_combine_kernel<32><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
         default: return (int)hipErrorInvalidValue;
     }
     if (n_fix > 0)

@@ -458,22 +458,29 @@ at::Tensor spmv_csr(const at::Tensor& row_ptr, const at::Tensor& col, const at::
 // XCD-sliced CSR (see spmv.hip): meta is a CPU int64 tensor [2 * n_slices + 1] = slice nz0[n_slices] ++
 // slice item0[n_slices + 1]; ypart [n_slices * n_rows] and extra [n_items] are caller-owned scratch.
 at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::Tensor& val, const at::Tensor& x,
-                       const at::Tensor& items, const at::Tensor& fix, const at::Tensor& meta, at::Tensor ypart,
-                       at::Tensor extra, int64_t n_rows, const c10::optional<at::Tensor>& out, int64_t mode) {
+                       const at::Tensor& items, const at::Tensor& row_mask, const at::Tensor& chunk_base,
+                       const at::Tensor& fix, const at::Tensor& meta, at::Tensor ypart, at::Tensor extra, int64_t n_rows,
+                       const c10::optional<at::Tensor>& out, int64_t mode) {
     check_gpu(lrow, "lrow", at::kShort), check_gpu(col, "col", at::kInt), check_gpu(val, "val", at::kFloat);
     check_gpu(x, "x", at::kFloat), check_gpu(items, "items", at::kLong), check_gpu(fix, "fix", at::kInt);
     check_gpu(ypart, "ypart", at::kFloat), check_gpu(extra, "extra", at::kFloat);
+    check_gpu(row_mask, "row_mask", at::kInt), check_gpu(chunk_base, "chunk_base", at::kInt);
     TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous(), "spmv_sliced: CPU int64 meta");
-    const int64_t S = (meta.numel() - 1) / 2;
-    TORCH_CHECK(S >= 8 && S % 8 == 0 && S <= PCMX_SPMV_MAX_SLICES, "spmv_sliced: 8, 16, 24 or 32 slices");
-    TORCH_CHECK(ypart.numel() >= S * n_rows && lrow.numel() == col.numel() && val.numel() == col.numel(),
-                "spmv_sliced: ypart / lrow / val shape");
-    TORCH_CHECK(x.numel() < (int64_t(1) << 30), "spmv_sliced: x must be < 2^30 elements (32-bit buffer offsets)");
+    const int64_t S = (meta.numel() - 2) / 3;  // meta = [nz0 (S) | item0 (S + 1) | out0 (S + 1)]
+    TORCH_CHECK(meta.numel() == 3 * S + 2 && S >= 8 && S % 8 == 0 && S <= PCMX_SPMV_MAX_SLICES,
+                "spmv_sliced: 8, 16, 24 or 32 slices");
     const int64_t* m = meta.data_ptr<int64_t>();
+    const int64_t* out0 = m + 2 * S + 1;
+    TORCH_CHECK(lrow.numel() == col.numel() && val.numel() == col.numel(), "spmv_sliced: lrow / val shape");
+    TORCH_CHECK(row_mask.numel() >= n_rows && chunk_base.numel() >= ((n_rows + 63) / 64) * S,
+                "spmv_sliced: row_mask / chunk_base shape");
+    TORCH_CHECK(out0[0] == 0 && ypart.numel() >= out0[S], "spmv_sliced: ypart must hold every compact partial");
+    TORCH_CHECK(x.numel() < (int64_t(1) << 30), "spmv_sliced: x must be < 2^30 elements (32-bit buffer offsets)");
     TORCH_CHECK(m[S] >= 0 && m[2 * S] <= items.size(0) && extra.numel() >= items.size(0), "spmv_sliced: items/extra shape");
     TORCH_CHECK(fix.dim() == 2 && fix.size(1) == 2, "spmv_sliced: fix [k, 2]");
     for (int64_t k = 0; k < S; ++k)
-        TORCH_CHECK(m[k] >= 0 && m[k] <= col.numel() && m[S + k] <= m[S + k + 1], "spmv_sliced: meta");
+        TORCH_CHECK(m[k] >= 0 && m[k] <= col.numel() && m[S + k] <= m[S + k + 1] && out0[k] <= out0[k + 1],
+                    "spmv_sliced: meta");
     const at::DeviceGuard g(val.device());
     at::Tensor y;
     if (out.has_value()) {
@@ -487,8 +494,9 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
     check_rc(pcmx_spmv_sliced(reinterpret_cast<const unsigned short*>(lrow.data_ptr<int16_t>()), col.data_ptr<int>(),
                               val.data_ptr<float>(), x.data_ptr<float>(), ypart.data_ptr<float>(), extra.data_ptr<float>(),
                               y.data_ptr<float>(), (int)n_rows, (int)x.numel(), (int)S, (const long long*)m,
-                              (const long long*)m + S, items.data_ptr(), fix.data_ptr(), (int)fix.size(0), (int)mode,
-                              cur_stream(val)),
+                              (const long long*)m + S, (const long long*)out0, items.data_ptr(),
+                              reinterpret_cast<const unsigned*>(row_mask.data_ptr<int>()), chunk_base.data_ptr<int>(),
+                              fix.data_ptr(), (int)fix.size(0), (int)mode, cur_stream(val)),
              "spmv_sliced");
     return y;
 }
@@ -533,13 +541,14 @@ void unpack_halo_(at::Tensor tile, const at::Tensor& buf, int64_t mask, const c1
 }
 
 // host-side CSR analysis (CPU int64 row_ptr -> int64 [n_items, 3] work items)
-at::Tensor spmv_csr_plan(const at::Tensor& row_ptr) {
+at::Tensor spmv_csr_plan(const at::Tensor& row_ptr, int64_t item_nnz) {
     TORCH_CHECK(!row_ptr.is_cuda() && row_ptr.scalar_type() == at::kLong, "spmv_csr_plan: CPU int64 row_ptr");
     auto rp = row_ptr.contiguous();
     const int n_rows = (int)rp.numel() - 1;
-    const long long k = pcmx_spmv_csr_plan((const long long*)rp.data_ptr<int64_t>(), n_rows, nullptr, 0);
+    const long long k = pcmx_spmv_csr_plan_nnz((const long long*)rp.data_ptr<int64_t>(), n_rows, nullptr, 0, (int)item_nnz);
+    TORCH_CHECK(k >= 0, "spmv_csr_plan: item_nnz must be a multiple of 64 in [64, 1024]");
     auto items = at::empty({k, 3}, rp.options());
-    pcmx_spmv_csr_plan((const long long*)rp.data_ptr<int64_t>(), n_rows, items.data_ptr(), k);
+    pcmx_spmv_csr_plan_nnz((const long long*)rp.data_ptr<int64_t>(), n_rows, items.data_ptr(), k, (int)item_nnz);
     return items;
 }
 
@@ -573,7 +582,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
-    m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None, int mode=0) -> Tensor");
+    m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor row_mask, Tensor chunk_base, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None, int mode=0) -> Tensor");
     m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x) -> Tensor");
     m.def("pack_edges(Tensor tile) -> Tensor");
     m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask, Tensor(b!)? changed=None) -> ()");
@@ -614,5 +623,6 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
 PYBIND11_MODULE(_C, mod) {
     mod.doc() = "pcmx MI355X kernels (ops live under torch.ops.pcmx)";
     mod.def("device_count", []() { return pcmx_device_count(); });
-    mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr");
+    mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr",
+            pybind11::arg("row_ptr"), pybind11::arg("item_nnz") = 1024);
 }

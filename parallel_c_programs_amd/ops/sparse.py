@@ -59,19 +59,26 @@ class SlicedCSR:
     """XCD-sliced CSR for SpMV on MI355X (csrc/kernels/spmv.hip: spmv_sliced_kernel).
 
     The columns are cut into ``n_slices`` (8 x phases) ranges of about equal nnz; slice s keeps its nonzeros
-    contiguous (slice-major copy of col/val, row order kept), the u16 row offset of every nonzero inside its
-    work item (``lrow``) and its own nnz-balanced items. The kernel deals slice s to the workgroups that share
-    one XCD, so each 4-MiB L2 only holds one slice's part of x. ``head``: the lowest-index columns holding that
+    contiguous (slice-major copy of col/val, row order kept) and its own nnz-balanced work items over the rows it
+    TOUCHES (rows with >= 1 nonzero in the slice); ``lrow`` holds, per nonzero, the offset of its row among the
+    item's touched rows. The kernel deals slice s to the workgroups that share one XCD, so each 4-MiB L2 only
+    holds one slice's part of x, and writes one compact partial per touched row (``ypart``, slice-major); the
+    combine pass sums each row's partials using ``row_mask`` (bit s: slice s touches the row) and ``chunk_base``
+    (touched rows of each slice before every 64-row chunk). ``head``: the lowest-index columns holding that
     fraction of the nonzeros (the hottest of a power-law graph) are dealt to the slices by row blocks instead,
     so every XCD keeps its own copy of them. Same product as the plain CSR kernel (fp32 sums in a different,
     fixed order). Built once per matrix on the matrix's device (torch ops; the item cuts use the host planner).
     """
 
-    def __init__(self, m: CSR, n_slices: int = 16, head: float = 0.0625, balance: float = 0.0):
+    def __init__(self, m: CSR, n_slices: int = 16, head: float = 0.0625, balance: float = 0.0, item_nnz: int = 1024):
         from .. import _C  # noqa: F401  (pybind module carries the planner)
 
         if n_slices % 8 or not 8 <= n_slices <= 32:
             raise ValueError("n_slices must be 8, 16, 24 or 32")
+        if item_nnz not in (512, 1024):
+            raise ValueError("item_nnz must be 512 or 1024 (8 or 16 nonzeros per lane)")
+        self.item_nnz = item_nnz
+        self.mode = 2 if item_nnz == 512 else 0  # kernel layout bit: items of 512 nonzeros
         dev = m.val.device
         n, S, nnz = m.n_rows, n_slices, m.nnz
         self.n_rows, self.n_cols, self.n_slices, self.nnz = n, m.n_cols, S, nnz
@@ -109,43 +116,66 @@ class SlicedCSR:
             raise ValueError("a slice holds >= 2^31 nonzeros: use more slices")
         nz0 = torch.zeros(S, dtype=torch.int64)
         nz0[1:] = slice_nnz.cumsum(0)[:-1]
-        items, fix, item0 = [], [], [0]
+        n_chunks = (n + 63) // 64
+        mask = torch.zeros(n, dtype=torch.int64, device=dev)
+        base = torch.zeros(n_chunks, S, dtype=torch.int32, device=dev)
+        items, fix, item0, out0 = [], [], [0], [0]
         self.lrow = torch.empty(nnz, dtype=torch.int16, device=dev)
         for k in range(S):
-            rp = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-            rp[1:] = counts[k].cumsum(0)
+            touched = counts[k] > 0
+            trows = torch.nonzero(touched).flatten()  # the rows slice k touches, ascending
+            tcnt = counts[k][trows]
+            mask |= touched.long() << k
+            csum = touched.int().cumsum(0, dtype=torch.int32)
+            base[1:, k] = csum[63:64 * (n_chunks - 1):64]  # touched rows before row 64c
+            rp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
+            rp[1:] = tcnt.cumsum(0)
             rpc = rp.cpu()
-            it = _C.spmv_csr_plan(rpc)
+            it = _C.spmv_csr_plan(rpc, item_nnz)  # items over the compact (touched) rows (rows <= nnz per item)
             r0, r1 = it[:, 0] & 0xFFFFFFFF, it[:, 0] >> 32
             # a later piece of a split long row: a single-row item not starting at the row's first nonzero;
             # encoded as an empty row range (row1 == row0), its sum goes to extra[] and is fixed up into y
             idx = torch.nonzero(((r1 - r0) == 1) & (it[:, 1] != rpc[r0])).flatten()
-            fix.append(torch.stack([idx + item0[-1], r0[idx]], 1))
+            fix.append(torch.stack([idx + item0[-1], trows.cpu()[r0[idx]]], 1))
             it[idx, 0] = r0[idx] | (r0[idx] << 32)
             items.append(it)
             item0.append(item0[-1] + it.shape[0])
+            out0.append(out0[-1] + trows.numel())
             nzk = int(rpc[-1])
-            if nzk:  # row offset of every nonzero inside its item (< kItemRows = 1023; 0 for single-row items)
+            if nzk:  # offset of every nonzero's row among its item's touched rows (< kItemRows = 1023)
                 itd = it.to(dev)
-                row_of = torch.repeat_interleave(torch.arange(n, device=dev), counts[k])
+                row_of = torch.repeat_interleave(torch.arange(trows.numel(), device=dev), tcnt)
                 item_of = torch.repeat_interleave(torch.arange(itd.shape[0], device=dev), itd[:, 2] - itd[:, 1])
                 off = (row_of - (itd[:, 0] & 0xFFFFFFFF)[item_of]).clamp_(min=0)
                 self.lrow[int(nz0[k]):int(nz0[k]) + nzk] = off.to(torch.int16)
                 del itd, row_of, item_of, off
+            del touched, trows, tcnt, csum, rp
         del counts
         self.items = torch.cat(items).to(dev)
         self.fix = torch.cat(fix).to(torch.int32).contiguous().to(dev)
-        self.meta = torch.cat([nz0, torch.tensor(item0, dtype=torch.int64)]).contiguous()
-        self.ypart = torch.empty(S * n, dtype=torch.float32, device=dev)
+        self.row_mask = mask.to(torch.int32).contiguous()  # bit 31 wraps into the sign: read as u32 on device
+        self.chunk_base = base.contiguous()
+        self.meta = torch.cat([nz0, torch.tensor(item0, dtype=torch.int64), torch.tensor(out0, dtype=torch.int64)])
+        self.meta = self.meta.contiguous()
+        self.ypart = torch.empty(max(1, out0[-1]), dtype=torch.float32, device=dev)
         self.extra = torch.empty(max(1, item0[-1]), dtype=torch.float32, device=dev)
 
-    def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    @property
+    def partials(self) -> int:
+        """Compact partials per product (touched (row, slice) pairs)."""
+        return int(self.meta[-1])
+
+    def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None, mode: int = 0) -> torch.Tensor:
         """y = A x; `out` (contiguous f32, >= n_rows elements) receives y in place when given."""
-        return ops().spmv_sliced(self.lrow, self.col, self.val, x, self.items, self.fix, self.meta, self.ypart,
-                                 self.extra, self.n_rows, out)
+        return ops().spmv_sliced(self.lrow, self.col, self.val, x, self.items, self.row_mask, self.chunk_base, self.fix,
+                                 self.meta, self.ypart, self.extra, self.n_rows, out, mode | self.mode)
+
+    def touched_rows(self, k: int) -> torch.Tensor:
+        """Rows slice k touches (ascending), from the row mask."""
+        return torch.nonzero((self.row_mask.long() >> k) & 1).flatten()
 
     def rows(self) -> torch.Tensor:
-        """Row of every stored nonzero, rebuilt from the items and lrow (the layout the kernel reads)."""
+        """Row of every stored nonzero, rebuilt from the items, lrow and the row mask (the layout the kernel reads)."""
         it = self.items
         r0 = it[:, 0] & 0xFFFFFFFF
         S = self.n_slices
@@ -156,14 +186,19 @@ class SlicedCSR:
             itk = it[a:b]
             item_of = torch.repeat_interleave(torch.arange(b - a, device=it.device), itk[:, 2] - itk[:, 1])
             nzk = int(item_of.numel())
-            out[base:base + nzk] = r0[a:b][item_of] + self.lrow[base:base + nzk].long()
+            trows = self.touched_rows(k).to(it.device)
+            out[base:base + nzk] = trows[r0[a:b][item_of] + self.lrow[base:base + nzk].long()]
         return out
 
     def reference(self, x: torch.Tensor) -> torch.Tensor:
-        """fp64 product straight from the sliced layout (tests the layout on any device)."""
-        y = torch.zeros(self.n_rows, dtype=torch.float64, device=x.device)
-        y.index_add_(0, self.rows().to(x.device), self.val.double().to(x.device) * x.double()[self.col.long()])
-        return y
+        """fp64 product straight from the sliced layout (tests the layout on any device). Row sums are segment
+        reductions over the row-sorted products (an fp64 index_add_ serialises on a power-law graph's hot rows:
+        ~10 s at 1e8 nnz on the GPU)."""
+        rows = self.rows().to(x.device)
+        order = torch.sort(rows, stable=True).indices
+        prod = (self.val.double().to(x.device) * x.double()[self.col.long().to(x.device)])[order]
+        lengths = torch.bincount(rows, minlength=self.n_rows)
+        return torch.segment_reduce(prod, "sum", lengths=lengths, unsafe=True)
 
 
 class _CSRStruct(ctypes.Structure):

@@ -49,7 +49,7 @@ def padded_index(cuts: list[int], chunks: int, L: int, device="cpu") -> torch.Te
 
 class DistributedSpMV:
     def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
-                 head: float = 0.0625, balance: float = 0.0, chunks: int | None = None):
+                 head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 1024):
         W, dev = ctx.world, ctx.device
         self.ctx, self.cuts = ctx, cuts
         self.n = row_ptr.numel() - 1
@@ -72,7 +72,7 @@ class DistributedSpMV:
             a, b = min(c * self.L, self.rows), min((c + 1) * self.L, self.rows)
             part = m.row_block(a, b)
             if dev.type == "cuda":
-                part = SlicedCSR(part, slices, head, balance) if self.sliced else part.plan()
+                part = SlicedCSR(part, slices, head, balance, item_nnz) if self.sliced else part.plan()
             self.parts.append((a, b, part))
         del m, col
         self.send = torch.zeros(C, self.L, dtype=torch.float32, device=dev)  # tails of short chunks stay 0
@@ -81,11 +81,11 @@ class DistributedSpMV:
     @staticmethod
     def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
                  slices: int = 0, head: float = 0.0625, balance: float = 0.0,
-                 chunks: int | None = None) -> "DistributedSpMV":
+                 chunks: int | None = None, item_nnz: int = 1024) -> "DistributedSpMV":
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)
-        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks)
+        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz)
 
     @property
     def local_nnz(self) -> int:

@@ -39,11 +39,64 @@ def test_sliced_items_split_long_rows_and_cover_every_row():
     it = s.items
     r0, r1 = it[:, 0] & 0xFFFFFFFF, it[:, 0] >> 32
     assert bool(((it[:, 2] - it[:, 1]) <= 1024).all()) and bool(((r1 - r0) <= 1023).all())
-    for k in range(8):  # every slice's items tile [0, n_rows) (later pieces are empty ranges)
+    for k in range(8):  # every slice's items tile its touched rows [0, T_k) (later pieces are empty ranges)
         a, b = int(s.meta[8 + k]), int(s.meta[9 + k])
-        covered = torch.zeros(n, dtype=torch.int64)
+        tk = int(s.meta[17 + k + 1] - s.meta[17 + k])
+        assert tk == s.touched_rows(k).numel()
+        covered = torch.zeros(tk, dtype=torch.int64)
         for i in range(a, b):
             covered[int(r0[i]):int(r1[i])] += 1
         assert bool((covered == 1).all())
     x = torch.rand(3000, generator=g)
     assert torch.allclose(s.reference(x), _fp64(m, x), rtol=0, atol=1e-9)
+
+
+def _emulate(s, x):
+    """fp64 model of what the gfx950 kernels compute from the layout: per-item compact partials (later pieces of
+    long rows into extra[]), the mask/chunk-base combine, the fix-up."""
+    S, it = s.n_slices, s.items
+    out0 = s.meta[2 * S + 1:]
+    comp = torch.zeros(int(out0[-1]), dtype=torch.float64)
+    extra = torch.zeros(it.shape[0], dtype=torch.float64)
+    r0, r1 = it[:, 0] & 0xFFFFFFFF, it[:, 0] >> 32
+    for k in range(S):
+        a, b, base = int(s.meta[S + k]), int(s.meta[S + k + 1]), int(s.meta[k])
+        item_of = torch.repeat_interleave(torch.arange(a, b), it[a:b, 2] - it[a:b, 1])
+        sl = slice(base, base + item_of.numel())
+        prod = s.val[sl].double() * x.double()[s.col[sl].long()]
+        later = r1[item_of] == r0[item_of]
+        comp.index_add_(0, int(out0[k]) + (r0[item_of] + s.lrow[sl].long())[~later], prod[~later])
+        extra.index_add_(0, item_of[later], prod[later])
+    y = torch.zeros(s.n_rows, dtype=torch.float64)
+    mask = s.row_mask.long() & 0xFFFFFFFF
+    for k in range(S):
+        bit = (mask >> k) & 1
+        rank = torch.cumsum(bit, 0) - bit  # touched rows before each row
+        assert torch.equal(s.chunk_base[:, k].long(), rank[::64])  # the kernel's per-chunk base
+        on = bit.bool()
+        y[on] += comp[int(out0[k]) + rank[on]]
+    y.index_add_(0, s.fix[:, 1].long(), extra[s.fix[:, 0].long()])
+    return y
+
+
+@pytest.mark.parametrize("slices,head", [(8, 0.0), (16, 0.0625), (32, 0.2)])
+def test_sliced_compact_partials_and_combine_model(slices, head):
+    """The compact-partial layout (touched rows only) + row mask + chunk bases reproduce the product."""
+    m = ops.powerlaw_csr(30000, 400_000, alpha=2.2, seed=4)
+    s = ops.SlicedCSR(m, slices, head=head)
+    assert s.partials < slices * m.n_rows  # only touched (row, slice) pairs get a partial
+    x = torch.rand(m.n_cols)
+    assert torch.allclose(_emulate(s, x), _fp64(m, x), rtol=0, atol=1e-9)
+
+
+def test_sliced_compact_long_rows_model():
+    n = 300
+    lens = torch.tensor([0, 30000, 2, 0, 5000] + [3] * (n - 5))
+    rp = torch.zeros(n + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(lens, 0)
+    g = torch.Generator().manual_seed(2)
+    col = torch.randint(0, 3000, (int(rp[-1]),), dtype=torch.int32, generator=g)
+    m = ops.CSR(rp, col, torch.rand(int(rp[-1]), generator=g), 3000)
+    s = ops.SlicedCSR(m, 8, head=0.05)
+    x = torch.rand(3000, generator=g)
+    assert torch.allclose(_emulate(s, x), _fp64(m, x), rtol=0, atol=1e-9)
