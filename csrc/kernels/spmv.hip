@@ -40,7 +40,7 @@ constexpr int kItemRows = 1023;           // rows per multi-row item (bounds the
 constexpr int kRpPerLane = (kItemRows + 1 + 63) / 64;  // row pointers per lane (kItemRows + 1 per item)
 constexpr int kPerLane = kItemNnz / kWave;  // nonzeros per lane
 constexpr int kMaxSlices = PCMX_SPMV_MAX_SLICES;
-constexpr int kPersistBlocks = 2;  // sliced kernel: resident blocks (of 4 waves) per CU (170 VGPRs -> 2 waves/SIMD)
+constexpr int kPersistBlocks = 3;  // sliced kernel: resident blocks (of 4 waves) per CU (161 VGPRs -> 3 waves/SIMD)
 
 // ------------------------------------------------------------------------------------------ plain CSR
 // One wave per item. All column/value loads of the item AND its row pointers are issued up front, then all
@@ -172,6 +172,33 @@ struct SlicedCtx {
 // One pipeline step: gathers of the current item, stream loads of the next item, then the current item's
 // LDS scatter and stores. Called alternately with the two register sets swapped (a register copy would make
 // the compiler wait for the prefetch).
+// One step of a segmented inclusive scan over the wave (Hillis-Steele on DPP): (v, f) = (running sum, "a segment
+// starts at or after the combined range"); a lane without a source in this pattern keeps its value (old = 0).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void seg_scan_step(float& v, int& f) {
+    const float vp = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, kRowMask, 0xf, false));
+    const int fp = __builtin_amdgcn_update_dpp(0, f, kCtrl, kRowMask, 0xf, false);
+    v = f ? v : v + vp;
+    f |= fp;
+}
+__device__ __forceinline__ void seg_scan_wave(float& v, int& f) {
+    seg_scan_step<0x111, 0xf>(v, f);  // row_shr:1 .. row_shr:8: within rows of 16 lanes
+    seg_scan_step<0x112, 0xf>(v, f);
+    seg_scan_step<0x114, 0xf>(v, f);
+    seg_scan_step<0x118, 0xf>(v, f);
+    seg_scan_step<0x142, 0xa>(v, f);  // row_bcast:15 into rows 1 and 3
+    seg_scan_step<0x143, 0xc>(v, f);  // row_bcast:31 into rows 2 and 3
+}
+
+// One pipeline step: gathers of the current item, stream loads of the next item, then the current item's row
+// sums and stores. Called alternately with the two register sets swapped (a register copy would make the
+// compiler wait for the prefetch).
+// kMode bit 2 (production): row sums by a segmented DPP scan per 64-element stripe — an item's nonzeros are
+// sorted by row, so element i = j * 64 + lane continues the row of element i - 1 unless its lrow differs; the
+// lane holding a row's LAST element stores the row sum straight to the compact partials (a row running past a
+// stripe carries its partial sum into the next stripe). No LDS, no barriers. Otherwise: LDS scatter (ds_add_f32
+// into the item's rows, then one store per row) — measured LDS-issue bound (34% of wave cycles in
+// SQ_WAIT_INST_LDS, profiles/r2_spmv).
 template <int kMode, int kPL>
 __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, const Item& cur, const StreamRegs<kPL>& q,
                                             Item& nitem, StreamRegs<kPL>& nq) {
@@ -187,42 +214,76 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
     load_item_stream(k.col, k.val, k.lrow, nitem, nq, lane);  // (a harmless re-read of the last item at the end)
     const int n = (int)(cur.nz1 - cur.nz0);
     const int nrows = cur.row1 - cur.row0;
-    float* dst;
-    int nstore;
-    if (nrows <= 1) {  // whole short row or a piece of a long row (later piece: row1 == row0 -> extra[it])
-        float acc = 0.f;
+    if constexpr ((kMode & 4) != 0) {
+        if (nrows <= 1) {  // whole short row or a piece of a long row (later piece: row1 == row0 -> extra[it])
+            float acc = 0.f;
 #pragma unroll
-        for (int j = 0; j < kPL; ++j) acc += q.v[j] * g[j];
-        acc = pcmx::wave_reduce<float, 0>(acc);
-        if (lane == 0) k.yw[0] = acc;
-        dst = nrows == 1 ? k.yp + cur.row0 : k.extra + it;
-        nstore = 1;
+            for (int j = 0; j < kPL; ++j) acc += q.v[j] * g[j];
+            acc = pcmx::wave_reduce<float, 0>(acc);
+            const auto r1 = rsrc(nrows == 1 ? k.yp + cur.row0 : k.extra + it, 4u);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc), r1, lane == 0 ? 0u : 0x80000000u, 0, 2);
+        } else {
+            const auto ry = rsrc(k.yp + cur.row0, (unsigned)nrows * 4);
+            float carry = 0.f;
+            int rprev = -1;  // row of the element before this stripe (wave-uniform)
+#pragma unroll
+            for (int j = 0; j < kPL; ++j) {
+                const bool valid = j * kWave + lane < n;
+                const int r = valid ? (int)q.r[j] : 0x10000;  // past the item: one trailing non-row segment
+                float v = valid ? q.v[j] * g[j] : 0.f;
+                const int rp = __builtin_amdgcn_update_dpp(rprev, r, 0x138, 0xf, 0xf, false);  // wave_shr:1
+                int f = r != rp;
+                seg_scan_wave(v, f);
+                v = f ? v : v + carry;  // lanes still in the row carried in from the previous stripe
+                const int rnext0 = (j + 1 < kPL && (j + 1) * kWave < n)
+                                       ? __builtin_amdgcn_readlane((int)q.r[j + 1 < kPL ? j + 1 : j], 0)
+                                       : 0x10000;
+                const int rn = __builtin_amdgcn_update_dpp(rnext0, r, 0x130, 0xf, 0xf, false);  // wave_shl:1
+                const bool tail = valid && r != rn;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, tail ? (unsigned)r * 4u : 0x80000000u, 0, 2);
+                const int r63 = __builtin_amdgcn_readlane(r, 63);
+                carry = r63 == rnext0 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)) : 0.f;
+                rprev = r63;
+            }
+        }
     } else {
+        float* dst;
+        int nstore;
+        if (nrows <= 1) {
+            float acc = 0.f;
 #pragma unroll
-        for (int j = 0; j < kPL; ++j) {  // compact rows: every row of an item holds >= 1 of its <= 64 kPL nonzeros
-            const int i = j * kWave + lane;
-            if (i < nrows) k.yw[i] = 0.f;
+            for (int j = 0; j < kPL; ++j) acc += q.v[j] * g[j];
+            acc = pcmx::wave_reduce<float, 0>(acc);
+            if (lane == 0) k.yw[0] = acc;
+            dst = nrows == 1 ? k.yp + cur.row0 : k.extra + it;
+            nstore = 1;
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPL; ++j) {  // compact rows: every row of an item holds >= 1 of its <= 64 kPL nonzeros
+                const int i = j * kWave + lane;
+                if (i < nrows) k.yw[i] = 0.f;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < kPL; ++j) {
+                const int i = j * kWave + lane;
+                if (i < n) atomicAdd(&k.yw[q.r[j]], q.v[j] * g[j]);
+            }
+            dst = k.yp + cur.row0;
+            nstore = nrows;
         }
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const auto ry = rsrc(dst, (unsigned)nstore * 4);
 #pragma unroll
         for (int j = 0; j < kPL; ++j) {
             const int i = j * kWave + lane;
-            if (i < n) atomicAdd(&k.yw[q.r[j]], q.v[j] * g[j]);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(k.yw[i]), ry, i * 4, 0, 2);
         }
-        dst = k.yp + cur.row0;
-        nstore = nrows;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // next item's zeroing after these LDS reads
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const auto ry = rsrc(dst, (unsigned)nstore * 4);
-#pragma unroll
-    for (int j = 0; j < kPL; ++j) {
-        const int i = j * kWave + lane;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(k.yw[i]), ry, i * 4, 0, 2);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // next item's zeroing after these LDS reads
     it = nxt;
     return more;
 }
@@ -405,12 +466,19 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         const unsigned nb = (unsigned)(bp * n_slices);
         const Item* it = reinterpret_cast<const Item*>(items);
         const dim3 blk(kWavesPerBlock * kWave);
-        switch (mode & 3) {  // bit 0: skip the x gathers (lab), bit 1: items of 512 nonzeros (8 per lane)
-            case 0: spmv_sliced_kernel<0, 16><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
-            case 1: spmv_sliced_kernel<1, 16><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
-            case 2: spmv_sliced_kernel<0, 8><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
-            default: spmv_sliced_kernel<1, 8><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp); break;
+        // bit 0: skip the x gathers (lab), bit 1: items of 512 nonzeros (8 per lane), bit 2: LDS row sums (lab)
+#define PCMX_SLICED(M, PL) spmv_sliced_kernel<M, PL><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp)
+        switch (mode & 7) {
+            case 0: PCMX_SLICED(4, 16); break;
+            case 1: PCMX_SLICED(5, 16); break;
+            case 2: PCMX_SLICED(4, 8); break;
+            case 3: PCMX_SLICED(5, 8); break;
+            case 4: PCMX_SLICED(0, 16); break;
+            case 5: PCMX_SLICED(1, 16); break;
+            case 6: PCMX_SLICED(0, 8); break;
+            default: PCMX_SLICED(1, 8); break;
         }
+#undef PCMX_SLICED
     }
     const unsigned cb = (unsigned)((n_rows + 2047) / 2048) * 8;  // 4 waves of 64 rows per block, 8k blocks
     switch (n_slices) {

@@ -37,7 +37,8 @@ def bench(meta, reps=20):
 
 for mode, what in [(1 | 2 << 8, "no x gathers"), (1 << 8, "1 block/CU"), (2 << 8, "2 blocks/CU"),
                    (3 << 8, "3 blocks/CU"), (4 << 8, "4 blocks/CU"), (5 << 8, "5 blocks/CU"), (6 << 8, "6 blocks/CU"),
-                   (1 | 5 << 8, "no x gathers, 5 blocks/CU")]:
+                   (1 | 5 << 8, "no x gathers, 5 blocks/CU"), (4 | 2 << 8, "LDS row sums, 2 blocks/CU"),
+                   (4 | 5 << 8, "LDS row sums, 5 blocks/CU")]:
     MODE = mode
     print(f"mode {mode} ({what}): {bench(s.meta):.3f} ms")
 MODE = 0
