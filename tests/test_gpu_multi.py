@@ -96,3 +96,57 @@ def test_volume3d_torchrun_rccl(gpu, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert out["region_voxels"] == 2197899 and out["image_sum"] == 127183
+
+
+@pytest.mark.parametrize("world,fuse", [(2, 6), (8, 6), (8, 4), (4, 8)])
+def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse):
+    """Every rank of a `world`-rank row-slab stencil on one GPU: halos copied slab to slab (what the grouped RCCL
+    send/recv moves), then the overlapped launch split of StencilSlab.step (interior rows, then the two boundary
+    ranges) — bit-identical to the single-domain oracle. At world 8 a slab of a 2048-row grid is a short range,
+    so this runs the v2 kernel's 32-rows-per-wave launch with interior and edge waves."""
+    from parallel_c_programs_amd.parallel.dist import Context
+    from parallel_c_programs_amd.parallel.stencil import StencilSlab, reference_run
+
+    n, cols, steps = 2048, 1000, 2 * fuse
+    slabs = [StencilSlab(Context(rank=r, world=world, device=gpu), n, cols, fuse=fuse) for r in range(world)]
+    for _ in range(steps // fuse):
+        for r, s in enumerate(slabs):  # halo exchange: T rows from each neighbour
+            h = s.halo
+            if r > 0:
+                s.u[0:h].copy_(slabs[r - 1].u[slabs[r - 1].rows:slabs[r - 1].rows + h])
+            if r < world - 1:
+                s.u[s.rows + h:s.rows + 2 * h].copy_(slabs[r + 1].u[h:2 * h])
+        for s in slabs:
+            d = s.halo
+            s._update(s.u, s.v, (d, s.rows - d))
+            s._update(s.u, s.v, (0, d))
+            s._update(s.u, s.v, (s.rows - d, s.rows))
+        for s in slabs:
+            s.u, s.v = s.v, s.u
+    got = torch.cat([s.interior() for s in slabs]).cpu()
+    ref = reference_run(n, steps, cols, device=gpu).cpu()
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_spmv_ranks_emulated_on_one_gpu(gpu, world):
+    """Every rank's local product of the distributed power-law SpMV on one GPU: nnz-balanced row blocks, columns
+    renumbered into the padded all-gather layout, 4 pipeline chunks per rank, XCD-sliced compact-partial kernel
+    — each chunk checked against the fp64 product of the same rows."""
+    from parallel_c_programs_amd.parallel.dist import Context
+    from parallel_c_programs_amd.parallel.spmv import DistributedSpMV
+
+    for r in sorted({0, world // 2, world - 1}):
+        d = DistributedSpMV.powerlaw(Context(rank=r, world=world, device=gpu), 300_000, 3_000_000, slices=16, chunks=4)
+        assert d.chunks == 4 and d.n_pad >= d.n
+        xp = torch.rand(d.n_pad, device=gpu)
+        got = []
+        for c, (a, b, part) in enumerate(d.parts):
+            if b > a:
+                d._mul(part, xp, d.send[c, :b - a])
+                got.append(d.send[c, :b - a].double())
+        got = torch.cat(got)
+        ref = d.reference_local(xp)
+        assert got.shape == ref.shape == (d.rows,)
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        assert err < 1e-5, (r, err)
