@@ -461,16 +461,17 @@ extern "C" int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols
     if (halo < steps && ((r0 < steps && !top_global) || (r1 > rows - steps && !bot_global))) return -1;
     const unsigned short* ui = (const unsigned short*)u;
     unsigned short* uo = (unsigned short*)out;
-    // T = 2 is HBM-bound: the v1 kernel. T >= 3 is VALU-bound: v2 with 48 rows per wave, or 32 on short ranges
-    // (a rank's slab at N = 8 is 2048 rows: shorter waves give 2x the waves at 2T/RPW more redundant rows;
-    // measured 2.6 vs 2.0 TGLUP/s at T = 6 on a 2048 x 16384 slab, scripts/stencil_lab.hip)
-    const bool short_range = r1 - r0 < 8192;
+    // T = 2 is HBM-bound: the v1 kernel. T >= 3 is VALU-bound: v2 with 48 rows per wave, or 24 on ranges under
+    // 6144 rows (a rank's slab at N = 4 / 8 is 4096 / 2048 rows: shorter waves give 2x the waves at 2T/RPW more
+    // redundant rows; T = 6, 16384 columns, scripts/stencil_lab.hip: 2048 rows 2.0 -> 2.97, 4096 rows 3.1 -> 4.0
+    // TGLUP/s; at 8192 rows 48 and 32 tie and 24 is 4% slower)
+    const bool short_range = r1 - r0 < 6144;
     auto grid_for = [&](int rpw) {
         return dim3((cols + kOutCols - 1) / kOutCols, (rows + kWaves * rpw - 1) / (kWaves * rpw));
     };
 #define PCMX_STENCIL_V2(T)                                                                                          \
     if (short_range)                                                                                                \
-        stencil5xT2_kernel<T, 6, 32><<<grid_for(32), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,     \
+        stencil5xT2_kernel<T, 6, 24><<<grid_for(24), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,     \
                                                                           global_row0, global_rows, k);             \
     else                                                                                                            \
         stencil5xT2_kernel<T, 6, 48><<<grid_for(48), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,     \

@@ -68,6 +68,8 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
     same("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
     same("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
     same("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
+    same("v2rpw24", [&] { launch<2, T, 24>(u, o, n, ld, halo, k); });
+    same("v2rpw16", [&] { launch<2, T, 16>(u, o, n, ld, halo, k); });
     for (int rnd = 0; rnd < 2; ++rnd) {
         time("v1", [&] { launch<1, T, 64>(u, o, n, ld, halo, k); });
         time("v2", [&] { launch<2, T, 64>(u, o, n, ld, halo, k); });
@@ -76,6 +78,8 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
         time("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
         time("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
         time("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
+        time("v2rpw24", [&] { launch<2, T, 24>(u, o, n, ld, halo, k); });
+        time("v2rpw16", [&] { launch<2, T, 16>(u, o, n, ld, halo, k); });
     }
     return 0;
 }

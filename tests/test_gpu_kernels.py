@@ -219,8 +219,8 @@ def test_stencil_row_range_split(gpu):
 @pytest.mark.parametrize("shape", [(256, 512), (1000, 1000), (515, 4096), (9, 2000), (8300, 1000)])
 def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
     """Temporal-blocking kernel == `steps` single steps (bf16 bits); random data so every lane/strip-overlap
-    path counts; column counts that are not multiples of the 496-column output strip; >= 8192 rows takes the
-    48-rows-per-wave launch, fewer the 32-row one (interior waves: v2 fast path, edge waves: v1 pipeline)."""
+    path counts; column counts that are not multiples of the 496-column output strip; >= 6144 rows takes the
+    48-rows-per-wave launch, fewer the 24-row one (interior waves: v2 fast path, edge waves: v1 pipeline)."""
     rows, cols = shape
     g = torch.Generator().manual_seed(rows + steps)
     u = (torch.rand(rows + 2, cols, generator=g) * 4 - 2).to(torch.bfloat16)

@@ -103,7 +103,7 @@ def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse):
     """Every rank of a `world`-rank row-slab stencil on one GPU: halos copied slab to slab (what the grouped RCCL
     send/recv moves), then the overlapped launch split of StencilSlab.step (interior rows, then the two boundary
     ranges) — bit-identical to the single-domain oracle. At world 8 a slab of a 2048-row grid is a short range,
-    so this runs the v2 kernel's 32-rows-per-wave launch with interior and edge waves."""
+    so this runs the v2 kernel's 24-rows-per-wave launch with interior and edge waves."""
     from parallel_c_programs_amd.parallel.dist import Context
     from parallel_c_programs_amd.parallel.stencil import StencilSlab, reference_run
 
