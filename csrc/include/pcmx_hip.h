@@ -152,6 +152,11 @@ int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, int ld, int
  * halo >= steps. pcmx_stencil5x2_bf16 = steps 2. */
 int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0, int r1,
                          long long global_row0, long long global_rows, float k, hipStream_t s);
+/* the same over two row spans [r0a, r1a) and [r0b, r1b) (disjoint, either may be empty) in ONE launch: the
+ * distributed step updates both rank-edge bands with one kernel once the halo rows have arrived */
+int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0a,
+                               int r1a, int r0b, int r1b, long long global_row0, long long global_rows, float k,
+                               hipStream_t s);
 int pcmx_stencil5x2_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int r0, int r1,
                          long long global_row0, long long global_rows, float k, hipStream_t s);
 

@@ -224,16 +224,29 @@ __device__ __forceinline__ u32x4 update_pairs(const Row8& n, const Row8& c, cons
 // fully unrolled prefetch loop turns into compile-time register names (no window-shifting moves). Rings hold
 // PACKED bf16 rows (4 VGPRs each): the kernel is latency-bound, so unpacking a row per use (ALU) is cheaper
 // than the occupancy lost to 8-VGPR float rows (T=4: 187 -> ~110 VGPRs, 2 -> 4 waves per SIMD).
+// Row spans of one launch: blocks [0, nby_a) of grid.y cover local rows [a0, a1), the rest [b0, b1) (empty when
+// b0 == b1). A distributed step updates both rank-edge row bands in ONE launch after the halo arrives, and a
+// launch covers only its rows (no grid over the whole slab with idle blocks).
+struct RowSpans {
+    int a0, a1, b0, b1, nby_a;
+};
+// The rows [rs, re) of this wave (rs >= re: none).
+template <int RPW>
+__device__ __forceinline__ void wave_rows(const RowSpans& sp, int wave, int& rs, int& re) {
+    int by = (int)blockIdx.y, base = sp.a0, lim = sp.a1;
+    if (by >= sp.nby_a) by -= sp.nby_a, base = sp.b0, lim = sp.b1;
+    rs = base + by * (kWaves * RPW) + wave * RPW;
+    re = min(lim, rs + RPW);
+}
+
 template <int T, int kAhead, int RPW = kRowsPerWave>
 __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict__ u, unsigned short* __restrict__ out,
-                                                int rows, int cols, int ld, int halo, int r0, int r1, long long grow0,
+                                                int rows, int cols, int ld, int halo, int rs, int re, long long grow0,
                                                 long long grows, float k) {
     static_assert(T >= 1 && T <= 8, "lanes 1..62 stay exact for at most 8 levels");
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const int c0 = (int)blockIdx.x * kOutCols - 8 + lane * 8;  // first column of this lane (may be < 0)
-    const int rs = max(r0, (int)(blockIdx.y * (kWaves * RPW) + wave * RPW));
-    const int re = min(r1, (int)(blockIdx.y * (kWaves * RPW) + (wave + 1) * RPW));
     if (rs >= re) return;
     const bool in_grid = c0 >= 0 && c0 + 8 <= cols;  // cols % 8 == 0
     const bool store_lane = in_grid && lane >= 1 && lane <= 62;
@@ -288,9 +301,11 @@ __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict
 template <int T, int kAhead, int RPW = kRowsPerWave>
 __global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned short* __restrict__ u,
                                                                  unsigned short* __restrict__ out, int rows, int cols,
-                                                                 int ld, int halo, int r0, int r1, long long grow0,
+                                                                 int ld, int halo, RowSpans sp, long long grow0,
                                                                  long long grows, float k) {
-    stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, r0, r1, grow0, grows, k);
+    int rs, re;
+    wave_rows<RPW>(sp, (int)threadIdx.x >> 6, rs, re);
+    stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
 }
 
 // ---- v2: the same T-level row pipeline with ~30% fewer VALU ops per level (the kernel is VALU-issue bound):
@@ -398,15 +413,15 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
 template <int T, int kAhead, int RPW = kRowsPerWave>
 __global__ __launch_bounds__(kWaves * 64) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
                                                                   unsigned short* __restrict__ out, int rows, int cols,
-                                                                  int ld, int halo, int r0, int r1, long long grow0,
+                                                                  int ld, int halo, RowSpans sp, long long grow0,
                                                                   long long grows, float k) {
     static_assert(T >= 1 && T <= 8, "lanes 1..62 stay exact for at most 8 levels");
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int c0 = (int)blockIdx.x * kOutCols - 8 + lane * 8;  // first column of this lane (may be < 0)
-    const int rs = max(r0, (int)(blockIdx.y * (kWaves * RPW)) + wave * RPW);
-    const int re = min(r1, (int)(blockIdx.y * (kWaves * RPW)) + (wave + 1) * RPW);
+    int rs, re;
+    wave_rows<RPW>(sp, wave, rs, re);
     if (rs >= re) return;
     const bool in_grid = c0 >= 0 && c0 + 8 <= cols;  // cols % 8 == 0
     const bool store_lane = in_grid && lane >= 1 && lane <= 62;
@@ -426,7 +441,7 @@ __global__ __launch_bounds__(kWaves * 64) void stencil5xT2_kernel(const unsigned
     const bool edge_rows = (g0 <= 0 && 0 <= g1) || (g0 <= grows - 1 && grows - 1 <= g1);
     const bool slow = edge_rows || __builtin_amdgcn_ballot_w64(fix0 || fix7) != 0;
     if (slow)  // a few waves per grid: the v1 pipeline (per-column selects, per-row Dirichlet test; same results)
-        stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, r0, r1, grow0, grows, k);
+        stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
     else
         pipeline_v2<T, kAhead>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
 }
@@ -447,40 +462,59 @@ extern "C" int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, 
     return (int)hipGetLastError();
 }
 
-// T fused updates over local rows [r0, r1) of a slab with `halo` rows above and below (T = 2, 3, 4, 6, 8).
-extern "C" int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0,
-                                    int r1, long long global_row0, long long global_rows, float k, hipStream_t s) {
+namespace {
+// the halo rule of one row range: rows within `steps` of a non-global slab edge read `steps` halo rows
+bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row0, long long global_rows) {
+    const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
+    return halo >= steps || r0 >= r1 || !((r0 < steps && !top_global) || (r1 > rows - steps && !bot_global));
+}
+}  // namespace
+
+// T fused updates over local rows [r0a, r1a) and [r0b, r1b) (either may be empty) of a slab with `halo` rows
+// above and below (T = 2, 3, 4, 6, 8), in one launch.
+extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, int cols, int ld, int halo, int steps,
+                                          int r0a, int r1a, int r0b, int r1b, long long global_row0,
+                                          long long global_rows, float k, hipStream_t s) {
     if (rows <= 0 || cols <= 0 || ld < cols || (ld & 7) || (cols & 7) || halo < 1 || steps < 1 ||
         (((uintptr_t)u | (uintptr_t)out) & 15))
         return -1;
-    r0 = max(r0, 0);
-    r1 = min(r1, rows);
-    if (r0 >= r1) return 0;
-    // rows that read `steps` rows beyond the local range need that deep a halo unless the side is a global edge
-    const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
-    if (halo < steps && ((r0 < steps && !top_global) || (r1 > rows - steps && !bot_global))) return -1;
+    r0a = max(r0a, 0), r1a = min(r1a, rows), r0b = max(r0b, 0), r1b = min(r1b, rows);
+    if (r0a >= r1a) r0a = r1a = 0;
+    if (r0b >= r1b) r0b = r1b = 0;
+    if (r1a == 0 && r1b == 0) return 0;
+    if (r1a > r0b && r1b > r0a) return -1;  // overlapping spans would race (two waves storing one row)
+    if (!halo_ok(rows, halo, steps, r0a, r1a, global_row0, global_rows) ||
+        !halo_ok(rows, halo, steps, r0b, r1b, global_row0, global_rows))
+        return -1;
     const unsigned short* ui = (const unsigned short*)u;
     unsigned short* uo = (unsigned short*)out;
     // T = 2 is HBM-bound: the v1 kernel. T >= 3 is VALU-bound: v2 with 48 rows per wave, or 24 on ranges under
     // 6144 rows (a rank's slab at N = 4 / 8 is 4096 / 2048 rows: shorter waves give 2x the waves at 2T/RPW more
     // redundant rows; T = 6, 16384 columns, scripts/stencil_lab.hip: 2048 rows 2.0 -> 2.97, 4096 rows 3.1 -> 4.0
     // TGLUP/s; at 8192 rows 48 and 32 tie and 24 is 4% slower)
-    const bool short_range = r1 - r0 < 6144;
-    auto grid_for = [&](int rpw) {
-        return dim3((cols + kOutCols - 1) / kOutCols, (rows + kWaves * rpw - 1) / (kWaves * rpw));
+    const bool short_range = (r1a - r0a) + (r1b - r0b) < 6144;
+    auto launch_dims = [&](int rpw, RowSpans& sp) {
+        const int per = kWaves * rpw;
+        sp = RowSpans{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per};
+        return dim3((cols + kOutCols - 1) / kOutCols, sp.nby_a + (r1b - r0b + per - 1) / per);
     };
+    RowSpans sp;
 #define PCMX_STENCIL_V2(T)                                                                                          \
-    if (short_range)                                                                                                \
-        stencil5xT2_kernel<T, 6, 24><<<grid_for(24), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,     \
-                                                                          global_row0, global_rows, k);             \
-    else                                                                                                            \
-        stencil5xT2_kernel<T, 6, 48><<<grid_for(48), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,     \
-                                                                          global_row0, global_rows, k);
+    if (short_range) {                                                                                              \
+        const dim3 g = launch_dims(24, sp);                                                                         \
+        stencil5xT2_kernel<T, 6, 24><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,       \
+                                                               global_rows, k);                                     \
+    } else {                                                                                                        \
+        const dim3 g = launch_dims(48, sp);                                                                         \
+        stencil5xT2_kernel<T, 6, 48><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,       \
+                                                               global_rows, k);                                     \
+    }
     switch (steps) {
-        case 2:
-            stencil5xT_kernel<2, 6><<<grid_for(kRowsPerWave), kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, r0, r1,
-                                                                                 global_row0, global_rows, k);
+        case 2: {
+            const dim3 g = launch_dims(kRowsPerWave, sp);
+            stencil5xT_kernel<2, 6><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0, global_rows, k);
             break;
+        }
         case 3: PCMX_STENCIL_V2(3) break;
         case 4: PCMX_STENCIL_V2(4) break;
         case 6: PCMX_STENCIL_V2(6) break;
@@ -489,6 +523,12 @@ extern "C" int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols
     }
 #undef PCMX_STENCIL_V2
     return (int)hipGetLastError();
+}
+
+// T fused updates over local rows [r0, r1) of a slab with `halo` rows above and below (T = 2, 3, 4, 6, 8).
+extern "C" int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0,
+                                    int r1, long long global_row0, long long global_rows, float k, hipStream_t s) {
+    return pcmx_stencil5xT_bf16_spans(u, out, rows, cols, ld, halo, steps, r0, r1, 0, 0, global_row0, global_rows, k, s);
 }
 
 // Two fused updates (kept as the named entry point of the fuse=2 path).

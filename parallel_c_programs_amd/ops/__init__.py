@@ -4,7 +4,7 @@ from .halo import pack_edges, unpack_halo_
 from .image import (SEED_3D, Camera, apply_region_mask, corner_seeds, create_volume, default_camera, histeq, pad1,
                     raycast, region2d, region2d_grow_padded_, region3d)
 from .sparse import CSR, SlicedCSR, banded_csr, create_vector, powerlaw_csr, spmv, spmv_banded
-from .stencil import init_grid, stencil5_reference, stencil5_step_, stencil5x2_step_, stencil5_fused_step_
+from .stencil import init_grid, stencil5_reference, stencil5_step_, stencil5x2_step_, stencil5_fused_step_, stencil5_fused_spans_
 from .vector import OP_CODES, axpy_, dot, fill_, rand_uniform_, reduce, scan, vadd, vmul
 
 __all__ = [
@@ -12,7 +12,7 @@ __all__ = [
     "vmul", "vadd", "axpy_", "dot", "reduce", "scan", "fill_", "rand_uniform_", "OP_CODES",
     "histeq", "region2d", "region2d_grow_padded_", "region3d", "corner_seeds", "pad1", "apply_region_mask",
     "create_volume", "raycast", "default_camera", "Camera", "SEED_3D",
-    "stencil5_step_", "stencil5x2_step_", "stencil5_fused_step_", "stencil5_reference", "init_grid",
+    "stencil5_step_", "stencil5x2_step_", "stencil5_fused_step_", "stencil5_fused_spans_", "stencil5_reference", "init_grid",
     "CSR", "SlicedCSR", "banded_csr", "create_vector", "powerlaw_csr", "spmv", "spmv_banded",
     "pack_edges", "unpack_halo_",
 ]

@@ -77,6 +77,24 @@ def stencil5_fused_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 
     return out
 
 
+def stencil5_fused_spans_(u: torch.Tensor, out: torch.Tensor, spans, global_row0: int = 0,
+                          global_rows: int | None = None, k: float = DEFAULT_K, halo: int = 1,
+                          steps: int = 2) -> torch.Tensor:
+    """`steps` fused updates over two disjoint local row spans [(a0, a1), (b0, b1)] in ONE kernel launch (the
+    distributed step's two rank-edge bands once the halo has arrived); same results as one call per span."""
+    (a0, a1), (b0, b1) = spans
+    if u.is_cuda:
+        rows = u.shape[0] - 2 * halo
+        global_rows = rows if global_rows is None else global_rows
+        ops().stencil5xT_spans_(u, out, int(halo), int(steps), int(a0), int(a1), int(b0), int(b1), int(global_row0),
+                                int(global_rows), float(k))
+        return out
+    for r in ((a0, a1), (b0, b1)):
+        if r[1] > r[0]:
+            stencil5_fused_step_(u, out, global_row0, global_rows, k, halo, steps, r)
+    return out
+
+
 def stencil5x2_step_(u, out, global_row0=0, global_rows=None, k=DEFAULT_K, halo=1, row_range=None):
     """Two fused updates (see stencil5_fused_step_)."""
     return stencil5_fused_step_(u, out, global_row0, global_rows, k, halo, 2, row_range)

@@ -4,16 +4,22 @@ CSR benchmark of ref 3-serial-optimization/spmv.c:170-177, 331-367).
   * partition: contiguous row blocks balanced by NNZ (not rows) — a power-law graph's heavy rows would
     otherwise pile onto one GPU. Every rank derives the same cut from the O(n) row pointer, then generates
     ONLY its own rows (bit-identical to the serial matrix), so a 1e8-nnz matrix never exists on one host.
-  * iterate (power-iteration pattern): y_local = A_local x, then every rank needs all of y as the next x.
-  * padded vector layout: each rank's row block is cut into `chunks` pieces of L rows (the block padded to
-    chunks x L); vector entry of global row g (rank r, local row l) lives at
-        p(g) = (l // L) * (world * L) + r * L + (l % L).
-    Chunk c of every rank is then ONE contiguous all_gather_into_tensor region, so RCCL writes the
-    gathered y straight into the next x: no staging copy, no index_select. The matrix's column indices are
-    renumbered into this layout once at set-up (on one rank the layout is the identity).
-  * overlap: the product runs chunk by chunk; chunk c's all-gather is issued (async, RCCL's own stream
-    waits only for chunk c's kernel) while chunk c+1 is multiplied, so only the last chunk's gather is
-    exposed: t_step ~= t_local + t_gather / chunks when t_gather <= t_local (docs/ARCHITECTURE.md, SpMV).
+  * iterate (power-iteration pattern): y_local = A_local x, then every rank needs the entries of y its rows
+    reference as the next x. Each rank's row block is cut into `chunks` pieces of L rows.
+  * exchange="ghost" (default at N > 1): each rank keeps only the x entries its nonzeros reference — its own
+    rows plus "ghost" entries owned by other ranks (63% of the 1e7 columns per rank at N=8 on the 1e8-nnz graph)
+    — in a compact local vector laid out chunk-major, owner-minor:
+        [chunk 0: ghosts of rank 0 | ... | own rows of chunk 0 | ... | ghosts of rank W-1] [chunk 1: ...] ...
+    so one chunk's product is one contiguous own segment and every (chunk, peer) ghost segment is contiguous:
+    after chunk c's product, its send entries (one index list per peer, fixed at set-up) are packed and moved
+    with one grouped RCCL send/recv per peer pair (point-to-point xGMI links, no all-gather of the whole y)
+    straight into the peers' ghost segments, while chunk c+1 is multiplied. The column indices are renumbered
+    into this layout once at set-up; on one rank it is the identity.
+  * exchange="allgather": the padded replicated layout (every rank holds all of y): entry of global row g
+    (rank r, local row l) lives at p(g) = (l // L) * (world * L) + r * L + (l % L), so chunk c of every rank is
+    ONE contiguous all_gather_into_tensor region written straight into the next x.
+  * overlap (both): chunk c's exchange is issued async (RCCL's own stream waits only for chunk c's kernel)
+    while chunk c+1 is multiplied, so only the last chunk's exchange is exposed (docs/ARCHITECTURE.md, SpMV).
 """
 from __future__ import annotations
 
@@ -49,9 +55,12 @@ def padded_index(cuts: list[int], chunks: int, L: int, device="cpu") -> torch.Te
 
 class DistributedSpMV:
     def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
-                 head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 1024):
+                 head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 1024,
+                 exchange: str = "ghost"):
         W, dev = ctx.world, ctx.device
-        self.ctx, self.cuts = ctx, cuts
+        if exchange not in ("ghost", "allgather"):
+            raise ValueError("exchange: 'ghost' or 'allgather'")
+        self.ctx, self.cuts, self.exchange = ctx, cuts, exchange if W > 1 else "ghost"
         self.n = row_ptr.numel() - 1
         self.row0, self.row1 = cuts[ctx.rank], cuts[ctx.rank + 1]
         self.rows = self.row1 - self.row0
@@ -60,11 +69,14 @@ class DistributedSpMV:
         C = max(1, min(int(C), self.block))
         self.chunks = C
         self.L = -(-self.block // C)
-        self.n_pad = C * W * self.L
-        self.colmap = padded_index(cuts, C, self.L, dev)  # identity when W == 1
         col = local.col.to(dev)
-        if W > 1:
-            col = self.colmap[col.long()].to(torch.int32)
+        if self.exchange == "allgather":
+            self.n_pad = C * W * self.L
+            self.colmap = padded_index(cuts, C, self.L, dev)  # identity when W == 1
+            if W > 1:
+                col = self.colmap[col.long()].to(torch.int32)
+        else:
+            col = self._ghost_layout(col)
         m = CSR(local.row_ptr.to(dev), col, local.val.to(dev), self.n_pad)
         self.sliced = bool(slices) and dev.type == "cuda"
         self.parts = []  # (first local row, last local row + 1, CSR or SlicedCSR)
@@ -75,34 +87,128 @@ class DistributedSpMV:
                 part = SlicedCSR(part, slices, head, balance, item_nnz) if self.sliced else part.plan()
             self.parts.append((a, b, part))
         del m, col
-        self.send = torch.zeros(C, self.L, dtype=torch.float32, device=dev)  # tails of short chunks stay 0
+        if self.exchange == "allgather":
+            self.send = torch.zeros(C, self.L, dtype=torch.float32, device=dev)  # tails of short chunks stay 0
         self.bufs = [torch.zeros(self.n_pad, dtype=torch.float32, device=dev) for _ in range(2)]
+
+    # ---- ghost layout (set-up: one exchange of the index lists)
+    def _ghost_layout(self, col: torch.Tensor) -> torch.Tensor:
+        """Builds the compact chunk-major / owner-minor layout, the per-(chunk, peer) send and receive lists, and
+        returns `col` renumbered into the layout."""
+        ctx, W, r, C, L, dev = self.ctx, self.ctx.world, self.ctx.rank, self.chunks, self.L, self.ctx.device
+        cuts_t = torch.tensor(self.cuts, dtype=torch.int64, device=dev)
+        need = torch.unique(col.long())  # ascending global ids = owner-major
+        owner = torch.searchsorted(cuts_t[1:], need, right=True)
+        need, owner = need[owner != r], owner[owner != r]  # ghosts (own rows are all kept)
+        chunk = (need - cuts_t[owner]) // L
+        # receive side: ghost (chunk c, owner q) counts; own segment of chunk c = own rows of chunk c
+        cnt = torch.bincount(chunk * W + owner, minlength=C * W).view(C, W).cpu()
+        own = [max(0, min((c + 1) * L, self.rows) - min(c * L, self.rows)) for c in range(C)]
+        for c in range(C):
+            cnt[c, r] = own[c]
+        seg = torch.zeros(C * W + 1, dtype=torch.int64)
+        seg[1:] = cnt.flatten().cumsum(0)
+        self.seg = seg.view(-1).tolist()  # segment (c, q) = [seg[c*W+q], seg[c*W+q+1])
+        self.n_pad = max(1, self.seg[-1])
+        self.recv_counts = cnt.tolist()  # [c][q]
+        # layout position of every ghost: its segment start + rank among the ghosts of that segment (ascending g)
+        key = chunk * W + owner
+        order = torch.sort(key * (self.n + 1) + need).indices  # stable (c, q, g) order
+        pos = torch.empty_like(need)
+        seg_dev = torch.tensor(self.seg[:-1], dtype=torch.int64, device=dev)
+        ks = key[order]
+        first = torch.searchsorted(ks, ks, right=False)  # index of the first ghost of the same segment
+        pos[order] = seg_dev[ks] + (torch.arange(ks.numel(), device=dev) - first)
+        # renumber the local columns: own rows -> own segment of their chunk, ghosts -> pos
+        g = col.long()
+        mine = (g >= self.row0) & (g < self.row1)
+        lo = g - self.row0
+        own_pos = seg_dev[(lo // L).clamp(0, C - 1) * W + r] + lo % L
+        gpos = pos[torch.searchsorted(need, g).clamp(max=max(0, need.numel() - 1))] if need.numel() else g
+        out = torch.where(mine, own_pos, gpos).to(torch.int32)
+        self.ghost_ids, self.ghost_pos = need, pos
+        self.send_idx, self.send_counts, self.sendbuf = [torch.zeros(0, dtype=torch.int64, device=dev)] * C, \
+            [[0] * W for _ in range(C)], [torch.zeros(0, device=dev)] * C
+        if ctx.distributed:  # (a Context without a process group only emulates one rank's products)
+            # send side: tell every owner which of its rows this rank needs (counts, then ids, owner-major)
+            dev_c = dev if ctx.backend == "nccl" else torch.device("cpu")
+            req_counts = torch.bincount(owner, minlength=W).to(dev_c)
+            got_counts = torch.empty_like(req_counts)
+            dist.all_to_all_single(got_counts, req_counts)
+            got = torch.empty(int(got_counts.sum()), dtype=torch.int64, device=dev_c)
+            dist.all_to_all_single(got, need.to(dev_c), got_counts.tolist(), req_counts.tolist())
+            got = got.to(dev) - self.row0  # local rows peer q needs, ascending per peer
+            peer = torch.repeat_interleave(torch.arange(W, device=dev), got_counts.to(dev))
+            gchunk = got // L
+            self.send_idx, self.send_counts = [], []
+            for c in range(C):
+                sel = gchunk == c  # owner-major order kept: peers in rank order, rows ascending
+                self.send_idx.append((got[sel] - c * L + self.seg[c * W + r]).contiguous())  # layout positions
+                self.send_counts.append(torch.bincount(peer[sel], minlength=W).tolist())
+            self.sendbuf = [torch.empty(ix.numel(), dtype=torch.float32, device=dev) for ix in self.send_idx]
+        self.n_ghost = int(need.numel())
+        return out
 
     @staticmethod
     def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
                  slices: int = 0, head: float = 0.0625, balance: float = 0.0,
-                 chunks: int | None = None, item_nnz: int = 1024) -> "DistributedSpMV":
+                 chunks: int | None = None, item_nnz: int = 1024, exchange: str = "ghost") -> "DistributedSpMV":
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)
-        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz)
+        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz, exchange)
 
     @property
     def local_nnz(self) -> int:
         return sum(p.nnz for _, _, p in self.parts)
 
-    # ---- layout conversion (natural global order <-> padded layout)
+    # ---- layout conversion (natural global order <-> local layout)
+    def layout_ids(self) -> torch.Tensor:
+        """Global id of every local-layout entry (-1: padding), int64 [n_pad]."""
+        dev = self.ctx.device
+        if self.exchange == "allgather":
+            ids = torch.full((self.n_pad,), -1, dtype=torch.int64, device=dev)
+            ids[self.colmap] = torch.arange(self.n, device=dev)
+            return ids
+        ids = torch.full((self.n_pad,), -1, dtype=torch.int64, device=dev)
+        ids[self.local_positions()] = torch.arange(self.row0, self.row1, device=dev)
+        ids[self.ghost_pos] = self.ghost_ids
+        return ids
+
     def to_padded(self, x: torch.Tensor) -> torch.Tensor:
+        """x (natural order, full) -> this rank's layout vector."""
+        x = x.to(self.ctx.device, torch.float32)
+        if self.exchange == "allgather":
+            xp = torch.zeros(self.n_pad, dtype=torch.float32, device=self.ctx.device)
+            xp[self.colmap] = x
+            return xp
         xp = torch.zeros(self.n_pad, dtype=torch.float32, device=self.ctx.device)
-        xp[self.colmap] = x.to(xp.device, torch.float32)
+        xp[self.local_positions()] = x[self.row0:self.row1]
+        xp[self.ghost_pos] = x[self.ghost_ids]  # the entries the exchange delivers, taken from the full x here
         return xp
 
     def from_padded(self, xp: torch.Tensor) -> torch.Tensor:
-        return xp[self.colmap]
+        """Layout vector -> full natural-order vector (ghost layout: own rows all-gathered; tests / inspection)."""
+        if self.exchange == "allgather":
+            return xp[self.colmap]
+        mine = xp[self.local_positions()]
+        if not self.ctx.distributed:
+            return mine.clone()
+        buf = torch.zeros(self.block, dtype=mine.dtype, device=mine.device)
+        buf[:self.rows] = mine
+        parts = self.ctx.all_gather(buf)
+        return torch.cat([p[:self.cuts[q + 1] - self.cuts[q]] for q, p in enumerate(parts)])
+
+    def local_positions_chunk(self, c: int) -> torch.Tensor:
+        a, b = min(c * self.L, self.rows), min((c + 1) * self.L, self.rows)
+        s0 = self.seg[c * self.ctx.world + self.ctx.rank]
+        return torch.arange(s0, s0 + (b - a), device=self.ctx.device)
 
     def local_positions(self) -> torch.Tensor:
-        """Padded positions of this rank's rows, in local row order."""
-        return self.colmap[self.row0:self.row1]
+        """Layout positions of this rank's rows, in local row order."""
+        if self.exchange == "allgather":
+            return self.colmap[self.row0:self.row1]
+        return torch.cat([self.local_positions_chunk(c) for c in range(self.chunks)])
 
     # ---- products
     def _mul(self, part, xp: torch.Tensor, dst: torch.Tensor) -> None:
@@ -111,20 +217,41 @@ class DistributedSpMV:
         else:
             dst.copy_(spmv(part, xp))
 
+    def _post_chunk(self, out: torch.Tensor, c: int):
+        """Ghost exchange of chunk c: pack this rank's send entries, one grouped send/recv per peer pair."""
+        W, r, ops = self.ctx.world, self.ctx.rank, []
+        if self.send_idx[c].numel():
+            torch.index_select(out, 0, self.send_idx[c], out=self.sendbuf[c])
+        s0 = 0
+        for q in range(W):
+            n_s, n_r = self.send_counts[c][q], self.recv_counts[c][q]
+            if q != r and n_s:
+                ops.append(dist.P2POp(dist.isend, self.sendbuf[c][s0:s0 + n_s], q))
+            if q != r and n_r:
+                a = self.seg[c * W + q]
+                ops.append(dist.P2POp(dist.irecv, out[a:a + n_r], q))
+            s0 += n_s
+        return dist.batch_isend_irecv(ops) if ops else []
+
     def step_padded(self, xp: torch.Tensor) -> torch.Tensor:
-        """xp (padded layout, replicated) -> A xp (padded layout, replicated on every rank). The result lives in
-        one of two internal buffers; the buffer that is not `xp` is overwritten."""
+        """xp (this rank's layout) -> A xp in the same layout (own rows + every ghost the next product reads).
+        The result lives in one of two internal buffers; the buffer that is not `xp` is overwritten."""
         out = self.bufs[0] if xp.data_ptr() != self.bufs[0].data_ptr() else self.bufs[1]
-        W, L = self.ctx.world, self.L
-        if not self.ctx.distributed:
-            for c, (a, b, part) in enumerate(self.parts):
-                self._mul(part, xp, out[c * L:c * L + (b - a)])
-            return out
-        works = []
+        W, L, works = self.ctx.world, self.L, []
         for c, (a, b, part) in enumerate(self.parts):
+            if self.exchange == "allgather":
+                dst = out[c * L:c * L + (b - a)] if not self.ctx.distributed else self.send[c, :b - a]
+            else:
+                s0 = self.seg[c * W + self.ctx.rank]
+                dst = out[s0:s0 + (b - a)]
             if b > a:
-                self._mul(part, xp, self.send[c, :b - a])
-            works.append(dist.all_gather_into_tensor(out[c * W * L:(c + 1) * W * L], self.send[c], async_op=True))
+                self._mul(part, xp, dst)
+            if not self.ctx.distributed:
+                continue
+            if self.exchange == "allgather":
+                works.append(dist.all_gather_into_tensor(out[c * W * L:(c + 1) * W * L], self.send[c], async_op=True))
+            else:
+                works += self._post_chunk(out, c)
         for w in works:
             w.wait()
         return out
@@ -134,7 +261,7 @@ class DistributedSpMV:
         return self.from_padded(self.step_padded(self.to_padded(x)))
 
     def reference_local(self, xp: torch.Tensor) -> torch.Tensor:
-        """fp64 product of this rank's rows with xp (padded layout), in local row order."""
+        """fp64 product of this rank's rows with xp (its layout), in local row order."""
         outs = []
         for a, b, part in self.parts:
             if isinstance(part, SlicedCSR):

@@ -8,7 +8,7 @@ own point-to-point link.
 
 Overlap: the halo exchange is posted as one grouped RCCL send/recv (RCCL runs it on its own stream);
 the interior rows, which do not read the halo, are computed on the compute stream meanwhile; only the
-boundary rows wait for the halo.
+boundary rows wait for the halo, and both boundary bands are updated by ONE launch (two row spans).
 
 Temporal blocking (fuse=T in 2, 3, 4, 6, 8): the slab keeps T halo rows per side, one grouped exchange moves
 T rows per neighbour every T updates (1/T of the messages — the halos are latency-bound on xGMI), and one
@@ -19,7 +19,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ..ops.stencil import DEFAULT_K, FUSED_STEPS, init_grid, stencil5_fused_step_, stencil5_step_
+from ..ops.stencil import DEFAULT_K, FUSED_STEPS, init_grid, stencil5_fused_spans_, stencil5_fused_step_, stencil5_step_
 from .dist import Context
 from .topology import split
 
@@ -59,6 +59,15 @@ class StencilSlab:
         else:
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=row_range)
 
+    def _update_edges(self, u, v):
+        """The two rank-edge bands (rows within `halo` of either end), after the halo rows arrived: one launch."""
+        d, rows = self.halo, self.rows
+        if self.fuse > 1:
+            stencil5_fused_spans_(u, v, ((0, d), (rows - d, rows)), self.row0, self.n, self.k, halo=d, steps=self.fuse)
+        else:
+            stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(0, d))
+            stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(rows - d, rows))
+
     def step(self, overlap: bool = True) -> None:
         """Advances `fuse` time steps (one halo exchange, one kernel launch per row range)."""
         ctx, rows, d = self.ctx, self.rows, self.halo  # rows within d of a rank edge read the halo
@@ -69,8 +78,7 @@ class StencilSlab:
             self._update(self.u, self.v, (d, rows - d))
             for r in reqs:
                 r.wait()
-            self._update(self.u, self.v, (0, d))
-            self._update(self.u, self.v, (rows - d, rows))
+            self._update_edges(self.u, self.v)
         else:
             for r in self._post_exchange():
                 r.wait()

@@ -1,0 +1,64 @@
+"""SpMV rank lab: one rank's local product per distributed step of the 1e8-nnz / 1e7-row power-law SpMV at
+N = 2 / 4 / 8 on one GPU (ranks emulated one at a time, no exchange), for both vector layouts:
+
+  ghost      compact local vector: own rows + only the x entries the rank's nonzeros reference
+  allgather  padded replicated vector (every row of y on every rank)
+
+Prints the product time (4 pipeline chunks, as the bench runs N > 1), the layout length and the exchange
+volume per step: bytes this rank receives (ghost: its ghosts; allgather: every other rank's rows).
+Run: python scripts/spmv_rank_lab.py [world ...]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from parallel_c_programs_amd.parallel.dist import Context  # noqa: E402
+from parallel_c_programs_amd.parallel.spmv import DistributedSpMV  # noqa: E402
+
+
+def timed(fn, reps=20):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    worlds = [int(a) for a in sys.argv[1:]] or [8, 4]
+    dev = torch.device("cuda", 0)
+    n, nnz = 10_000_000, 100_000_000
+    for W in worlds:
+        for r in sorted({0, W - 1}):
+            for ex in ("ghost", "allgather"):
+                d = DistributedSpMV.powerlaw(Context(rank=r, world=W, device=dev), n, nnz, slices=16, chunks=4,
+                                             exchange=ex)
+                xp = torch.rand(d.n_pad, device=dev)
+                dsts = [torch.empty(max(1, b - a), device=dev) for a, b, _ in d.parts]
+
+                def products():
+                    for (a, b, part), dst in zip(d.parts, dsts):
+                        if b > a:
+                            d._mul(part, xp, dst[:b - a])
+
+                ms = timed(products)
+                got = torch.cat([dst[:b - a] for (a, b, _), dst in zip(d.parts, dsts)]).double()
+                ref = d.reference_local(xp)
+                err = ((got - ref).abs().max() / ref.abs().max()).item()
+                recv = d.n_ghost if ex == "ghost" else d.n - d.rows
+                print(f"N={W} rank {r} {ex:9s} nnz {d.local_nnz} layout {d.n_pad:9d} product {ms:.4f} ms "
+                      f"({2 * d.local_nnz / ms / 1e6:.1f} GFLOP/s) recv/step {recv * 4 / 1e6:.1f} MB err {err:.1e}",
+                      flush=True)
+                del d, xp, dsts, got, ref
+                torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -250,6 +250,34 @@ def test_stencil_fused_deep_halo_slab_and_row_split(gpu, global_row0, global_row
         ops.stencil5_fused_step_(a, part, global_row0, global_rows, halo=steps, steps=steps, row_range=rr)
     assert torch.equal(full, part)
     assert torch.equal(full.cpu()[steps:-steps].view(torch.int16), ref[steps:-steps].view(torch.int16))
+    # both edge bands in ONE launch (two row spans), as the distributed step does after the halo arrives
+    spans = a.clone()
+    ops.stencil5_fused_step_(a, spans, global_row0, global_rows, halo=steps, steps=steps,
+                             row_range=(steps, rows - steps))
+    ops.stencil5_fused_spans_(a, spans, ((0, steps), (rows - steps, rows)), global_row0, global_rows, halo=steps,
+                              steps=steps)
+    assert torch.equal(full, spans)
+
+
+@pytest.mark.parametrize("steps", [4, 6])
+@pytest.mark.parametrize("spans", [((0, 700), (5000, 6500)), ((0, 0), (100, 7000)), ((6000, 7000), (0, 0)),
+                                   ((0, 3), (7997, 8000))])
+def test_stencil_fused_spans_match_full(gpu, steps, spans):
+    """Row spans in one launch (short and >= 6144-row span totals, one empty span, spans ending at the slab
+    edges) write exactly their rows, bit-identical to the full-range launch, and nothing else."""
+    rows, cols = 8000, 1000
+    g = torch.Generator().manual_seed(steps)
+    u = (torch.rand(rows + 2 * steps, cols, generator=g) * 4 - 2).to(torch.bfloat16).to(gpu)
+    full = u.clone()
+    ops.stencil5_fused_step_(u, full, 100, 20000, halo=steps, steps=steps)
+    sentinel = torch.full_like(u, 7.0)
+    out = sentinel.clone()
+    ops.stencil5_fused_spans_(u, out, spans, 100, 20000, halo=steps, steps=steps)
+    mask = torch.zeros(rows + 2 * steps, dtype=torch.bool, device=gpu)
+    for a0, a1 in spans:
+        mask[steps + a0:steps + a1] = True
+    assert torch.equal(out[mask], full[mask])
+    assert torch.equal(out[~mask], sentinel[~mask])
 
 
 def test_spmv_banded_vs_host(gpu):

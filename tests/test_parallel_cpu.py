@@ -208,22 +208,24 @@ def test_stencil_checkpoint_resume_world2(tmp_path):
     assert np.array_equal(fa, reference_run(40, 7, 24).view(torch.int16).numpy())
 
 
-def _spmv(ctx, q, n, nnz, chunks):
-    d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1, chunks=chunks)
+def _spmv(ctx, q, n, nnz, chunks, exchange):
+    d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1, chunks=chunks, exchange=exchange)
     x = torch.linspace(0, 1, n)
     y = d.step(x)
     y2 = d.step(y / y.abs().max())
-    # padded fast path: iterate in the padded layout, gathered straight into the next x (no index_select)
+    # fast path: iterate in the rank's layout (ghost segments / padded all-gather slots filled in place)
     xp = d.to_padded(x)
     yp = d.step_padded(xp)
     yp2 = d.step_padded(yp / yp.abs().max())
-    q.put((ctx.rank, (y.numpy(), y2.numpy(), d.from_padded(yp2).numpy(), d.n_pad)))
+    ids = d.layout_ids()
+    q.put((ctx.rank, (y.numpy(), y2.numpy(), d.from_padded(yp2).numpy(), d.n_pad, ids.numpy(), yp2.numpy())))
 
 
+@pytest.mark.parametrize("exchange", ["ghost", "allgather"])
 @pytest.mark.parametrize("world,chunks", [(3, 1), (3, 4), (2, 3), (4, 2)])
-def test_distributed_spmv_matches_serial(world, chunks):
+def test_distributed_spmv_matches_serial(world, chunks, exchange):
     n, nnz = 3000, 40000
-    res = _collect(world, _spmv, n, nnz, chunks)
+    res = _collect(world, _spmv, n, nnz, chunks, exchange)
     m = ops.powerlaw_csr(n, nnz, seed=1)
     x = torch.linspace(0, 1, n)
     y = ops.spmv(m, x)
@@ -232,7 +234,13 @@ def test_distributed_spmv_matches_serial(world, chunks):
         assert torch.equal(torch.from_numpy(res[r][0]), y)  # same rows, same kernel: bit-identical
         assert torch.allclose(torch.from_numpy(res[r][1]), y2, rtol=1e-5, atol=1e-5)
         assert torch.allclose(torch.from_numpy(res[r][2]), y2, rtol=1e-5, atol=1e-5)
-        assert res[r][3] >= n
+        # every layout entry (own rows and the ghosts / replicas the exchange delivered) holds y2 of its row
+        ids, yp2 = torch.from_numpy(res[r][4]), torch.from_numpy(res[r][5])
+        assert torch.allclose(yp2[ids >= 0], y2[ids[ids >= 0]], rtol=1e-5, atol=1e-5)
+        if exchange == "allgather":
+            assert res[r][3] >= n
+        else:  # compact: own rows + the ghosts its nonzeros reference, never more than the whole vector
+            assert res[r][3] <= n and int((ids >= 0).sum()) == res[r][3]
 
 
 def test_padded_index_is_a_permutation_and_identity_on_one_rank():
