@@ -16,7 +16,8 @@ by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harne
            halo exchange per neighbour overlapped with the interior update; bit-exact check of the same
            distributed path against the single-step oracle
   spmv     power-law CSR, 1e8 nnz / 1e7 rows, strong scaling: nnz-balanced row blocks, XCD-sliced kernel,
-           chunked all-gather of y overlapped with the product; fp64 check of every rank's rows
+           ghost exchange (only the x entries each rank's nonzeros reference, grouped per-peer send/recv) chunked
+           and overlapped with the product; fp64 check of every rank's rows
   (N > 1)  256 MiB RCCL all-reduce bus bandwidth
 
 rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra
@@ -48,7 +49,7 @@ def parse(argv=None):
     ap.add_argument("--stencil-fuse", type=int, default=6)
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
-    ap.add_argument("--spmv-chunks", type=int, default=0, help="all-gather pipeline depth (0: 1 at N=1, else 4)")
+    ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")
     ap.add_argument("--sections", default=",".join(SECTIONS), help="comma list out of " + ",".join(SECTIONS))
     ap.add_argument("--no-ref", action="store_true", help="skip the torch.matmul (hipBLASLt) reference timing")
     ap.add_argument("--small", action="store_true", help="tiny sizes (CPU/gloo rehearsal)")
@@ -151,6 +152,7 @@ def main(argv=None):
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
                     "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks,
+                    "spmv_exchange": sp.d.exchange if ctx.distributed else None,
                     "spmv_max_rel_err_vs_fp64": sp.check()["max_rel_err_vs_fp64"]})
         del sp
         free()

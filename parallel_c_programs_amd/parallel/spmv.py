@@ -55,7 +55,7 @@ def padded_index(cuts: list[int], chunks: int, L: int, device="cpu") -> torch.Te
 
 class DistributedSpMV:
     def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
-                 head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 1024,
+                 head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 0,
                  exchange: str = "ghost"):
         W, dev = ctx.world, ctx.device
         if exchange not in ("ghost", "allgather"):
@@ -65,7 +65,12 @@ class DistributedSpMV:
         self.row0, self.row1 = cuts[ctx.rank], cuts[ctx.rank + 1]
         self.rows = self.row1 - self.row0
         self.block = max(1, max(cuts[i + 1] - cuts[i] for i in range(W)))
-        C = chunks if chunks else (1 if W == 1 else 4)
+        # defaults from one rank's products at N=8 (scripts/spmv_rank_lab.py, profiles/r2_spmv/rank_lab.txt): every
+        # chunk is a kernel + combine launch pair over 1/C of a small matrix (4 chunks 0.161 ms, 2: 0.134, 1: 0.113),
+        # so 2 chunks balance the exposed last-chunk exchange against the launch overhead; 512-nnz items give the
+        # smaller per-rank matrices more waves (2 chunks: 0.134 -> 0.127 ms)
+        C = chunks if chunks else (1 if W == 1 else 2)
+        item_nnz = item_nnz or (1024 if W == 1 else 512)
         C = max(1, min(int(C), self.block))
         self.chunks = C
         self.L = -(-self.block // C)
@@ -152,7 +157,7 @@ class DistributedSpMV:
     @staticmethod
     def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
                  slices: int = 0, head: float = 0.0625, balance: float = 0.0,
-                 chunks: int | None = None, item_nnz: int = 1024, exchange: str = "ghost") -> "DistributedSpMV":
+                 chunks: int | None = None, item_nnz: int = 0, exchange: str = "ghost") -> "DistributedSpMV":
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)

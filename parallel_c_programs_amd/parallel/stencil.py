@@ -8,7 +8,10 @@ own point-to-point link.
 
 Overlap: the halo exchange is posted as one grouped RCCL send/recv (RCCL runs it on its own stream);
 the interior rows, which do not read the halo, are computed on the compute stream meanwhile; only the
-boundary rows wait for the halo, and both boundary bands are updated by ONE launch (two row spans).
+boundary rows wait for the halo, and both boundary bands are updated by ONE launch (two row spans). Measured on
+one rank's slab (scripts/stencil_rank_lab.py, profiles/r2_stencil/rank_lab.txt): one edge launch instead of two
+saves 8-16 us per step at N=2-8; issuing it on a side stream to run beside the interior kernel was 5% faster at
+N=8 but up to 17% slower at N=2/4 (cross-stream waits), so it stays on the compute stream.
 
 Temporal blocking (fuse=T in 2, 3, 4, 6, 8): the slab keeps T halo rows per side, one grouped exchange moves
 T rows per neighbour every T updates (1/T of the messages — the halos are latency-bound on xGMI), and one

@@ -37,9 +37,12 @@ def main():
     n, nnz = 10_000_000, 100_000_000
     for W in worlds:
         for r in sorted({0, W - 1}):
-            for ex in ("ghost", "allgather"):
-                d = DistributedSpMV.powerlaw(Context(rank=r, world=W, device=dev), n, nnz, slices=16, chunks=4,
-                                             exchange=ex)
+            for ex, C, item in (("ghost", 4, 1024), ("allgather", 4, 1024), ("ghost", 2, 1024), ("ghost", 1, 1024),
+                                ("ghost", 4, 512), ("ghost", 2, 512)):
+                if r and (ex, C, item) != ("ghost", 4, 1024):
+                    continue
+                d = DistributedSpMV.powerlaw(Context(rank=r, world=W, device=dev), n, nnz, slices=16, chunks=C,
+                                             exchange=ex, item_nnz=item)
                 xp = torch.rand(d.n_pad, device=dev)
                 dsts = [torch.empty(max(1, b - a), device=dev) for a, b, _ in d.parts]
 
@@ -53,7 +56,7 @@ def main():
                 ref = d.reference_local(xp)
                 err = ((got - ref).abs().max() / ref.abs().max()).item()
                 recv = d.n_ghost if ex == "ghost" else d.n - d.rows
-                print(f"N={W} rank {r} {ex:9s} nnz {d.local_nnz} layout {d.n_pad:9d} product {ms:.4f} ms "
+                print(f"N={W} rank {r} {ex:9s} chunks {C} item {item:4d} nnz {d.local_nnz} layout {d.n_pad:9d} product {ms:.4f} ms "
                       f"({2 * d.local_nnz / ms / 1e6:.1f} GFLOP/s) recv/step {recv * 4 / 1e6:.1f} MB err {err:.1e}",
                       flush=True)
                 del d, xp, dsts, got, ref

@@ -4,7 +4,8 @@ exchange, for the launch shapes a step can take:
 
   full      one launch over all rows (no overlap split)
   split3    interior launch + one launch per edge band (round-2 step)
-  split2    interior launch + both edge bands in ONE two-span launch (current step)
+  split2    interior launch + both edge bands in ONE two-span launch
+  split2c   split2 with the edge launch on a side stream, concurrent with the interior kernel (current step)
 
 Every variant is checked bit for bit against `full`. Prints ms per step and GLUP/s per GPU; with the 1-GPU
 full-grid time this bounds the strong-scaling efficiency of the compute part (docs/ARCHITECTURE.md, stencil).
@@ -57,9 +58,19 @@ def main():
                 ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
                 ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), row0, N, halo=T, steps=T)
 
+            side = torch.cuda.Stream(dev)
+
+            def split2c():  # the edge launch on a side stream, concurrent with the interior kernel
+                main = torch.cuda.current_stream(dev)
+                side.wait_stream(main)
+                ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
+                with torch.cuda.stream(side):
+                    ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), row0, N, halo=T, steps=T)
+                main.wait_stream(side)
+
             full()
             res = {}
-            for name, fn in (("full", full), ("split3", split3), ("split2", split2)):
+            for name, fn in (("full", full), ("split3", split3), ("split2", split2), ("split2c", split2c)):
                 out.zero_()
                 fn()
                 torch.cuda.synchronize()

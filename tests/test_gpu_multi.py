@@ -101,14 +101,22 @@ def test_volume3d_torchrun_rccl(gpu, tmp_path):
 @pytest.mark.parametrize("world,fuse", [(2, 6), (8, 6), (8, 4), (4, 8)])
 def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse):
     """Every rank of a `world`-rank row-slab stencil on one GPU: halos copied slab to slab (what the grouped RCCL
-    send/recv moves), then the overlapped launch split of StencilSlab.step (interior rows, then the two boundary
-    ranges) — bit-identical to the single-domain oracle. At world 8 a slab of a 2048-row grid is a short range,
-    so this runs the v2 kernel's 24-rows-per-wave launch with interior and edge waves."""
+    send/recv moves), then StencilSlab.step's overlapped path itself (interior rows, then both boundary bands in
+    one two-span launch) — bit-identical to the single-domain oracle. At
+    world 8 a slab of a 2048-row grid is a short range, so this runs the v2 kernel's 24-rows-per-wave launch with
+    interior and edge waves."""
     from parallel_c_programs_amd.parallel.dist import Context
     from parallel_c_programs_amd.parallel.stencil import StencilSlab, reference_run
 
+    class Emulated(Context):  # a rank of a distributed run whose halo exchange the test performs itself
+        @property
+        def distributed(self):
+            return True
+
     n, cols, steps = 2048, 1000, 2 * fuse
-    slabs = [StencilSlab(Context(rank=r, world=world, device=gpu), n, cols, fuse=fuse) for r in range(world)]
+    slabs = [StencilSlab(Emulated(rank=r, world=world, device=gpu), n, cols, fuse=fuse) for r in range(world)]
+    for s in slabs:
+        s._post_exchange = lambda: []
     for _ in range(steps // fuse):
         for r, s in enumerate(slabs):  # halo exchange: T rows from each neighbour
             h = s.halo
@@ -117,12 +125,7 @@ def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse):
             if r < world - 1:
                 s.u[s.rows + h:s.rows + 2 * h].copy_(slabs[r + 1].u[h:2 * h])
         for s in slabs:
-            d = s.halo
-            s._update(s.u, s.v, (d, s.rows - d))
-            s._update(s.u, s.v, (0, d))
-            s._update(s.u, s.v, (s.rows - d, s.rows))
-        for s in slabs:
-            s.u, s.v = s.v, s.u
+            s.step(overlap=True)
     got = torch.cat([s.interior() for s in slabs]).cpu()
     ref = reference_run(n, steps, cols, device=gpu).cpu()
     assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
