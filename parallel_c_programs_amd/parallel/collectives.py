@@ -39,10 +39,9 @@ def global_scan(x: torch.Tensor, ctx: Context, exclusive: bool = False) -> torch
     if not ctx.distributed:
         return ops.scan(x, exclusive=exclusive)
     total = ops.reduce(x, "sum").reshape(1).float()
-    totals = ctx.all_gather(total)
-    before = torch.zeros(1, dtype=torch.float32, device=x.device)
-    for r in range(ctx.rank):
-        before = before + totals[r]
+    totals = torch.empty(ctx.world, dtype=torch.float32, device=x.device)
+    dist.all_gather_into_tensor(totals, total)  # one collective into one tensor, no per-rank list
+    before = totals[:ctx.rank].sum().reshape(1) if ctx.rank else torch.zeros(1, dtype=torch.float32, device=x.device)
     return ops.scan(x, exclusive=exclusive, init=before)
 
 
