@@ -12,9 +12,9 @@ by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harne
            (1e9 f32 in total, 1e9/N per GPU); fp64 check
   scan     global inclusive prefix sum over the rank-ordered concatenation (reduce-then-scan): weak and
            strong like reduce; fp64 check of the first 2^20 outputs of every rank incl. its rank offset
-  stencil  16384^2 bf16 5-point stencil, strong scaling: row slabs, 6 fused updates per kernel and one 6-row
-           halo exchange per neighbour overlapped with the interior update; bit-exact check of the same
-           distributed path against the single-step oracle
+  stencil  16384^2 bf16 5-point stencil, strong scaling: row slabs, T fused updates per kernel (T by slab
+           height: 8 / 6 / 6 / 4 at N = 1 / 2 / 4 / 8) and one T-row halo exchange per neighbour overlapped with
+           the interior update; bit-exact check of the same distributed path against the single-step oracle
   spmv     power-law CSR, 1e8 nnz / 1e7 rows, strong scaling: nnz-balanced row blocks, XCD-sliced kernel,
            ghost exchange (only the x entries each rank's nonzeros reference, grouped per-peer send/recv) chunked
            and overlapped with the product; fp64 check of every rank's rows
@@ -46,7 +46,8 @@ def parse(argv=None):
     ap.add_argument("--size", type=int, default=8192, help="SGEMM M=N=K")
     ap.add_argument("--reduce-n", type=float, default=1e9, help="f32 elements (per GPU weak, in total strong)")
     ap.add_argument("--stencil-n", type=int, default=16384)
-    ap.add_argument("--stencil-fuse", type=int, default=6)
+    ap.add_argument("--stencil-fuse", type=int, default=0,
+                    help="fused updates per kernel / halo depth (0: by slab height, 8 / 6 / 6 / 4 at N = 1 / 2 / 4 / 8)")
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
     ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")

@@ -284,6 +284,9 @@ __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
                     const int r = i - t - 1;
+                    // level t+1 row r feeds a stored row only if r >= rs - (T - t - 1): the first 2t+2 rows of
+                    // every level lie outside the wave's trapezoid (level T: rows above rs; same results)
+                    if (i - i0 <= 2 * t + 1) continue;
                     const long long g = grow0 + r;
                     Row8 nx;
                     const u32x4 pk = update_pairs(ring[t][m2], ring[t][m1], ring[t][m0], g == 0 || g == grows - 1,
@@ -394,6 +397,7 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
                 for (int t = 0; t < T; ++t) {
                     const int r = i - t - 1;
                     if (t + 1 < T) {
+                        if (i - i0 <= 2 * t + 1) continue;  // outside the wave's trapezoid (see stencil5xT_body)
                         u32x4 unused;
                         level_pairs<false>(ring[t][m2], ring[t][m1], ring[t][m0], k, ring[t + 1 < T ? t + 1 : 0][m0],
                                            unused);
@@ -488,26 +492,34 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
         return -1;
     const unsigned short* ui = (const unsigned short*)u;
     unsigned short* uo = (unsigned short*)out;
-    // T = 2 is HBM-bound: the v1 kernel. T >= 3 is VALU-bound: v2 with 48 rows per wave, or 24 on ranges under
-    // 6144 rows (a rank's slab at N = 4 / 8 is 4096 / 2048 rows: shorter waves give 2x the waves at 2T/RPW more
-    // redundant rows; T = 6, 16384 columns, scripts/stencil_lab.hip: 2048 rows 2.0 -> 2.97, 4096 rows 3.1 -> 4.0
-    // TGLUP/s; at 8192 rows 48 and 32 tie and 24 is 4% slower)
-    const bool short_range = (r1a - r0a) + (r1b - r0b) < 6144;
-    auto launch_dims = [&](int rpw, RowSpans& sp) {
-        const int per = kWaves * rpw;
+    // T = 2 is HBM-bound: the v1 kernel. T >= 3 is VALU-bound: v2, rows per wave by the launched row count (each
+    // wave recomputes the T-row trapezoid overlap with its neighbours, so short waves trade redundant level rows for
+    // more waves; scripts/stencil_lab.hip sweep after the trapezoid skip, profiles/r2_stencil/rpw_sweep_trapezoid.txt,
+    // 16384 columns, GLUP/s of the best RPW: 2048 rows T=4 24 (3.9k), T=6/8 16 (3.6k/3.4k); 4096 rows 24 (4.4-4.5k);
+    // 8192 rows 24-32 (4.9-5.1k); 16384 rows T=6/8 64 (5.4k/5.5k), T=4 24 (4.8k))
+    const int span_rows = (r1a - r0a) + (r1b - r0b);
+    const int rpw = span_rows < 3072 ? (steps <= 4 ? 24 : 16) : span_rows < 6144 ? 24 : span_rows < 12288 ? 32
+                    : (steps <= 4 ? 24 : 64);
+    auto launch_dims = [&](int rpw_, RowSpans& sp) {
+        const int per = kWaves * rpw_;
         sp = RowSpans{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per};
         return dim3((cols + kOutCols - 1) / kOutCols, sp.nby_a + (r1b - r0b + per - 1) / per);
     };
     RowSpans sp;
+#define PCMX_STENCIL_V2_RPW(T, R)                                                                                   \
+    case R: {                                                                                                       \
+        const dim3 g = launch_dims(R, sp);                                                                          \
+        stencil5xT2_kernel<T, 6, R><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,        \
+                                                              global_rows, k);                                      \
+        break;                                                                                                      \
+    }
 #define PCMX_STENCIL_V2(T)                                                                                          \
-    if (short_range) {                                                                                              \
-        const dim3 g = launch_dims(24, sp);                                                                         \
-        stencil5xT2_kernel<T, 6, 24><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,       \
-                                                               global_rows, k);                                     \
-    } else {                                                                                                        \
-        const dim3 g = launch_dims(48, sp);                                                                         \
-        stencil5xT2_kernel<T, 6, 48><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,       \
-                                                               global_rows, k);                                     \
+    switch (rpw) {                                                                                                  \
+        PCMX_STENCIL_V2_RPW(T, 16)                                                                                  \
+        PCMX_STENCIL_V2_RPW(T, 24)                                                                                  \
+        PCMX_STENCIL_V2_RPW(T, 32)                                                                                  \
+        PCMX_STENCIL_V2_RPW(T, 64)                                                                                  \
+        default: return -1;                                                                                         \
     }
     switch (steps) {
         case 2: {
@@ -522,6 +534,7 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
         default: return -1;
     }
 #undef PCMX_STENCIL_V2
+#undef PCMX_STENCIL_V2_RPW
     return (int)hipGetLastError();
 }
 

@@ -120,13 +120,14 @@ class Scan(Workload):
 class Stencil(Workload):
     """16384^2 bf16 5-point stencil, row slabs + halo exchange overlapped with the interior update.
     Strong scaling across ranks when `global_n` is fixed (the grid is split); weak when `per_rank`.
-    fuse=T (default 6): T time steps per kernel (temporal blocking, bit-identical to single steps) and a T-row
+    fuse=T (default 0: auto_fuse of the slab height): T time steps per kernel (temporal blocking, bit-identical to single steps) and a T-row
     halo exchange every T steps; one step() then advances T time steps and counts T updates per cell."""
 
-    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, fuse=6, **_):
-        from ..parallel.stencil import StencilSlab
+    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, fuse=0, **_):
+        from ..parallel.stencil import StencilSlab, auto_fuse
 
         rows = n * (ctx.world if per_rank else 1)
+        fuse = int(fuse) or auto_fuse(rows // ctx.world)
         super().__init__(ctx, {"n": n, "rows": rows, "graph_steps": graph_steps, "fuse": fuse}, "stencil", "GLUP/s")
         self.slab = StencilSlab(ctx, rows, n, fuse=fuse)
         self.overlap = overlap

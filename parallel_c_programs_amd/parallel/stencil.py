@@ -27,6 +27,14 @@ from .dist import Context
 from .topology import split
 
 
+def auto_fuse(slab_rows: int) -> int:
+    """Fused updates per kernel for a rank's slab height: the fused kernel is VALU-bound and every wave recomputes
+    its T-row trapezoid overlap, so deep fusion pays on tall slabs and short slabs want shallow fusion
+    (scripts/stencil_lab.hip, profiles/r2_stencil/rpw_sweep_trapezoid.txt, 16384 columns, best GLUP/s: 16384 rows
+    T=8 5.5k / T=6 5.4k; 8192 T=6 5.1k; 4096 T=6 4.5k; 2048 T=4 3.9k / T=6 3.6k)."""
+    return 8 if slab_rows >= 12288 else 6 if slab_rows >= 4096 else 4
+
+
 class StencilSlab:
     """One rank's (rows + 2, cols) bf16 slab and its double buffer."""
 

@@ -216,11 +216,13 @@ def test_stencil_row_range_split(gpu):
 
 
 @pytest.mark.parametrize("steps", [2, 3, 4, 6, 8])
-@pytest.mark.parametrize("shape", [(256, 512), (1000, 1000), (515, 4096), (9, 2000), (8300, 1000)])
+@pytest.mark.parametrize("shape", [(256, 512), (1000, 1000), (515, 4096), (9, 2000), (4000, 800), (8300, 1000),
+                                   (12400, 600)])
 def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
     """Temporal-blocking kernel == `steps` single steps (bf16 bits); random data so every lane/strip-overlap
-    path counts; column counts that are not multiples of the 496-column output strip; >= 6144 rows takes the
-    48-rows-per-wave launch, fewer the 24-row one (interior waves: v2 fast path, edge waves: v1 pipeline)."""
+    path counts; column counts that are not multiples of the 496-column output strip; the row counts cover every
+    rows-per-wave launch (16/24 under 3072 rows, 24 under 6144, 32 under 12288, 64 (T >= 6) / 24 above; interior
+    waves: v2 fast path with the trapezoid skip, edge waves: v1 pipeline)."""
     rows, cols = shape
     g = torch.Generator().manual_seed(rows + steps)
     u = (torch.rand(rows + 2, cols, generator=g) * 4 - 2).to(torch.bfloat16)
