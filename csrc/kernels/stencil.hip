@@ -154,6 +154,13 @@ __global__ __launch_bounds__(kWaves * 64) void stencil5_kernel(const unsigned sh
 //  * Slab: (rows + 2*halo) x ld, local row r at slab row r + halo. Rows within T of a rank boundary read T
 //    halo rows (halo >= T, checked by the launcher); at a GLOBAL edge the clamped rows only feed Dirichlet rows.
 constexpr int kOutCols = kStripCols - 16;  // 496 output columns per wave strip
+// Strip x loads columns [x*496, x*496 + 512): lanes 1..62 store [x*496 + 8, x*496 + 504). A lane whose first or last
+// column is a GLOBAL edge column (Dirichlet, never changes) stays exact at every level, so lane 0 of strip 0 and a
+// lane 63 ending at column cols-1 store too: 16384 columns = 504 + 31 x 496 + 504, 33 strips instead of 34.
+__device__ __forceinline__ int strip_c0(int lane) { return (int)blockIdx.x * kOutCols + lane * 8; }
+__device__ __forceinline__ bool strip_store_lane(int lane, int c0, int cols, bool in_grid) {
+    return in_grid && ((lane >= 1 && lane <= 62) || c0 == 0 || c0 + 8 == cols);
+}
 
 __device__ __forceinline__ void unpack8(const u32x4& w, float (&v)[8]) {
     v[0] = lo(w.x), v[1] = hi(w.x), v[2] = lo(w.y), v[3] = hi(w.y);
@@ -246,10 +253,10 @@ __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict
     static_assert(T >= 1 && T <= 8, "lanes 1..62 stay exact for at most 8 levels");
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63;
-    const int c0 = (int)blockIdx.x * kOutCols - 8 + lane * 8;  // first column of this lane (may be < 0)
+    const int c0 = strip_c0(lane);  // first column of this lane
     if (rs >= re) return;
-    const bool in_grid = c0 >= 0 && c0 + 8 <= cols;  // cols % 8 == 0
-    const bool store_lane = in_grid && lane >= 1 && lane <= 62;
+    const bool in_grid = c0 + 8 <= cols;  // cols % 8 == 0
+    const bool store_lane = strip_store_lane(lane, c0, cols, in_grid);
     const bool fix0 = c0 == 0, fix7 = c0 + 8 == cols;
     const int slab_rows = rows + 2 * halo;
     const unsigned short* base = u + (in_grid ? c0 : 0);
@@ -423,12 +430,12 @@ __global__ __launch_bounds__(kWaves * 64) void stencil5xT2_kernel(const unsigned
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int c0 = (int)blockIdx.x * kOutCols - 8 + lane * 8;  // first column of this lane (may be < 0)
+    const int c0 = strip_c0(lane);  // first column of this lane
     int rs, re;
     wave_rows<RPW>(sp, wave, rs, re);
     if (rs >= re) return;
-    const bool in_grid = c0 >= 0 && c0 + 8 <= cols;  // cols % 8 == 0
-    const bool store_lane = in_grid && lane >= 1 && lane <= 62;
+    const bool in_grid = c0 + 8 <= cols;  // cols % 8 == 0
+    const bool store_lane = strip_store_lane(lane, c0, cols, in_grid);
     const bool fix0 = c0 == 0, fix7 = c0 + 8 == cols;
     const int slab_rows = rows + 2 * halo;
     const int i0 = rs - T, i1 = re + T;  // u rows consumed: [i0, i1); level rows computed: [i0 - T, i1 - 1)
@@ -467,6 +474,12 @@ extern "C" int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, 
 }
 
 namespace {
+// strips covering `cols` columns (see strip_c0): strip x ends at x*496 + 504, or at x*496 + 512 == cols
+int strips_for(int cols) {
+    int n = 1;
+    while ((n - 1) * kOutCols + 504 < cols && (n - 1) * kOutCols + 512 != cols) ++n;
+    return n;
+}
 // the halo rule of one row range: rows within `steps` of a non-global slab edge read `steps` halo rows
 bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row0, long long global_rows) {
     const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
@@ -503,7 +516,7 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
     auto launch_dims = [&](int rpw_, RowSpans& sp) {
         const int per = kWaves * rpw_;
         sp = RowSpans{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per};
-        return dim3((cols + kOutCols - 1) / kOutCols, sp.nby_a + (r1b - r0b + per - 1) / per);
+        return dim3(strips_for(cols), sp.nby_a + (r1b - r0b + per - 1) / per);
     };
     RowSpans sp;
 #define PCMX_STENCIL_V2_RPW(T, R)                                                                                   \

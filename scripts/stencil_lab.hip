@@ -19,7 +19,7 @@ static int g_rows = 16384;  // rows of the slab (STENCIL_ROWS: 2048 = one rank's
 template <int V, int T, int RPW, int AH = 6>
 void launch(const unsigned short* u, unsigned short* o, int n, int ld, int halo, float k) {
     const int rows = g_rows;
-    dim3 grid((n + kOutCols - 1) / kOutCols, (rows + kWaves * RPW - 1) / (kWaves * RPW));
+    dim3 grid(strips_for(n), (rows + kWaves * RPW - 1) / (kWaves * RPW));
     const RowSpans sp{0, rows, 0, 0, (int)grid.y};
     if constexpr (V == 1)
         stencil5xT_kernel<T, 6, RPW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, sp, 0, rows, k);
