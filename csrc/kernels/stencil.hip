@@ -421,10 +421,8 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
     }
 }
 
-// kOcc: minimum waves per SIMD the register allocator must allow (1: no constraint)
-template <int T, int kAhead, int RPW = kRowsPerWave, int kOcc = 1>
-__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(kOcc))) void stencil5xT2_kernel(
-    const unsigned short* __restrict__ u,
+template <int T, int kAhead, int RPW = kRowsPerWave>
+__global__ __launch_bounds__(kWaves * 64) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
                                                                   unsigned short* __restrict__ out, int rows, int cols,
                                                                   int ld, int halo, RowSpans sp, long long grow0,
                                                                   long long grows, float k) {

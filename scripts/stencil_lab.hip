@@ -16,7 +16,7 @@
 
 static int g_rows = 16384;  // rows of the slab (STENCIL_ROWS: 2048 = one rank's slab of the 16384^2 grid at N=8)
 
-template <int V, int T, int RPW, int AH = 6, int OCC = 1>
+template <int V, int T, int RPW, int AH = 6>
 void launch(const unsigned short* u, unsigned short* o, int n, int ld, int halo, float k) {
     const int rows = g_rows;
     dim3 grid(strips_for(n), (rows + kWaves * RPW - 1) / (kWaves * RPW));
@@ -24,7 +24,7 @@ void launch(const unsigned short* u, unsigned short* o, int n, int ld, int halo,
     if constexpr (V == 1)
         stencil5xT_kernel<T, 6, RPW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, sp, 0, rows, k);
     else
-        stencil5xT2_kernel<T, AH, RPW, OCC><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, sp, 0, rows, k);
+        stencil5xT2_kernel<T, AH, RPW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, sp, 0, rows, k);
 }
 
 template <int T>
@@ -67,10 +67,6 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
     same("v2rpw96", [&] { launch<2, T, 96>(u, o, n, ld, halo, k); });
 
     same("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
-    constexpr int OC = T <= 4 ? 4 : 3;  // one more wave per SIMD than the unconstrained allocation allows
-    same("v2occ", [&] { launch<2, T, 64, 6, OC>(u, o, n, ld, halo, k); });
-    same("v2occ24", [&] { launch<2, T, 24, 6, OC>(u, o, n, ld, halo, k); });
-    same("v2occA3", [&] { launch<2, T, 64, 3, OC>(u, o, n, ld, halo, k); });
     same("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
     same("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
     same("v2rpw24", [&] { launch<2, T, 24>(u, o, n, ld, halo, k); });
@@ -81,11 +77,6 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
         time("v2rpw96", [&] { launch<2, T, 96>(u, o, n, ld, halo, k); });
 
         time("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
-        time("v2occ", [&] { launch<2, T, 64, 6, OC>(u, o, n, ld, halo, k); });
-        time("v2occ24", [&] { launch<2, T, 24, 6, OC>(u, o, n, ld, halo, k); });
-        time("v2occA3", [&] { launch<2, T, 64, 3, OC>(u, o, n, ld, halo, k); });
-        time("v2occ16", [&] { launch<2, T, 16, 6, OC>(u, o, n, ld, halo, k); });
-        time("v2occ32", [&] { launch<2, T, 32, 6, OC>(u, o, n, ld, halo, k); });
         time("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
         time("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
         time("v2rpw24", [&] { launch<2, T, 24>(u, o, n, ld, halo, k); });
