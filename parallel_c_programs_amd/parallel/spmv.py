@@ -9,11 +9,11 @@ CSR benchmark of ref 3-serial-optimization/spmv.c:170-177, 331-367).
   * exchange="ghost" (default at N > 1): each rank keeps only the x entries its nonzeros reference — its own
     rows plus "ghost" entries owned by other ranks (63% of the 1e7 columns per rank at N=8 on the 1e8-nnz graph)
     — in a compact local vector laid out chunk-major, owner-minor:
-        [chunk 0: ghosts of rank 0 | ... | own rows of chunk 0 | ... | ghosts of rank W-1] [chunk 1: ...] ...
-    so one chunk's product is one contiguous own segment and every (chunk, peer) ghost segment is contiguous:
-    after chunk c's product, its send entries (one index list per peer, fixed at set-up) are packed and moved
-    with one grouped RCCL send/recv per peer pair (point-to-point xGMI links, no all-gather of the whole y)
-    straight into the peers' ghost segments, while chunk c+1 is multiplied. The column indices are renumbered
+        [chunk 0: ghosts of ranks 0..W-1 except r, in rank order | own rows of chunk 0] [chunk 1: ...] ...
+    so one chunk's product is one contiguous own segment and its ghosts one contiguous region: after chunk c's
+    product, its send entries (one index list per peer, fixed at set-up) are packed and moved by ONE
+    all_to_all_single (RCCL: grouped per-peer sends over the point-to-point xGMI links, no all-gather of the
+    whole y) straight into the peers' ghost regions, while chunk c+1 is multiplied. The column indices are renumbered
     into this layout once at set-up; on one rank it is the identity.
   * exchange="allgather": the padded replicated layout (every rank holds all of y): entry of global row g
     (rank r, local row l) lives at p(g) = (l // L) * (world * L) + r * L + (l % L), so chunk c of every rank is
@@ -111,16 +111,22 @@ class DistributedSpMV:
         own = [max(0, min((c + 1) * L, self.rows) - min(c * L, self.rows)) for c in range(C)]
         for c in range(C):
             cnt[c, r] = own[c]
-        seg = torch.zeros(C * W + 1, dtype=torch.int64)
-        seg[1:] = cnt.flatten().cumsum(0)
-        self.seg = seg.view(-1).tolist()  # segment (c, q) = [seg[c*W+q], seg[c*W+q+1])
-        self.n_pad = max(1, self.seg[-1])
+        # chunk c = [ghosts of every peer q != r, in rank order | own rows of chunk c]: the ghost part is ONE
+        # contiguous all_to_all_single output whose per-peer regions follow rank order (self region empty)
         self.recv_counts = cnt.tolist()  # [c][q]
+        self.seg, self.ghost0, self.ghost_len, off = [0] * (C * W), [0] * C, [0] * C, 0
+        for c in range(C):
+            self.ghost0[c] = off
+            for q in [q for q in range(W) if q != r] + [r]:
+                self.seg[c * W + q] = off  # segment (c, q) starts here
+                off += self.recv_counts[c][q]
+            self.ghost_len[c] = self.seg[c * W + r] - self.ghost0[c]
+        self.n_pad = max(1, off)
         # layout position of every ghost: its segment start + rank among the ghosts of that segment (ascending g)
         key = chunk * W + owner
         order = torch.sort(key * (self.n + 1) + need).indices  # stable (c, q, g) order
         pos = torch.empty_like(need)
-        seg_dev = torch.tensor(self.seg[:-1], dtype=torch.int64, device=dev)
+        seg_dev = torch.tensor(self.seg, dtype=torch.int64, device=dev)
         ks = key[order]
         first = torch.searchsorted(ks, ks, right=False)  # index of the first ghost of the same segment
         pos[order] = seg_dev[ks] + (torch.arange(ks.numel(), device=dev) - first)
@@ -223,20 +229,17 @@ class DistributedSpMV:
             dst.copy_(spmv(part, xp))
 
     def _post_chunk(self, out: torch.Tensor, c: int):
-        """Ghost exchange of chunk c: pack this rank's send entries, one grouped send/recv per peer pair."""
-        W, r, ops = self.ctx.world, self.ctx.rank, []
+        """Ghost exchange of chunk c: pack this rank's send entries, then ONE all_to_all_single (RCCL groups the
+        per-peer sends/receives over the xGMI links) straight into the chunk's ghost region. One collective call
+        instead of a batch of per-peer P2P ops: ~14 us of host time per call vs ~10 us per op (RCCL on MI355X,
+        scripts/host_overhead_lab.py), which at N = 8 would otherwise make the step launch-bound."""
+        W, r = self.ctx.world, self.ctx.rank
         if self.send_idx[c].numel():
             torch.index_select(out, 0, self.send_idx[c], out=self.sendbuf[c])
-        s0 = 0
-        for q in range(W):
-            n_s, n_r = self.send_counts[c][q], self.recv_counts[c][q]
-            if q != r and n_s:
-                ops.append(dist.P2POp(dist.isend, self.sendbuf[c][s0:s0 + n_s], q))
-            if q != r and n_r:
-                a = self.seg[c * W + q]
-                ops.append(dist.P2POp(dist.irecv, out[a:a + n_r], q))
-            s0 += n_s
-        return dist.batch_isend_irecv(ops) if ops else []
+        recv = [0 if q == r else self.recv_counts[c][q] for q in range(W)]
+        send = [0 if q == r else self.send_counts[c][q] for q in range(W)]
+        g0 = self.ghost0[c]
+        return [dist.all_to_all_single(out[g0:g0 + self.ghost_len[c]], self.sendbuf[c], recv, send, async_op=True)]
 
     def step_padded(self, xp: torch.Tensor) -> torch.Tensor:
         """xp (this rank's layout) -> A xp in the same layout (own rows + every ghost the next product reads).
