@@ -183,7 +183,7 @@ int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* va
                      float* extra, float* y, int n_rows, int n_cols, int n_slices, const long long* slice_nz0,
                      const long long* slice_item0, const long long* slice_out0, const void* items,
                      const unsigned* row_mask, const int* chunk_base, const void* fix, int n_fix, int mode,
-                     hipStream_t s);
+                     const int* slice_colbase, hipStream_t s);
 int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                      const float* x, float* y, hipStream_t s);
 

@@ -127,7 +127,13 @@ struct SliceMeta {
     long long nz0[kMaxSlices];    // first nonzero of slice s in the slice-major col/val/lrow
     long long item0[kMaxSlices + 1];
     long long out0[kMaxSlices];   // first compact partial of slice s
+    int colbase[kMaxSlices];      // packed layout: first tail column of slice s
 };
+// Packed layout (kMode bit 3): ONE 32-bit word per nonzero instead of a 4-B column + a 2-B row offset —
+//   bits 0-20 column - colbase[s] (tail) or the column itself (head, bit 21 set), bits 22-31 the row offset in
+//   the item (< 1023) — 6 -> 4 B of index stream per nonzero and one stream load instruction fewer per element.
+constexpr unsigned kPackColMask = 0x1FFFFFu, kPackHead = 0x200000u;
+constexpr int kPackRowShift = 22;
 
 template <int kPL>
 struct StreamRegs {
@@ -140,7 +146,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int kPL>
+template <int kPL, bool kPacked = false>
 __device__ __forceinline__ void load_item_stream(const int* __restrict__ col, const float* __restrict__ val,
                                                  const unsigned short* __restrict__ lrow, const Item& it,
                                                  StreamRegs<kPL>& q, int lane) {
@@ -152,8 +158,10 @@ __device__ __forceinline__ void load_item_stream(const int* __restrict__ col, co
         q.c[j] = __builtin_amdgcn_raw_buffer_load_b32(rc, i * 4, 0, 2);
         q.v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, i * 4, 0, 2));
     }
+    if constexpr (!kPacked) {
 #pragma unroll
-    for (int j = 0; j < kPL; ++j) q.r[j] = __builtin_amdgcn_raw_buffer_load_b16(rr, (j * kWave + lane) * 2, 0, 2);
+        for (int j = 0; j < kPL; ++j) q.r[j] = __builtin_amdgcn_raw_buffer_load_b16(rr, (j * kWave + lane) * 2, 0, 2);
+    }
 }
 
 struct SlicedCtx {
@@ -167,6 +175,7 @@ struct SlicedCtx {
     float* yw;
     long long i1, stride;
     int lane;
+    int colbase;  // packed layout: first tail column of the slice
 };
 
 // One pipeline step: gathers of the current item, stream loads of the next item, then the current item's
@@ -202,16 +211,24 @@ __device__ __forceinline__ void seg_scan_wave(float& v, int& f) {
 template <int kMode, int kPL>
 __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, const Item& cur, const StreamRegs<kPL>& q,
                                             Item& nitem, StreamRegs<kPL>& nq) {
+    constexpr bool kPacked = (kMode & 8) != 0;
     const int lane = k.lane;
     float g[kPL];
 #pragma unroll
-    for (int j = 0; j < kPL; ++j)
+    for (int j = 0; j < kPL; ++j) {
+        const unsigned w = (unsigned)q.c[j];
+        const unsigned c = kPacked ? (w & kPackColMask) + ((w & kPackHead) ? 0u : (unsigned)k.colbase) : w;
         g[j] = (kMode & 1) ? __int_as_float(q.c[j])
-                           : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(k.rx, q.c[j] * 4, 0, 0));
+                           : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(k.rx, c * 4, 0, 0));
+    }
+    // the row offset of element j (packed: the word's top bits; read before nq may reuse q's registers)
+    auto lrow_of = [&](int j) __attribute__((always_inline)) {
+        return kPacked ? (int)((unsigned)q.c[j] >> kPackRowShift) : (int)q.r[j];
+    };
     const long long nxt = it + k.stride;
     const bool more = nxt < k.i1;
     nitem = k.items[more ? nxt : it];
-    load_item_stream(k.col, k.val, k.lrow, nitem, nq, lane);  // (a harmless re-read of the last item at the end)
+    load_item_stream<kPL, kPacked>(k.col, k.val, k.lrow, nitem, nq, lane);  // (a harmless re-read of the last item)
     const int n = (int)(cur.nz1 - cur.nz0);
     const int nrows = cur.row1 - cur.row0;
     if constexpr ((kMode & 4) != 0) {
@@ -229,14 +246,14 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
 #pragma unroll
             for (int j = 0; j < kPL; ++j) {
                 const bool valid = j * kWave + lane < n;
-                const int r = valid ? (int)q.r[j] : 0x10000;  // past the item: one trailing non-row segment
+                const int r = valid ? lrow_of(j) : 0x10000;  // past the item: one trailing non-row segment
                 float v = valid ? q.v[j] * g[j] : 0.f;
                 const int rp = __builtin_amdgcn_update_dpp(rprev, r, 0x138, 0xf, 0xf, false);  // wave_shr:1
                 int f = r != rp;
                 seg_scan_wave(v, f);
                 v = f ? v : v + carry;  // lanes still in the row carried in from the previous stripe
                 const int rnext0 = (j + 1 < kPL && (j + 1) * kWave < n)
-                                       ? __builtin_amdgcn_readlane((int)q.r[j + 1 < kPL ? j + 1 : j], 0)
+                                       ? __builtin_amdgcn_readlane(lrow_of(j + 1 < kPL ? j + 1 : j), 0)
                                        : 0x10000;
                 const int rn = __builtin_amdgcn_update_dpp(rnext0, r, 0x130, 0xf, 0xf, false);  // wave_shl:1
                 const bool tail = valid && r != rn;
@@ -268,7 +285,7 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
 #pragma unroll
             for (int j = 0; j < kPL; ++j) {
                 const int i = j * kWave + lane;
-                if (i < n) atomicAdd(&k.yw[q.r[j]], q.v[j] * g[j]);
+                if (i < n) atomicAdd(&k.yw[lrow_of(j)], q.v[j] * g[j]);
             }
             dst = k.yp + cur.row0;
             nstore = nrows;
@@ -305,12 +322,13 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     if (it >= k.i1) return;
     const long long base = meta.nz0[s];
     k.col = col + base, k.val = val + base, k.lrow = lrow + base;
+    k.colbase = meta.colbase[s];
     k.rx = rsrc(x, (unsigned)n_cols * 4);
     k.items = items, k.extra = extra, k.yp = ypart + meta.out0[s], k.yw = yl[w];
     k.lane = pcmx::lane_id();
     Item ia = items[it], ib;
     StreamRegs<kPL> qa, qb;
-    load_item_stream<kPL>(k.col, k.val, k.lrow, ia, qa, k.lane);
+    load_item_stream<kPL, (kMode & 8) != 0>(k.col, k.val, k.lrow, ia, qa, k.lane);
     while (sliced_step<kMode, kPL>(k, it, ia, qa, ib, qb) && sliced_step<kMode, kPL>(k, it, ib, qb, ia, qa)) {
     }
 }
@@ -439,7 +457,7 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
                                 float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
                                 const long long* slice_nz0, const long long* slice_item0, const long long* slice_out0,
                                 const void* items, const unsigned* row_mask, const int* chunk_base, const void* fix,
-                                int n_fix, int mode, hipStream_t s) {
+                                int n_fix, int mode, const int* slice_colbase, hipStream_t s) {
     if (n_rows <= 0) return 0;
     if (n_slices <= 0 || n_slices % 8 || n_slices > kMaxSlices) return (int)hipErrorInvalidValue;
     const int persist_blocks = (mode >> 8) ? (mode >> 8) : kPersistBlocks;
@@ -454,6 +472,7 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         most = slice_item0[k + 1] - slice_item0[k] > most ? slice_item0[k + 1] - slice_item0[k] : most;
     }
     meta.item0[n_slices] = slice_item0[n_slices];
+    for (int k = 0; k < n_slices; ++k) meta.colbase[k] = slice_colbase ? slice_colbase[k] : 0;
     so.out0[n_slices] = slice_out0[n_slices];
     if (most > 0) {
         int dev = 0, cus = 256;
@@ -468,7 +487,15 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         const dim3 blk(kWavesPerBlock * kWave);
         // bit 0: skip the x gathers (lab), bit 1: items of 512 nonzeros (8 per lane), bit 2: LDS row sums (lab)
 #define PCMX_SLICED(M, PL) spmv_sliced_kernel<M, PL><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp)
-        switch (mode & 7) {
+        // slice_colbase != NULL: col holds the packed words (production layout when every slice is < 2^21 columns)
+        if (slice_colbase) {
+            if ((mode & 7) == 2)
+                PCMX_SLICED(12, 8);
+            else if ((mode & 7) == 0)
+                PCMX_SLICED(12, 16);
+            else
+                return (int)hipErrorInvalidValue;  // the lab modes read the unpacked layout
+        } else switch (mode & 7) {
             case 0: PCMX_SLICED(4, 16); break;
             case 1: PCMX_SLICED(5, 16); break;
             case 2: PCMX_SLICED(4, 8); break;

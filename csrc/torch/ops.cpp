@@ -479,12 +479,23 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
     check_gpu(ypart, "ypart", at::kFloat), check_gpu(extra, "extra", at::kFloat);
     check_gpu(row_mask, "row_mask", at::kInt), check_gpu(chunk_base, "chunk_base", at::kInt);
     TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous(), "spmv_sliced: CPU int64 meta");
-    const int64_t S = (meta.numel() - 2) / 3;  // meta = [nz0 (S) | item0 (S + 1) | out0 (S + 1)]
-    TORCH_CHECK(meta.numel() == 3 * S + 2 && S >= 8 && S % 8 == 0 && S <= PCMX_SPMV_MAX_SLICES,
+    // mode bit 3: packed layout (col holds one word per nonzero: column offset + head flag + row offset; lrow unused)
+    // and meta = [nz0 (S) | item0 (S + 1) | out0 (S + 1) | colbase (S)]; otherwise meta = [nz0 | item0 | out0]
+    const bool packed = (mode & 8) != 0;
+    const int64_t S = (meta.numel() - 2) / (packed ? 4 : 3);
+    TORCH_CHECK(meta.numel() == (packed ? 4 : 3) * S + 2 && S >= 8 && S % 8 == 0 && S <= PCMX_SPMV_MAX_SLICES,
                 "spmv_sliced: 8, 16, 24 or 32 slices");
     const int64_t* m = meta.data_ptr<int64_t>();
     const int64_t* out0 = m + 2 * S + 1;
-    TORCH_CHECK(lrow.numel() == col.numel() && val.numel() == col.numel(), "spmv_sliced: lrow / val shape");
+    TORCH_CHECK((packed || lrow.numel() == col.numel()) && val.numel() == col.numel(), "spmv_sliced: lrow / val shape");
+    std::vector<int> colbase;
+    if (packed) {
+        for (int64_t k = 0; k < S; ++k) {
+            TORCH_CHECK(m[3 * S + 2 + k] >= 0 && m[3 * S + 2 + k] < x.numel(), "spmv_sliced: packed column base");
+            colbase.push_back((int)m[3 * S + 2 + k]);
+        }
+        TORCH_CHECK((mode & 7) == 0 || (mode & 7) == 2, "spmv_sliced: the packed layout runs the production modes only");
+    }
     TORCH_CHECK(row_mask.numel() >= n_rows && chunk_base.numel() >= ((n_rows + 63) / 64) * S,
                 "spmv_sliced: row_mask / chunk_base shape");
     TORCH_CHECK(out0[0] == 0 && ypart.numel() >= out0[S], "spmv_sliced: ypart must hold every compact partial");
@@ -504,12 +515,14 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
     } else {
         y = at::empty({n_rows}, val.options());
     }
-    check_rc(pcmx_spmv_sliced(reinterpret_cast<const unsigned short*>(lrow.data_ptr<int16_t>()), col.data_ptr<int>(),
+    check_rc(pcmx_spmv_sliced(reinterpret_cast<const unsigned short*>(lrow.numel() ? lrow.data_ptr<int16_t>() : nullptr),
+                              col.data_ptr<int>(),
                               val.data_ptr<float>(), x.data_ptr<float>(), ypart.data_ptr<float>(), extra.data_ptr<float>(),
                               y.data_ptr<float>(), (int)n_rows, (int)x.numel(), (int)S, (const long long*)m,
                               (const long long*)m + S, (const long long*)out0, items.data_ptr(),
                               reinterpret_cast<const unsigned*>(row_mask.data_ptr<int>()), chunk_base.data_ptr<int>(),
-                              fix.data_ptr(), (int)fix.size(0), (int)mode, cur_stream(val)),
+                              fix.data_ptr(), (int)fix.size(0), (int)(mode & ~8), packed ? colbase.data() : nullptr,
+                              cur_stream(val)),
              "spmv_sliced");
     return y;
 }

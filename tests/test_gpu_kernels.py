@@ -333,6 +333,40 @@ def test_spmv_sliced_powerlaw_vs_fp64(gpu, slices, head):
     assert ((out - want).abs() / (absrow + 1e-3)).max().item() < 1e-5
     plain = ops.spmv(m.to(gpu), x.to(gpu)).cpu().double()
     assert ((out - plain).abs() / (absrow + 1e-3)).max().item() < 1e-5
+    # the packed index stream (production) and the unpacked col + lrow arrays: same products, same order
+    assert s.cr is not None
+    unpacked = ops.SlicedCSR(m.to(gpu), slices, head=head, pack=False)
+    assert unpacked.cr is None
+    assert torch.equal(out, unpacked.spmv(x.to(gpu)).cpu().double())
+
+
+@pytest.mark.parametrize("item_nnz", [512, 1024])
+def test_spmv_sliced_packed_wide_slices(gpu, item_nnz):
+    """Slices close to the 2^21-column limit of the packed word (few slices over 8e6 columns, head columns
+    flagged) and 512-/1024-nnz items: packed == unpacked bit for bit, both close to fp64."""
+    n_rows, n_cols = 2000, 8_000_000
+    g = torch.Generator().manual_seed(11)
+    lens = torch.randint(0, 400, (n_rows,), generator=g)
+    rp = torch.zeros(n_rows + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(lens, 0)
+    nnz = int(rp[-1])
+    # half the nonzeros in a hot head (low columns), half uniform over all columns; sorted within each row
+    col = torch.where(torch.rand(nnz, generator=g) < 0.5, torch.randint(0, 3000, (nnz,), generator=g),
+                      torch.randint(0, n_cols, (nnz,), generator=g)).to(torch.int32)
+    for r in range(0, n_rows, 1):
+        a, b = int(rp[r]), int(rp[r + 1])
+        col[a:b] = torch.sort(col[a:b]).values
+    m = ops.CSR(rp, col, torch.rand(nnz, generator=g) - 0.5, n_cols)
+    x = torch.rand(n_cols, generator=g)
+    s = ops.SlicedCSR(m.to(gpu), 8, head=0.3, item_nnz=item_nnz)
+    assert s.cr is not None and s.head_cols > 0
+    u = ops.SlicedCSR(m.to(gpu), 8, head=0.3, item_nnz=item_nnz, pack=False)
+    xg = x.to(gpu)
+    out = s.spmv(xg).cpu().double()
+    assert torch.equal(out, u.spmv(xg).cpu().double())
+    rows = torch.repeat_interleave(torch.arange(n_rows), lens)
+    want = torch.zeros(n_rows, dtype=torch.float64).index_add_(0, rows, m.val.double() * x.double()[m.col.long()])
+    assert (out - want).abs().max().item() < 1e-3
 
 
 def test_spmv_sliced_long_rows_and_unsorted_columns(gpu):
