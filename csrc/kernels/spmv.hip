@@ -345,7 +345,9 @@ __global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restri
                                                            int n_rows) {
     // XCD-aware chunk order: workgroups are dealt round-robin over the 8 XCDs, so block b takes chunk group
     // (b % 8) * (gridDim.x / 8) + b / 8 and each XCD walks ONE contiguous row range (a slice's partial runs of
-    // neighbouring chunks share cache lines in that XCD's L2 instead of being fetched by two XCDs)
+    // neighbouring chunks share cache lines in that XCD's L2 instead of being fetched by two XCDs). One 64-row
+    // chunk per wave: 2, 4 or 8 chunks per wave (more loads in flight per round trip) measured the same
+    // (0.739-0.749 ms per product, scripts/spmv_combine_lab.py history in profiles/r2_spmv).
     const int g = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
     const int c = __builtin_amdgcn_readfirstlane(g * 4 + (int)threadIdx.x / kWave);
     const int lane = pcmx::lane_id();
@@ -372,11 +374,26 @@ __global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restri
     if (r < n_rows) y[r] = acc;
 }
 
-// later pieces of split long rows: fix[k] = {item index, row}
+// later pieces of split long rows: fix[k] = {item index, row}, sorted by row (item order kept within a row). The
+// wave of the first entry of each row's run sums the run's extras (lane-strided, then a fixed-order wave
+// reduction) and adds them once: deterministic, unlike one float atomic per piece (whose order, and so whose
+// rounding, varied run to run), and parallel (a hub row of the power-law graph has hundreds of pieces).
 __global__ __launch_bounds__(256) void spmv_fixup_kernel(const float* __restrict__ extra, const int2* __restrict__ fix,
                                                          int n_fix, float* __restrict__ y) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k < n_fix) atomicAdd(&y[fix[k].y], extra[fix[k].x]);
+    const int k = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)threadIdx.x / kWave);  // one wave per entry
+    const int lane = pcmx::lane_id();
+    if (k >= n_fix) return;
+    const int row = fix[k].y;
+    if (k > 0 && fix[k - 1].y == row) return;
+    float acc = 0.f;
+    for (int j0 = k;; j0 += kWave) {  // a row's entries are contiguous: the run ends in the first stripe with a gap
+        const int j = j0 + lane;
+        const bool in = j < n_fix && fix[j].y == row;
+        if (in) acc += extra[fix[j].x];
+        if (__builtin_amdgcn_ballot_w64(!in) != 0) break;
+    }
+    acc = pcmx::wave_reduce<float, 0>(acc);
+    if (lane == 0) y[row] += acc;
 }
 
 // one wave per row of the banded matrix
@@ -516,7 +533,7 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         default: return (int)hipErrorInvalidValue;
     }
     if (n_fix > 0)
-        spmv_fixup_kernel<<<(n_fix + 255) / 256, 256, 0, s>>>(extra, reinterpret_cast<const int2*>(fix), n_fix, y);
+        spmv_fixup_kernel<<<(n_fix + 3) / 4, 256, 0, s>>>(extra, reinterpret_cast<const int2*>(fix), n_fix, y);
     return (int)hipGetLastError();
 }
 

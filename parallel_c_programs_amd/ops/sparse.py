@@ -153,7 +153,9 @@ class SlicedCSR:
             del touched, trows, tcnt, csum, rp
         del counts
         self.items = torch.cat(items).to(dev)
-        self.fix = torch.cat(fix).to(torch.int32).contiguous().to(dev)
+        fix = torch.cat(fix)
+        fix = fix[torch.sort(fix[:, 1], stable=True).indices]  # by row, item order kept: deterministic fix-up sums
+        self.fix = fix.to(torch.int32).contiguous().to(dev)
         self.row_mask = mask.to(torch.int32).contiguous()  # bit 31 wraps into the sign: read as u32 on device
         self.chunk_base = base.contiguous()
         self.meta = torch.cat([nz0, torch.tensor(item0, dtype=torch.int64), torch.tensor(out0, dtype=torch.int64)])
@@ -192,7 +194,8 @@ class SlicedCSR:
                 self._meta_packed = torch.cat([self.meta, torch.tensor(self.colbase, dtype=torch.int64)]).contiguous()
                 self._no_lrow = torch.empty(0, dtype=torch.int16, device=self.cr.device)
             return ops().spmv_sliced(self._no_lrow, self.cr, self.val, x, self.items, self.row_mask, self.chunk_base,
-                                     self.fix, self._meta_packed, self.ypart, self.extra, self.n_rows, out, 8 | self.mode)
+                                     self.fix, self._meta_packed, self.ypart, self.extra, self.n_rows, out,
+                                     8 | self.mode)
         return ops().spmv_sliced(self.lrow, self.col, self.val, x, self.items, self.row_mask, self.chunk_base, self.fix,
                                  self.meta, self.ypart, self.extra, self.n_rows, out, mode | self.mode)
 
