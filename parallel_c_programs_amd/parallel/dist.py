@@ -56,6 +56,32 @@ class Context:
             dist.broadcast(t, src)
         return t
 
+    def neighbour_exchange(self, pairs, async_op: bool = False) -> list:
+        """Sends / receives with a few peers: pairs = [(peer, send tensor, recv tensor)], each peer at most once,
+        tensors contiguous. On RCCL this is ONE list all_to_all (empty tensors for the other ranks; RCCL groups the
+        sends and receives over the point-to-point xGMI links): ~19 us of host time, against ~10 us per op for a
+        batch_isend_irecv of P2P ops (scripts/host_overhead_lab.py). gloo has no list all_to_all: a P2P batch.
+        Returns the works to wait on (empty when async_op is False: already complete on the stream)."""
+        if not self.distributed or not pairs:
+            return []
+        if self.backend == "nccl":
+            empty = pairs[0][1].new_empty(0)
+            ins, outs = [empty] * self.world, [empty] * self.world
+            for peer, snd, rcv in pairs:
+                ins[peer], outs[peer] = snd, rcv
+            w = dist.all_to_all(outs, ins, async_op=True)
+        else:
+            ops = []
+            for peer, snd, rcv in pairs:
+                ops += [dist.P2POp(dist.isend, snd, peer), dist.P2POp(dist.irecv, rcv, peer)]
+            w = dist.batch_isend_irecv(ops)
+        works = w if isinstance(w, list) else [w]
+        if async_op:
+            return works
+        for x in works:
+            x.wait()
+        return []
+
     def scalar(self, v, dtype=torch.float64) -> torch.Tensor:
         return torch.tensor([v], dtype=dtype, device=self.device)
 

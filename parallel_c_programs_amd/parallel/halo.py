@@ -2,15 +2,14 @@
 distribute_image_halo + exchange).
 
 MI355X design: one pack kernel gathers the 4 interior edges into a contiguous buffer, the 4 sends and
-4 receives go out as ONE grouped RCCL operation (torch.distributed.batch_isend_irecv -> ncclGroupStart/End,
-point-to-point over xGMI), then one unpack kernel fills the halo ring. The grouped call is deadlock-free by
+4 receives go out as ONE grouped RCCL operation (Context.neighbour_exchange: a list all_to_all ->
+ncclGroupStart/End, point-to-point over xGMI), then one unpack kernel fills the halo ring. The grouped call is deadlock-free by
 construction, replacing the reference's parity-ordered blocking Send/Recv (which relied on eager buffering,
 B9). Absent neighbours (grid edge) are skipped and their halo is left untouched.
 """
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from ..ops.halo import BOTTOM, LEFT, RIGHT, TOP, edge_slices, pack_edges, unpack_halo_
 from .dist import Context
@@ -41,26 +40,17 @@ class HaloExchanger2D:
         if not self.ctx.distributed:
             return recv
         top, bottom, left, right = edge_slices(H, W)
-        ops = []
         # my top edge -> north neighbour's bottom halo; north's bottom edge -> my top halo, etc.
-        pairs = [("north", top, top), ("south", bottom, bottom), ("west", left, left), ("east", right, right)]
-        for side, s_send, s_recv in pairs:
+        pairs, recv_parts = [], []
+        for side, sl in (("north", top), ("south", bottom), ("west", left), ("east", right)):
             peer = self.nb[side]
             if peer < 0:
                 continue
-            ops.append(dist.P2POp(dist.isend, send[s_send].contiguous(), peer))
-        recv_parts = {}
-        for side, s_send, s_recv in pairs:
-            peer = self.nb[side]
-            if peer < 0:
-                continue
-            buf = torch.empty_like(send[s_recv])
-            recv_parts[side] = (buf, s_recv)
-            ops.append(dist.P2POp(dist.irecv, buf, peer))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        for side, (buf, sl) in recv_parts.items():
+            buf = torch.empty_like(send[sl])
+            recv_parts.append((buf, sl))
+            pairs.append((peer, send[sl].contiguous(), buf))
+        self.ctx.neighbour_exchange(pairs)  # ONE RCCL call for the up-to-4 neighbours (Context.neighbour_exchange)
+        for buf, sl in recv_parts:
             recv[sl] = buf
         unpack_halo_(tile, recv, self.mask(), changed)
         return recv

@@ -54,25 +54,15 @@ class StencilSlab:
         self.south = ctx.rank + 1 if ctx.rank < ctx.world - 1 else -1
 
     def _post_exchange(self):
-        """One grouped send/recv of `halo` contiguous boundary rows per neighbour. On RCCL it is ONE all_to_all
-        call (per-peer tensors, empty for non-neighbours: RCCL groups the two sends and two receives): ~19 us of
-        host time against ~60 us for a batch of four P2P ops (scripts/host_overhead_lab.py), which would make a
-        2048-row slab's step (~45 us of GPU time at N = 8) launch-bound. gloo has no list all_to_all: P2P batch."""
-        u, h, rows, ops = self.u, self.halo, self.rows, []
-        if self.ctx.backend == "nccl":
-            W, empty = self.ctx.world, u.new_empty(0)
-            ins, outs = [empty] * W, [empty] * W
-            if self.north >= 0:
-                ins[self.north], outs[self.north] = u[h:2 * h], u[0:h]
-            if self.south >= 0:
-                ins[self.south], outs[self.south] = u[rows:rows + h], u[rows + h:rows + 2 * h]
-            return [dist.all_to_all(outs, ins, async_op=True)]
+        """One grouped exchange of `halo` contiguous boundary rows per neighbour (Context.neighbour_exchange: ONE
+        list all_to_all on RCCL, ~19 us of host time against ~60 us for a batch of four P2P ops, which would make a
+        2048-row slab's step, ~45 us of GPU time at N = 8, launch-bound)."""
+        u, h, rows, pairs = self.u, self.halo, self.rows, []
         if self.north >= 0:
-            ops += [dist.P2POp(dist.isend, u[h:2 * h], self.north), dist.P2POp(dist.irecv, u[0:h], self.north)]
+            pairs.append((self.north, u[h:2 * h], u[0:h]))
         if self.south >= 0:
-            ops += [dist.P2POp(dist.isend, u[rows:rows + h], self.south),
-                    dist.P2POp(dist.irecv, u[rows + h:rows + 2 * h], self.south)]
-        return dist.batch_isend_irecv(ops) if ops else []
+            pairs.append((self.south, u[rows:rows + h], u[rows + h:rows + 2 * h]))
+        return self.ctx.neighbour_exchange(pairs, async_op=True)
 
     def _update(self, u, v, row_range=None):
         """`fuse` updates u -> v over local rows row_range (default all)."""

@@ -104,19 +104,16 @@ class DistributedVolume:
         """Boundary planes to the z-neighbours (one grouped send/recv), landing in their halo planes; raises
         `changed` on the device when a halo plane takes new values."""
         s, nz = self.slab, self.slab.nz
-        ops_, recv = [], []
+        pairs, recv = [], []
         if self.below >= 0:
             buf = torch.empty_like(s.region[0])
-            ops_ += [dist.P2POp(dist.isend, s.region[1].contiguous(), self.below), dist.P2POp(dist.irecv, buf, self.below)]
+            pairs.append((self.below, s.region[1].contiguous(), buf))
             recv.append((0, buf))
         if self.above >= 0:
             buf = torch.empty_like(s.region[0])
-            ops_ += [dist.P2POp(dist.isend, s.region[nz].contiguous(), self.above),
-                     dist.P2POp(dist.irecv, buf, self.above)]
+            pairs.append((self.above, s.region[nz].contiguous(), buf))
             recv.append((nz + 1, buf))
-        if ops_:
-            for r in dist.batch_isend_irecv(ops_):
-                r.wait()
+        self.ctx.neighbour_exchange(pairs)  # one RCCL call (Context.neighbour_exchange)
         for plane, buf in recv:
             changed.logical_or_(torch.ne(s.region[plane], buf).any().reshape(1))
             s.region[plane].copy_(buf)

@@ -156,3 +156,45 @@ def test_spmv_ranks_emulated_on_one_gpu(gpu, world, exchange):
         assert got.shape == ref.shape == (d.rows,)
         err = ((got - ref).abs().max() / ref.abs().max()).item()
         assert err < 1e-5, (r, err)
+
+
+_NEIGHBOUR_SCRIPT = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["PCMX_ROOT"])
+from parallel_c_programs_amd.parallel.dist import init, finalize
+os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1")
+ctx = init()
+if not dist.is_initialized():  # world 1: init() leaves the group out; the call shapes still need one
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=ctx.device)
+ctx.backend, ctx.world = "nccl", 1
+dev = ctx.device
+a = torch.arange(12, dtype=torch.float32, device=dev).view(3, 4)
+b = torch.zeros(3, 4, device=dev)
+class Ctx(type(ctx)):
+    @property
+    def distributed(self):
+        return True
+c = Ctx(0, 1, 0, dev, "nccl")
+for w in c.neighbour_exchange([(0, a[1], b[2])], async_op=True):
+    w.wait()
+c.neighbour_exchange([(0, a[0:2].reshape(-1), b[0:2].reshape(-1))])
+e = a.new_empty(0)
+dist.all_to_all([e], [e])  # zero-size entries (non-neighbours) pass through RCCL's grouped send/recv
+torch.cuda.synchronize()
+assert torch.equal(b[2], a[1]) and torch.equal(b[0:2], a[0:2]), b
+print("neighbour_exchange ok")
+dist.destroy_process_group()
+"""
+
+
+def test_neighbour_exchange_rccl_call_shape(gpu, tmp_path):
+    """Context.neighbour_exchange on RCCL (one list all_to_all, zero-size entries for non-neighbours) on a world-1
+    NCCL group with the rank as its own neighbour: the call shape the stencil halo, the 2-D region halo and the
+    z-slab exchange use at N > 1."""
+    from parallel_c_programs_amd.parallel import free_port
+
+    script = tmp_path / "nb.py"
+    script.write_text(_NEIGHBOUR_SCRIPT)
+    env = dict(cli_env(), PCMX_ROOT=str(ROOT), MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "neighbour_exchange ok" in r.stdout, r.stderr[-3000:]
