@@ -257,7 +257,9 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
                                        : 0x10000;
                 const int rn = __builtin_amdgcn_update_dpp(rnext0, r, 0x130, 0xf, 0xf, false);  // wave_shl:1
                 const bool tail = valid && r != rn;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, tail ? (unsigned)r * 4u : 0x80000000u, 0, 2);
+                // predicated: only a row's last lane issues its store (an out-of-range offset on the other lanes
+                // still cost them address slots: 0.706 -> 0.693 ms per product, profiles/r2_spmv/store_ab.txt)
+                if (tail) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, (unsigned)r * 4u, 0, 2);
                 const int r63 = __builtin_amdgcn_readlane(r, 63);
                 carry = r63 == rnext0 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)) : 0.f;
                 rprev = r63;
@@ -347,7 +349,7 @@ __global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restri
     // (b % 8) * (gridDim.x / 8) + b / 8 and each XCD walks ONE contiguous row range (a slice's partial runs of
     // neighbouring chunks share cache lines in that XCD's L2 instead of being fetched by two XCDs). One 64-row
     // chunk per wave: 2, 4 or 8 chunks per wave (more loads in flight per round trip) measured the same
-    // (0.739-0.749 ms per product, scripts/spmv_combine_lab.py history in profiles/r2_spmv).
+    // (profiles/r2_spmv/combine_chunks_ab.txt).
     const int g = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
     const int c = __builtin_amdgcn_readfirstlane(g * 4 + (int)threadIdx.x / kWave);
     const int lane = pcmx::lane_id();
@@ -356,17 +358,17 @@ __global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restri
     const unsigned m = r < n_rows ? __builtin_nontemporal_load(mask + r) : 0u;
     const unsigned long long below = (1ull << lane) - 1ull;
     const int* bc = base + (size_t)c * S;
-    // every slice's load is issued unconditionally (a lane whose row the slice does not touch reads out of its
-    // descriptor's range and gets 0), so the S gathers overlap instead of serialising behind branches
+    // predicated loads: only the lanes whose row slice k touches issue a load (~36% of them). The S loads still
+    // overlap (no wait inside the loop), and inactive lanes cost the address unit nothing — issuing every lane
+    // with an out-of-range buffer offset instead made the pass address-rate bound: 113 -> ~73 us per product
+    // (profiles/r2_spmv/combine_variants_ab.txt; a cooperative 16-B-load + LDS variant measured in between)
     float v[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) {
         const bool bit = (m >> k) & 1u;
         const unsigned long long bal = __builtin_amdgcn_ballot_w64(bit);
-        const auto rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(comp) + so.out0[k], (short)0,
-                                                          (int)((so.out0[k + 1] - so.out0[k]) * 4), 0x00020000);
-        const unsigned off = bit ? (unsigned)(bc[k] + (int)__popcll(bal & below)) * 4u : 0xffffffffu;
-        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rk, off, 0, 0));
+        v[k] = 0.f;
+        if (bit) v[k] = comp[so.out0[k] + bc[k] + (long long)__popcll(bal & below)];
     }
     float acc = 0.f;
 #pragma unroll
