@@ -152,7 +152,7 @@ def main(argv=None):
         t = timed(ctx, sp.step, K, Wm)
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
-                    "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks,
+                    "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks, "spmv_slices": sp.d.slices,
                     "spmv_exchange": sp.d.exchange if ctx.distributed else None,
                     "spmv_max_rel_err_vs_fp64": sp.check()["max_rel_err_vs_fp64"]})
         del sp

@@ -53,6 +53,14 @@ def padded_index(cuts: list[int], chunks: int, L: int, device="cpu") -> torch.Te
     return (local // L) * (W * L) + owner * L + local % L
 
 
+def auto_slices(n_cols: int) -> int:
+    """XCD slices for a vector of n_cols entries: about 400K columns (1.6 MB of x) per slice, a multiple of 8 in
+    [8, 32]. Measured (one MI355X, 1e8-nnz power-law): 1e7 columns 16/24/32 slices = 0.711/0.675/0.688 ms per
+    product (after predication; 16 was best before it); one N=8 rank's 6.4M-column ghost layout 16/24/32 =
+    0.120/0.125/0.128 ms (profiles/r2_spmv/rank_lab.txt, slices_sweep.txt)."""
+    return int(min(32, max(8, 8 * round(n_cols / 400_000 / 8))))
+
+
 class DistributedSpMV:
     def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
                  head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 0,
@@ -83,6 +91,9 @@ class DistributedSpMV:
         else:
             col = self._ghost_layout(col)
         m = CSR(local.row_ptr.to(dev), col, local.val.to(dev), self.n_pad)
+        if slices < 0:
+            slices = auto_slices(self.n_pad)
+        self.slices = slices
         self.sliced = bool(slices) and dev.type == "cuda"
         self.parts = []  # (first local row, last local row + 1, CSR or SlicedCSR)
         for c in range(C):

@@ -37,11 +37,11 @@ def main():
     n, nnz = 10_000_000, 100_000_000
     for W in worlds:
         for r in sorted({0, W - 1}):
-            for ex, C, item in (("ghost", 4, 1024), ("allgather", 4, 1024), ("ghost", 2, 1024), ("ghost", 1, 1024),
-                                ("ghost", 4, 512), ("ghost", 2, 512)):
-                if r and (ex, C, item) != ("ghost", 4, 1024):
+            for ex, C, item, S in (("ghost", 2, 512, 24), ("ghost", 2, 512, 16), ("ghost", 1, 512, 24),
+                                   ("ghost", 2, 1024, 24), ("allgather", 2, 512, 24), ("ghost", 2, 512, 32)):
+                if r and (ex, C, item, S) != ("ghost", 2, 512, 24):
                     continue
-                d = DistributedSpMV.powerlaw(Context(rank=r, world=W, device=dev), n, nnz, slices=16, chunks=C,
+                d = DistributedSpMV.powerlaw(Context(rank=r, world=W, device=dev), n, nnz, slices=S, chunks=C,
                                              exchange=ex, item_nnz=item)
                 xp = torch.rand(d.n_pad, device=dev)
                 dsts = [torch.empty(max(1, b - a), device=dev) for a, b, _ in d.parts]
@@ -56,7 +56,7 @@ def main():
                 ref = d.reference_local(xp)
                 err = ((got - ref).abs().max() / ref.abs().max()).item()
                 recv = d.n_ghost if ex == "ghost" else d.n - d.rows
-                print(f"N={W} rank {r} {ex:9s} chunks {C} item {item:4d} nnz {d.local_nnz} layout {d.n_pad:9d} product {ms:.4f} ms "
+                print(f"N={W} rank {r} {ex:9s} slices {S} chunks {C} item {item:4d} nnz {d.local_nnz} layout {d.n_pad:9d} product {ms:.4f} ms "
                       f"({2 * d.local_nnz / ms / 1e6:.1f} GFLOP/s) recv/step {recv * 4 / 1e6:.1f} MB err {err:.1e}",
                       flush=True)
                 del d, xp, dsts, got, ref
