@@ -189,13 +189,13 @@ class SlicedCSR:
 
     def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None, mode: int = 0) -> torch.Tensor:
         """y = A x; `out` (contiguous f32, >= n_rows elements) receives y in place when given."""
-        if self.cr is not None and mode == 0:  # production: packed index stream
+        if self.cr is not None and (mode & 0xFF) == 0:  # production: packed index stream (bits 8+: resident blocks)
             if getattr(self, "_meta_packed", None) is None:
                 self._meta_packed = torch.cat([self.meta, torch.tensor(self.colbase, dtype=torch.int64)]).contiguous()
                 self._no_lrow = torch.empty(0, dtype=torch.int16, device=self.cr.device)
             return ops().spmv_sliced(self._no_lrow, self.cr, self.val, x, self.items, self.row_mask, self.chunk_base,
                                      self.fix, self._meta_packed, self.ypart, self.extra, self.n_rows, out,
-                                     8 | self.mode)
+                                     8 | self.mode | mode)
         return ops().spmv_sliced(self.lrow, self.col, self.val, x, self.items, self.row_mask, self.chunk_base, self.fix,
                                  self.meta, self.ypart, self.extra, self.n_rows, out, mode | self.mode)
 
