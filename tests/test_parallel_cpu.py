@@ -243,6 +243,38 @@ def test_distributed_spmv_matches_serial(world, chunks, exchange):
             assert res[r][3] <= n and int((ids >= 0).sum()) == res[r][3]
 
 
+def _spmv_uneven(ctx, q, cuts, chunks, exchange):
+    from parallel_c_programs_amd.ops.sparse import powerlaw_csr_rows, powerlaw_row_ptr
+
+    n = cuts[-1]
+    rp = powerlaw_row_ptr(n, 30000, 2.5, 3)
+    local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n, 3)
+    d = DistributedSpMV(ctx, rp, local, cuts, chunks=chunks, exchange=exchange)
+    x = torch.linspace(0, 1, n)
+    y = d.step(x)
+    xp = d.to_padded(x)
+    y2 = d.from_padded(d.step_padded(d.step_padded(xp)))
+    q.put((ctx.rank, (y.numpy(), y2.numpy())))
+
+
+@pytest.mark.parametrize("exchange", ["ghost", "allgather"])
+@pytest.mark.parametrize("cuts,chunks", [([0, 0, 1200, 2000], 2), ([0, 700, 700, 2000], 3), ([0, 5, 1990, 2000], 4)])
+def test_distributed_spmv_uneven_and_empty_ranks(cuts, chunks, exchange):
+    """Row blocks of very different sizes, an EMPTY rank (no rows: no products, empty sends, still part of every
+    collective) and more chunks than a small rank has rows: the exchange still delivers every referenced entry."""
+    res = _collect(len(cuts) - 1, _spmv_uneven, cuts, chunks, exchange)
+    from parallel_c_programs_amd.ops.sparse import powerlaw_csr_rows, powerlaw_row_ptr
+
+    n = cuts[-1]
+    m = powerlaw_csr_rows(powerlaw_row_ptr(n, 30000, 2.5, 3), 0, n, n, 3)
+    x = torch.linspace(0, 1, n)
+    y = ops.spmv(m, x)
+    y2 = ops.spmv(m, ops.spmv(m, x))
+    for r in range(len(cuts) - 1):
+        assert torch.equal(torch.from_numpy(res[r][0]), y)
+        assert torch.allclose(torch.from_numpy(res[r][1]), y2, rtol=1e-5, atol=1e-4)
+
+
 def test_padded_index_is_a_permutation_and_identity_on_one_rank():
     from parallel_c_programs_amd.parallel.spmv import padded_index
 
