@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
     ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")
+    ap.add_argument("--spmv-exchange", default="ghost", choices=("ghost", "allgather"),
+                    help="N>1 vector exchange: only the referenced entries (ghost) or the whole y (allgather)")
     ap.add_argument("--sections", default=",".join(SECTIONS), help="comma list out of " + ",".join(SECTIONS))
     ap.add_argument("--no-ref", action="store_true", help="skip the torch.matmul (hipBLASLt) reference timing")
     ap.add_argument("--small", action="store_true", help="tiny sizes (CPU/gloo rehearsal)")
@@ -148,7 +150,8 @@ def main(argv=None):
 
     # ---- SpMV 1e8-nnz power-law graph, strong scaling
     if "spmv" in sections:
-        sp = W.SpMV(ctx, n_rows=int(args.spmv_rows), nnz=int(args.spmv_nnz), chunks=args.spmv_chunks)
+        sp = W.SpMV(ctx, n_rows=int(args.spmv_rows), nnz=int(args.spmv_nnz), chunks=args.spmv_chunks,
+                    exchange=args.spmv_exchange)
         t = timed(ctx, sp.step, K, Wm)
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
