@@ -57,6 +57,9 @@ def parse(argv=None):
     ap.add_argument("--no-ref", action="store_true", help="skip the torch.matmul (hipBLASLt) reference timing")
     ap.add_argument("--small", action="store_true", help="tiny sizes (CPU/gloo rehearsal)")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")
+    ap.add_argument("--backend", default=None, choices=("nccl", "gloo"),
+                    help="process-group backend (default: nccl = RCCL on a GPU). gloo with --device cuda runs every "
+                         "rank's GPU kernels with host-staged messages: N ranks on ONE GPU (tests of the N>1 path)")
     a = ap.parse_args(argv)
     if a.small:
         a.size, a.reduce_n, a.stencil_n, a.spmv_rows, a.spmv_nnz = 256, 1e5, 256, 2e4, 2e5
@@ -77,7 +80,7 @@ def main(argv=None):
     from parallel_c_programs_amd.parallel import finalize, init
     from parallel_c_programs_amd.utils.harness import timed
 
-    ctx = init(device=args.device)
+    ctx = init(backend=args.backend, device=args.device)
     world, rank, dev = ctx.world, ctx.rank, ctx.device
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
@@ -163,7 +166,7 @@ def main(argv=None):
         log(f"spmv {out['spmv_gflops']} GFLOP/s")
 
     # ---- RCCL all-reduce bus bandwidth over xGMI (N > 1)
-    if ctx.distributed and dev.type == "cuda":
+    if ctx.distributed and dev.type == "cuda" and ctx.backend == "nccl":
         import torch.distributed as dist
 
         v = torch.ones(64 << 20, device=dev)

@@ -97,7 +97,8 @@ _OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp
 def init(backend: str | None = None, device: str | None = None) -> Context:
     """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
 
-    backend: "nccl" (RCCL, default when a GPU is visible) or "gloo" (CPU tensors)."""
+    backend: "nccl" (RCCL, default when a GPU is visible) or "gloo" (CPU tensors, or CUDA tensors with host-staged
+    messages: several ranks can then share ONE GPU, which tests the N > 1 GPU paths on a 1-GPU box)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))

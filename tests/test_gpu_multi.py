@@ -48,6 +48,19 @@ def _ngpu():
     return torch.cuda.device_count()
 
 
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_ranks_share_one_gpu_over_gloo(gpu, nproc):
+    """The whole N>1 bench path on ONE GPU: nproc torchrun ranks run their own GPU kernels (ghost-layout sliced
+    SpMV with 2 exchange chunks, stencil slabs with the interior / two-span edge launches, seeded multi-rank scan,
+    strong and weak reduce, weak SGEMM) while gloo carries the messages through host memory; every section's
+    correctness check must pass (timings are meaningless: the ranks share the GPU)."""
+    out = _bench(nproc, "--steps", "2", "--warmup", "1", "--no-ref", "--backend", "gloo", "--size", "2048",
+                 "--reduce-n", "5e7", "--stencil-n", "2048", "--spmv-rows", "5e5", "--spmv-nnz", "5e6", timeout=110)
+    _check_line(out, nproc)
+    assert out["spmv_exchange"] == "ghost" and out["spmv_chunks"] == 2 and out["spmv_slices"] >= 8
+    assert out["stencil_updates_per_step"] == 4
+
+
 @pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 visible GPUs")
 def test_bench_small_torchrun_all_gpus(gpu):
     n = min(_ngpu(), 8)
