@@ -70,6 +70,20 @@ class Context:
             for peer, snd, rcv in pairs:
                 ins[peer], outs[peer] = snd, rcv
             w = dist.all_to_all(outs, ins, async_op=True)
+        elif pairs[0][1].is_cuda:
+            # gloo's point-to-point ops on CUDA tensors are not stream-ordered (the transport reads/writes the
+            # device buffers from the host, racing the kernels around them): stage through host tensors
+            # (synchronous copies), the test transport that lets several ranks share one GPU
+            ops, staged = [], []
+            for peer, snd, rcv in pairs:
+                buf = torch.empty(rcv.shape, dtype=rcv.dtype)
+                ops += [dist.P2POp(dist.isend, snd.cpu(), peer), dist.P2POp(dist.irecv, buf, peer)]
+                staged.append((rcv, buf))
+            for x in dist.batch_isend_irecv(ops):
+                x.wait()
+            for rcv, buf in staged:
+                rcv.copy_(buf)
+            return []
         else:
             ops = []
             for peer, snd, rcv in pairs:

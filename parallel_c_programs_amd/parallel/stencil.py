@@ -158,15 +158,17 @@ class StencilSlab:
         if not self.ctx.distributed:
             return self.interior().clone()
         mine = self.interior().contiguous()
+        # gloo moves CUDA tensors without stream ordering: host copies (synchronous) for that test transport
+        staged = self.ctx.backend == "gloo" and mine.is_cuda
         if self.ctx.is_root:
             parts = [mine]
             for r in range(1, self.ctx.world):
                 a, b = split(self.n, self.ctx.world, r)
-                buf = torch.empty((b - a, self.cols), dtype=mine.dtype, device=mine.device)
+                buf = torch.empty((b - a, self.cols), dtype=mine.dtype, device="cpu" if staged else mine.device)
                 dist.recv(buf, r)
-                parts.append(buf)
+                parts.append(buf.to(mine.device))
             return torch.cat(parts)
-        dist.send(mine, 0)
+        dist.send(mine.cpu() if staged else mine, 0)
         return None
 
 
