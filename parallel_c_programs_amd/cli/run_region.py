@@ -31,10 +31,11 @@ def main(argv=None) -> int:
     ap.add_argument("--threshold", type=int, default=2)
     ap.add_argument("--dims", type=int, nargs=2, default=None)
     ap.add_argument("--backend", default=None)
+    ap.add_argument("--device", default=None, help="cpu or cuda (default: cpu with --backend gloo, else the GPU)")
     ap.add_argument("--out", default="out.bmp")
     ap.add_argument("--stats", action="store_true")
     a = ap.parse_args(argv)
-    ctx = init(a.backend, "cpu" if a.backend == "gloo" else None)
+    ctx = init(a.backend, a.device or ("cpu" if a.backend == "gloo" else None))
     try:
         image = torch.from_numpy(bmp.read(a.file)) if ctx.is_root else None
         stats: dict = {}

@@ -96,6 +96,21 @@ class Context:
             x.wait()
         return []
 
+    def _staged(self, t: torch.Tensor) -> bool:
+        """gloo moves CUDA tensors point-to-point without stream ordering: such messages go through host copies."""
+        return self.backend == "gloo" and t.is_cuda
+
+    def send(self, t: torch.Tensor, dst: int) -> None:
+        dist.send(t.cpu() if self._staged(t) else t.contiguous(), dst)
+
+    def recv(self, t: torch.Tensor, src: int) -> None:
+        if self._staged(t):
+            buf = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(buf, src)
+            t.copy_(buf)
+        else:
+            dist.recv(t, src)
+
     def scalar(self, v, dtype=torch.float64) -> torch.Tensor:
         return torch.tensor([v], dtype=dtype, device=self.device)
 

@@ -52,12 +52,14 @@ def scatter_tiles(ctx: Context, topo: CartTopology, image: torch.Tensor | None, 
             blk = padded[a0:a1 + 2, b0:b1 + 2].contiguous()
             if r == 0:
                 mine.copy_(blk)
+            elif ctx._staged(blk):
+                ctx.send(blk, r)
             else:
                 reqs.append(dist.isend(blk, r))
         for q in reqs:
             q.wait()
     else:
-        dist.recv(mine, 0)
+        ctx.recv(mine, 0)
     return mine
 
 
@@ -66,7 +68,7 @@ def gather_tiles(ctx: Context, topo: CartTopology, interior: torch.Tensor, H: in
     if not ctx.distributed:
         return interior.contiguous()
     if not ctx.is_root:
-        dist.send(interior.contiguous(), 0)
+        ctx.send(interior.contiguous(), 0)
         return None
     full = torch.empty((H, W), dtype=interior.dtype, device=interior.device)
     r0, r1, c0, c1 = topo.tile(0, H, W)
@@ -74,7 +76,7 @@ def gather_tiles(ctx: Context, topo: CartTopology, interior: torch.Tensor, H: in
     for r in range(1, topo.size):
         a0, a1, b0, b1 = topo.tile(r, H, W)
         buf = torch.empty((a1 - a0, b1 - b0), dtype=interior.dtype, device=interior.device)
-        dist.recv(buf, r)
+        ctx.recv(buf, r)
         full[a0:a1, b0:b1] = buf
     return full
 

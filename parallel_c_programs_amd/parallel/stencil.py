@@ -20,7 +20,6 @@ fused kernel performs the T updates with a single HBM read + write per cell. Bit
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from ..ops.stencil import DEFAULT_K, FUSED_STEPS, init_grid, stencil5_fused_spans_, stencil5_fused_step_, stencil5_step_
 from .dist import Context
@@ -158,17 +157,15 @@ class StencilSlab:
         if not self.ctx.distributed:
             return self.interior().clone()
         mine = self.interior().contiguous()
-        # gloo moves CUDA tensors without stream ordering: host copies (synchronous) for that test transport
-        staged = self.ctx.backend == "gloo" and mine.is_cuda
         if self.ctx.is_root:
             parts = [mine]
             for r in range(1, self.ctx.world):
                 a, b = split(self.n, self.ctx.world, r)
-                buf = torch.empty((b - a, self.cols), dtype=mine.dtype, device="cpu" if staged else mine.device)
-                dist.recv(buf, r)
-                parts.append(buf.to(mine.device))
+                buf = torch.empty((b - a, self.cols), dtype=mine.dtype, device=mine.device)
+                self.ctx.recv(buf, r)  # (host-staged on the gloo test transport: Context.recv)
+                parts.append(buf)
             return torch.cat(parts)
-        dist.send(mine.cpu() if staged else mine, 0)
+        self.ctx.send(mine, 0)
         return None
 
 
