@@ -25,7 +25,6 @@ from __future__ import annotations
 import ctypes
 
 import torch
-import torch.distributed as dist
 
 from .._native import cpu_lib
 from .._native import ops as native
@@ -149,10 +148,10 @@ class DistributedVolume:
         state = torch.zeros((image_dim * image_dim, 6), dtype=torch.int32, device=s.device)
         top = self.above < 0
         if not top:
-            dist.recv(state, self.above)
+            ctx.recv(state, self.above)
         img = s.raycast_stage(state, init=top, bottom=self.below < 0, image_dim=image_dim)
         if self.below >= 0:
-            dist.send(state, self.below)
+            ctx.send(state, self.below)
         return img
 
     def gather_region(self) -> torch.Tensor | None:
@@ -166,10 +165,10 @@ class DistributedVolume:
             for r in range(1, ctx.world):
                 a, b = split(s.dim, ctx.world, r)
                 buf = torch.empty((b - a, s.dim, s.dim), dtype=torch.uint8, device=s.device)
-                dist.recv(buf, r)
+                ctx.recv(buf, r)
                 parts.append(buf)
             return torch.cat(parts)
-        dist.send(mine, 0)
+        ctx.send(mine, 0)
         return None
 
 

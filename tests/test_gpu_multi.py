@@ -126,6 +126,21 @@ def test_region_ranks_share_one_gpu_over_gloo(gpu, tmp_path, nproc):
     assert np.array_equal(bmp.read(tmp_path / "out.bmp"), bmp.read(ASSETS / "region_pic1_golden.bmp"))
 
 
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_volume3d_ranks_share_one_gpu_over_gloo(gpu, tmp_path, nproc):
+    """The z-slab 3-D pipeline (slab generation, tiled slab growing with halo planes and device MAX termination,
+    pipelined slab ray caster) at nproc ranks on ONE GPU over gloo: the reference box region and image."""
+    from parallel_c_programs_amd.parallel import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "parallel_c_programs_amd.cli.run_volume3d",
+           "--image-dim", "64", "--backend", "gloo", "--device", "cuda"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=cli_env(), cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["region_voxels"] == 2197899 and out["image_sum"] == 127183
+
+
 @pytest.mark.parametrize("world,fuse", [(2, 6), (8, 6), (8, 4), (4, 8)])
 def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse):
     """Every rank of a `world`-rank row-slab stencil on one GPU: halos copied slab to slab (what the grouped RCCL
