@@ -67,6 +67,8 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
     same("v2rpw96", [&] { launch<2, T, 96>(u, o, n, ld, halo, k); });
 
     same("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
+    same("v2ahead9", [&] { launch<2, T, 64, 9>(u, o, n, ld, halo, k); });
+    same("v2ahead12", [&] { launch<2, T, 64, 12>(u, o, n, ld, halo, k); });
     same("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
     same("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
     same("v2rpw24", [&] { launch<2, T, 24>(u, o, n, ld, halo, k); });
@@ -77,6 +79,8 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
         time("v2rpw96", [&] { launch<2, T, 96>(u, o, n, ld, halo, k); });
 
         time("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
+        time("v2ahead9", [&] { launch<2, T, 64, 9>(u, o, n, ld, halo, k); });
+        time("v2ahead12", [&] { launch<2, T, 64, 12>(u, o, n, ld, halo, k); });
         time("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
         time("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
         time("v2rpw24", [&] { launch<2, T, 24>(u, o, n, ld, halo, k); });
