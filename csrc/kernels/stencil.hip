@@ -505,9 +505,10 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
         return -1;
     const unsigned short* ui = (const unsigned short*)u;
     unsigned short* uo = (unsigned short*)out;
-    // Prefetch ring: 9 rows ahead at T >= 6 (2 waves per SIMD there, so deeper per-wave prefetch hides more of the
-    // load latency: T=8 0.390-0.403 -> 0.383 ms, T=6 0.305-0.320 -> 0.302 ms at 16384^2; 12 rows spill at T=8;
-    // profiles/r2_stencil/prefetch_depth_ab.txt), 6 below.
+    // Prefetch ring: 9 rows ahead at T >= 6 on 64-row waves (2 waves per SIMD there, so deeper per-wave prefetch
+    // hides more load latency: T=8 0.390-0.403 -> 0.383 ms, T=6 0.305-0.320 -> 0.302 ms at 16384^2; 12 rows spill
+    // at T=8; on the 24-row waves of a 4096-row slab 9 rows measured ~7% slower; profiles/r2_stencil/
+    // prefetch_depth_ab.txt), 6 otherwise.
     // T = 2 is HBM-bound: the v1 kernel. T >= 3 is VALU-bound: v2, rows per wave by the launched row count (each
     // wave recomputes the T-row trapezoid overlap with its neighbours, so short waves trade redundant level rows for
     // more waves; scripts/stencil_lab.hip sweep after the trapezoid skip, profiles/r2_stencil/rpw_sweep_trapezoid.txt,
@@ -525,8 +526,9 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
 #define PCMX_STENCIL_V2_RPW(T, R)                                                                                   \
     case R: {                                                                                                       \
         const dim3 g = launch_dims(R, sp);                                                                          \
-        stencil5xT2_kernel<T, (T >= 6 ? 9 : 6), R><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp,      \
-                                                                             global_row0, global_rows, k);          \
+        stencil5xT2_kernel<T, (T >= 6 && R >= 64 ? 9 : 6), R><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld,     \
+                                                                                       halo, sp,                    \
+                                                                                       global_row0, global_rows, k); \
         break;                                                                                                      \
     }
 #define PCMX_STENCIL_V2(T)                                                                                          \
