@@ -68,6 +68,8 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
 
     same("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
     same("v2ahead9", [&] { launch<2, T, 64, 9>(u, o, n, ld, halo, k); });
+    same("v2rpw24a9", [&] { launch<2, T, 24, 9>(u, o, n, ld, halo, k); });
+    same("v2rpw16a9", [&] { launch<2, T, 16, 9>(u, o, n, ld, halo, k); });
     same("v2ahead12", [&] { launch<2, T, 64, 12>(u, o, n, ld, halo, k); });
     same("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
     same("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
@@ -80,6 +82,8 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
 
         time("v2ahead3", [&] { launch<2, T, 64, 3>(u, o, n, ld, halo, k); });
         time("v2ahead9", [&] { launch<2, T, 64, 9>(u, o, n, ld, halo, k); });
+        time("v2rpw24a9", [&] { launch<2, T, 24, 9>(u, o, n, ld, halo, k); });
+        time("v2rpw16a9", [&] { launch<2, T, 16, 9>(u, o, n, ld, halo, k); });
         time("v2ahead12", [&] { launch<2, T, 64, 12>(u, o, n, ld, halo, k); });
         time("v2rpw48", [&] { launch<2, T, 48>(u, o, n, ld, halo, k); });
         time("v2rpw32", [&] { launch<2, T, 32>(u, o, n, ld, halo, k); });
