@@ -113,41 +113,49 @@ at::Tensor dot(const at::Tensor& a, const at::Tensor& b) {
     return out;
 }
 
-// Sticky look-back-timeout word per device in host-mapped pinned memory: a scan kernel whose look-back gives
-// up ORs 1 into it (system-scope atomic), so the host sees it without a copy or a sync. The next scan on that
-// device (or scan_check) turns it into an error instead of a silently wrong prefix.
-volatile unsigned* scan_err_word(int dev, unsigned** dev_ptr) {
+// Sticky look-back-timeout word per (device, stream) in host-mapped pinned memory: a scan kernel whose look-back
+// gives up ORs 1 into it (system-scope atomic), so the host sees it without a copy. scan_check (and
+// ops.scan(check=True)) synchronises THAT stream and raises; the next scan on the same stream raises too. One word
+// per stream, so a failed scan on one stream is never reported (and cleared) by an unrelated call on another.
+struct ScanErrWord {
+    unsigned* host = nullptr;
+    unsigned* dev = nullptr;
+};
+
+ScanErrWord& scan_err_word(int dev, hipStream_t stream) {
     static std::mutex mu;
-    static unsigned* host[64] = {};
-    static unsigned* devp[64] = {};
-    TORCH_CHECK(dev >= 0 && dev < 64, "scan: device index");
+    static std::map<std::pair<int, hipStream_t>, ScanErrWord> words;
+    TORCH_CHECK(dev >= 0, "scan: device index");
     std::lock_guard<std::mutex> lock(mu);
-    if (!host[dev]) {
+    ScanErrWord& w = words[{dev, stream}];
+    if (!w.host) {
         void* p = nullptr;
         TORCH_CHECK(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess,
                     "scan: pinned error word");
         *static_cast<volatile unsigned*>(p) = 0u;
         void* d = nullptr;
         TORCH_CHECK(hipHostGetDevicePointer(&d, p, 0) == hipSuccess, "scan: mapped error word");
-        host[dev] = static_cast<unsigned*>(p), devp[dev] = static_cast<unsigned*>(d);
+        w.host = static_cast<unsigned*>(p), w.dev = static_cast<unsigned*>(d);
     }
-    if (dev_ptr) *dev_ptr = devp[dev];
-    return host[dev];
+    return w;
 }
 
-void raise_pending_scan_error(int dev) {
-    volatile unsigned* w = scan_err_word(dev, nullptr);
+void raise_pending_scan_error(int dev, hipStream_t stream) {
+    volatile unsigned* w = scan_err_word(dev, stream).host;
     if (*w) {
         *w = 0u;
-        TORCH_CHECK(false, "pcmx::scan: an earlier scan on device ", dev, " timed out in its decoupled look-back ",
+        TORCH_CHECK(false, "pcmx::scan: a scan on device ", dev, " (this stream) timed out in its decoupled look-back ",
                     "(a predecessor tile never published); that result is invalid");
     }
 }
 
+// Waits for the current stream of `device` and raises if any scan issued on it gave up a look-back.
 void scan_check(int64_t device) {
-    const at::DeviceGuard g(at::Device(at::kCUDA, (c10::DeviceIndex)device));
-    TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "scan_check: device synchronize");
-    raise_pending_scan_error((int)device);
+    const at::Device d(at::kCUDA, (c10::DeviceIndex)device);
+    const at::DeviceGuard g(d);
+    hipStream_t s = c10::hip::getCurrentHIPStream(d.index()).stream();
+    TORCH_CHECK(hipStreamSynchronize(s) == hipSuccess, "scan_check: stream synchronize");
+    raise_pending_scan_error((int)device, s);
 }
 
 at::Tensor scan_out(const at::Tensor& x, at::Tensor out, bool exclusive, const c10::optional<at::Tensor>& init) {
@@ -155,9 +163,9 @@ at::Tensor scan_out(const at::Tensor& x, at::Tensor out, bool exclusive, const c
     TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() == out.numel(), "scan: contiguous same-size tensors");
     TORCH_CHECK(out.device() == x.device(), "scan: out must be on x's device");
     const at::DeviceGuard g(x.device());
-    unsigned* err_dev = nullptr;
-    scan_err_word(x.device().index(), &err_dev);
-    raise_pending_scan_error(x.device().index());
+    hipStream_t stream = cur_stream(x);
+    unsigned* err_dev = scan_err_word(x.device().index(), stream).dev;
+    raise_pending_scan_error(x.device().index(), stream);
     const float* init_ptr = nullptr;
     at::Tensor init_c;
     if (init.has_value() && init->defined()) {
@@ -173,7 +181,7 @@ at::Tensor scan_out(const at::Tensor& x, at::Tensor out, bool exclusive, const c
     }
     auto ws = workspace(x, pcmx_scan_workspace_bytes(xc.numel()));
     check_rc(pcmx_scan_f32(xc.data_ptr<float>(), oc.data_ptr<float>(), xc.numel(), exclusive ? 1 : 0, init_ptr, ws.data_ptr(),
-                           err_dev, cur_stream(x)),
+                           err_dev, stream),
              "scan");
     if (!oc.is_same(out)) out.copy_(oc);
     return out;

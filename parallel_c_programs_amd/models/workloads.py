@@ -106,15 +106,25 @@ class Scan(Workload):
         # 4 B/element reduce pass that seeds each rank's offset counts as time, not as work
         return 8.0 * self.x.numel()
 
-    def check(self):
-        n = min(self.x.numel(), 1 << 20)
-        ref = torch.cumsum(self.x[:n].double(), 0)
-        # offset of this rank = sum of lower ranks' totals
+    def check(self, chunk: int = 1 << 26):
+        """Every output of the timed scan (all n, not a prefix) against an fp64 cumsum carried across chunks, seeded
+        with this rank's offset (the fp64 sum of the lower ranks' totals); the look-back error word of the stream
+        is checked first (raises if any timed scan gave up a look-back)."""
+        if self.x.is_cuda:
+            ops.scan_check(self.x.device)
         tot = self.x.double().sum().reshape(1)
         totals = self.ctx.all_gather(tot)
-        off = sum(float(t) for t in totals[: self.ctx.rank])
-        err = ((self.y[:n].double() - (ref + off)).abs().max() / (ref[-1] + off)).item()
-        return {"rel_err_vs_fp64": err}
+        carry = torch.zeros((), dtype=torch.float64, device=self.x.device)
+        for t in totals[: self.ctx.rank]:
+            carry = carry + t.to(carry.device).reshape(())
+        err = torch.zeros((), dtype=torch.float64, device=self.x.device)
+        n = self.x.numel()
+        for s in range(0, n, chunk):
+            ref = torch.cumsum(self.x[s:s + chunk].double(), 0) + carry
+            err = torch.maximum(err, (self.y[s:s + chunk].double() - ref).abs().max())
+            carry = ref[-1]
+        # relative to this rank's largest prefix (its last one: the inputs are non-negative)
+        return {"rel_err_vs_fp64": (err / carry.abs().clamp_min(1e-30)).item(), "elements_checked": n}
 
 
 class Stencil(Workload):
@@ -152,11 +162,22 @@ class Stencil(Workload):
         return r
 
     def check(self):
-        """The timed path at this world size, bit for bit: a small grid stepped through the same slab code
-        (row slabs, fused T-row halo exchange, overlap) equals the single-domain single-step oracle."""
-        from ..parallel.stencil import StencilSlab, reference_run
+        """Two bit-exact checks.
+        timed grid: the grid the timed steps produced (warm-up + timed, `steps_done` updates of the full 16384^2
+          problem, this rank's rows) against a plain-PyTorch f32 single-step oracle of the whole grid
+          (ops.stencil5_reference, bf16 rounding per step) run on this rank's device;
+        small grid: a small grid stepped through the same slab code at this world size (row slabs, fused T-row
+          halo exchange, overlap) against the single-domain single-step oracle."""
+        from ..parallel.stencil import StencilSlab, reference_run, reference_run_torch
 
-        f = self.slab.fuse
+        sl = self.slab
+        ref = reference_run_torch(sl.n, sl.steps_done, sl.cols, sl.k, device=self.ctx.device)
+        mine = sl.interior()
+        timed_ok = float(torch.equal(mine.view(torch.int16), ref[sl.row0:sl.row0 + sl.rows].view(torch.int16)))
+        del ref
+        timed_ok = 1.0 - self.ctx.max_over_ranks(1.0 - timed_ok)
+
+        f = sl.fuse
         n, cols, steps = max(64, 2 * f * self.ctx.world + 8), 200, 4 * f
         small = StencilSlab(self.ctx, n, cols, fuse=f)
         small.run(steps, self.overlap)
@@ -166,8 +187,9 @@ class Stencil(Workload):
             ref = reference_run(n, steps, cols, device=self.ctx.device)
             ok = float(torch.equal(full.view(torch.int16), ref.view(torch.int16)))
         ok = self.ctx.broadcast_(self.ctx.scalar(ok)).item()
-        finite = float(torch.isfinite(self.slab.interior().float()).all())
-        return {"bit_exact_vs_single_step_oracle": bool(ok),
+        finite = float(torch.isfinite(mine.float()).all())
+        return {"timed_grid_bit_exact": bool(timed_ok == 1.0), "timed_grid_updates": sl.steps_done,
+                "bit_exact_vs_single_step_oracle": bool(ok),
                 "finite": bool(self.ctx.max_over_ranks(1.0 - finite) == 0.0)}
 
 
@@ -195,10 +217,9 @@ class SpMV(Workload):
         self.y = self.d.step_padded(self.xp)
 
     def check(self):
-        got = self.y[self.d.local_positions()].double()
-        ref = self.d.reference_local(self.xp)
-        err = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item() if ref.numel() else 0.0
-        return {"max_rel_err_vs_fp64": self.ctx.max_over_ranks(err)}
+        """Every entry of the timed step's output layout (own rows AND the ghost entries the exchange wrote) against
+        the fp64 product of its owner's row."""
+        return {"max_rel_err_vs_fp64": self.d.layout_max_rel_err(self.y, self.xp)}
 
     def work_per_step(self):
         return 2.0 * self.d.local_nnz

@@ -74,14 +74,19 @@ def reduce(x: torch.Tensor, op: str = "sum") -> torch.Tensor:
     return x.min() if op == "min" else x.max()
 
 
-def scan(x: torch.Tensor, exclusive: bool = False, init: torch.Tensor | None = None) -> torch.Tensor:
+def scan(x: torch.Tensor, exclusive: bool = False, init: torch.Tensor | None = None,
+         check: bool = False) -> torch.Tensor:
     """Prefix sum over the flattened tensor (decoupled look-back single pass on the GPU).
 
     ``init`` (a 1-element float32 tensor on the same device) is added to every output; the multi-GPU
-    scan feeds its rank offset through it without a host round trip.
+    scan feeds its rank offset through it without a host round trip. ``check=True`` waits for the current
+    stream and raises if this (or an earlier unchecked) scan on it gave up a look-back (scan_check).
     """
     if x.is_cuda:
-        return ops().scan(x, exclusive, init)
+        y = ops().scan(x, exclusive, init)
+        if check:
+            scan_check(x.device)
+        return y
     xf = _f32(x, "x").view(-1)
     out = torch.cumsum(xf.double(), 0)
     if exclusive:
@@ -89,6 +94,12 @@ def scan(x: torch.Tensor, exclusive: bool = False, init: torch.Tensor | None = N
     if init is not None:
         out = out + init.double().view(-1)[0]
     return out.float().view(x.shape)
+
+
+def scan_check(device=None) -> None:
+    """Synchronise the current stream of `device` and raise if a scan on it timed out in its look-back."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    ops().scan_check(dev.index if dev.index is not None else torch.cuda.current_device())
 
 
 def fill_(x: torch.Tensor, value: float) -> torch.Tensor:

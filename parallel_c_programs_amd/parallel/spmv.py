@@ -292,3 +292,23 @@ class DistributedSpMV:
                 y.index_add_(0, rows, part.val.double().to(xp.device) * xp.double()[part.col.long().to(xp.device)])
                 outs.append(y)
         return torch.cat(outs) if outs else torch.zeros(0, dtype=torch.float64, device=xp.device)
+
+    def layout_max_rel_err(self, y: torch.Tensor, xp: torch.Tensor) -> float:
+        """Max relative error of EVERY entry of the layout vector y = A xp against fp64: own rows and the ghost
+        entries the exchange delivered (each compared with its owner's fp64 row, gathered once), i.e. the
+        product and the exchange that the timed step performs. Same value on every rank."""
+        ref = self.reference_local(xp)
+        if self.ctx.distributed:
+            buf = torch.zeros(self.block, dtype=torch.float64, device=ref.device)
+            buf[:ref.numel()] = ref
+            parts = self.ctx.all_gather(buf)
+            full = torch.cat([p[:self.cuts[q + 1] - self.cuts[q]] for q, p in enumerate(parts)])
+        else:
+            full = ref
+        ids = self.layout_ids()
+        m = ids >= 0
+        got, want = y[m].double(), full[ids[m]]
+        scale = full.abs().max().clamp_min(1e-30) if full.numel() else torch.ones((), dtype=torch.float64)
+        err = ((got - want).abs().max() / scale).item() if want.numel() else 0.0
+        return self.ctx.max_over_ranks(err)
+

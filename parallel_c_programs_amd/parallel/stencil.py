@@ -178,3 +178,15 @@ def reference_run(n: int, steps: int, cols: int | None = None, k: float = DEFAUL
         stencil5_step_(u, v, 0, n, k)
         u, v = v, u
     return u[1:-1]
+
+
+def reference_run_torch(n: int, steps: int, cols: int | None = None, k: float = DEFAULT_K, device="cpu") -> torch.Tensor:
+    """Single-domain run on plain PyTorch f32 ops (ops.stencil5_reference: no HIP kernel involved), the oracle of
+    the bench's timed-grid check."""
+    from ..ops.stencil import stencil5_reference
+
+    cols = n if cols is None else cols
+    u = init_grid(n, cols, 0, n, device=device)
+    for _ in range(steps):
+        u = stencil5_reference(u, 0, n, k)
+    return u[1:-1]

@@ -42,3 +42,37 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, variant: int, out: torch.Tensor | No
     if rc:
         raise RuntimeError(f"lab sgemm variant {variant}: rc {rc}")
     return c
+
+
+_libs = {}
+
+
+def lab_lib(name: str, entry: str) -> ctypes.CDLL:
+    """Build scripts/<name>.hip into build/lab/lib<name>.so (on the box that runs it) and bind `entry` with the
+    variant-launcher signature (A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, variant, stream)."""
+    if name not in _libs:
+        src = ROOT / "scripts" / f"{name}.hip"
+        so = ROOT / "build" / "lab" / f"lib{name}.so"
+        if not so.exists() or so.stat().st_mtime < src.stat().st_mtime:
+            so.parent.mkdir(parents=True, exist_ok=True)
+            subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-shared", "--offload-arch=gfx950",
+                            f"-I{ROOT / 'csrc/include'}", f"-I{ROOT / 'csrc/runtime'}", str(src), "-o", str(so)],
+                           check=True)
+        torch.cuda.init()
+        lib = ctypes.CDLL(str(so))
+        fn = getattr(lib, entry)
+        fn.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 6 + [ctypes.c_float] * 2 + [ctypes.c_int, ctypes.c_void_p]
+        _libs[name] = fn
+    return _libs[name]
+
+
+def sgemm_dr(a: torch.Tensor, b: torch.Tensor, variant: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    fn = lab_lib("sgemm_dr_lab", "pcmx_sgemm_dr_lab_variant")
+    m, k = a.shape
+    n = b.shape[1]
+    c = torch.empty(m, n, device=a.device) if out is None else out
+    rc = fn(a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, a.stride(0), b.stride(0), c.stride(0), 1.0, 0.0, variant,
+            torch.cuda.current_stream(a.device).cuda_stream)
+    if rc:
+        raise RuntimeError(f"dr lab sgemm variant {variant}: rc {rc}")
+    return c
