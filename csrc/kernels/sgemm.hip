@@ -1,8 +1,13 @@
 // FP32 SGEMM on the gfx950 matrix cores — the headline "TFLOPS SGEMM 8192^2" kernel.
 // Reference ancestor: matrix_multiply, ref 1-introduction/matrix.c:63-81 (naive i-j-k on float**).
 //
-// Production kernels only (every experimental variant and tuning knob lives in scripts/sgemm_lab.hip):
-//   variant 16  register-staged 256x256x32 tile, 8 waves (2 per SIMD, 64x128 wave tiles) — large problems
+// Production kernels only (experimental variants and tuning knobs live in scripts/sgemm_lab.hip and
+// scripts/sgemm_dr_lab.hip):
+//   variant 17  persistent LDS-free "direct register" kernel, 4 waves (one per SIMD, 128x128 wave tiles) —
+//               large problems (round 3; 8192^3: 153.7-154.0 TFLOPS vs hipBLASLt 153.3-153.8 on the same box,
+//               both ~99% of the 155 TF measured f32 MFMA peak; scripts/sgemm_dr_ab.py)
+//   variant 18  variant 17 with the grid capped at 7 blocks (tests: many tiles per block, uneven split)
+//   variant 16  register-staged 256x256x32 tile, 8 waves (2 per SIMD, 64x128 wave tiles) — round-2 production
 //   variant 0   LDS-DMA 256x256x32 tile, 8 waves — fallback when buffer offsets would exceed 2 GiB
 //   variant 1   LDS-DMA 128x128x32 tile, 4 waves — problems with fewer than 192 256x256 tiles (fills 256 CUs)
 //   simt        reference-style f32 VALU GEMM (the "CUDA port recompiled" baseline), any shape
@@ -363,6 +368,150 @@ __global__ __launch_bounds__(CfgRS8::kThreads, 1) void sgemm_rs_kernel(const flo
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Variant 17 (production for large problems): persistent, LDS-free "direct register" kernel.
+// v_mfma_f32_32x32x2_f32 needs ONE operand VGPR per 2048 MACs, so a 128x128 wave tile (4x4 MFMA tiles, 256
+// accumulators) consumes only 8 operand VGPRs per 16 MFMAs (1024 SIMD cycles). That is few enough to load the
+// operands straight from L2 into the MFMA operand registers: no LDS stage, no ds_write/ds_read, no workgroup
+// barrier. Each of the 4 waves (one per SIMD, 512 registers) is an independent MFMA stream whose loads are
+// issued ~8k cycles ahead. Counters (profiles/r3_sgemm/): 98.3-98.5% of the kernel's cycles are MFMA-busy
+// against 96.4% for variant 16 (barrier stalls of its 8-wave LDS pipeline) and 97.9% for hipBLASLt.
+//  * MFMA step t of a 32-k chunk feeds k-slot h (= lane >> 5) with k = k0 + 16h + t.
+//  * A: lane (l32, h) loads A[row l32][k0 + 16h + 4q .. +3] (q = 0..3, issued back to back: the four loads share
+//    each row's 128-B line); component s is the operand of step 4q + s. Double-buffered per chunk.
+//  * B: lane (l32, h) loads B[k0 + 16h + t][c0 + 4 l32 .. +3]: N-tile j owns columns c0 + 4c + j, so one 16-B load
+//    holds the operands of the wave's 4 N-tiles (two 512-B row segments per instruction). 8-step register ring.
+//  * Persistent: grid = min(tiles, CUs); block b runs tiles j * grid + xcd_remap(b). In a tile's last iteration
+//    the look-ahead loads already fetch the next tile's chunk 0 / steps 0-7 (every tile-dependent address is a
+//    scalar soffset over one buffer resource per operand), so the next tile starts with its operands in flight
+//    and the epilogue's C stores drain under its MFMAs.
+//  * The prologue's B loads are pinned in step order so the loop-top wait (merged over the prologue and the back
+//    edge) stays vmcnt(7); the epilogue issues one store at a time (bounded live registers, no spills).
+template <bool BETA>
+__global__ __launch_bounds__(256, 1) void sgemm_direct_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                              float* __restrict__ C, int M, int N, int K, int lda,
+                                                              int ldb, int ldc, float alpha, float beta) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = pcmx::lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int ntiles = (M / 256) * (N / 256), grid = (int)gridDim.x;
+    const int xid = pcmx::xcd_remap((int)blockIdx.x, grid);
+
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, 0x7fffffff, 0x00020000);
+    int voA[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) voA[i] = ((32 * i + l32) * lda + 16 * h) * 4;
+    const int voB = (16 * h * ldb + 4 * l32) * 4;
+    const int voC = (4 * h * ldc + 4 * l32) * 4;
+    const int nk = K / 32;
+    const int ldb128 = ldb * 128;  // bytes per 32 k-rows of B
+    auto bload = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+        return __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+    };
+
+    // scalar byte bases of the block's tile j (past the end: the block's last tile, loaded and never used)
+    auto bases = [&](int j, int& ab, int& bb, int& m0, int& n0) {
+        int T = j * grid + xid;
+        if (T >= ntiles) T = ((ntiles - 1 - xid) / grid) * grid + xid;
+        const int tiles_n = N / 256, per_group = 8 * tiles_n, first_m = (T / per_group) * 8;
+        const int gsz = min(M / 256 - first_m, 8);
+        m0 = __builtin_amdgcn_readfirstlane((first_m + (T % per_group) % gsz) * 256);
+        n0 = __builtin_amdgcn_readfirstlane(((T % per_group) / gsz) * 256);
+        ab = __builtin_amdgcn_readfirstlane((m0 + wm * 128) * lda * 4);
+        bb = __builtin_amdgcn_readfirstlane((n0 + wn * 128) * 4);
+    };
+
+    pcmx::f32x4 a[2][4][4];  // [chunk parity][M-tile i][q]
+    pcmx::f32x4 b[8];        // ring: step t's B operands in slot t % 8
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0};
+    auto pin = [](auto&& f) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        f();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    int ab, bb, m0, n0;
+    bases(0, ab, bb, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[0][i][q] = bload(rA, voA[i] + 16 * q, ab);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) pin([&] { b[t] = bload(rB, voB, bb + t * ldb * 4); });
+
+    int jt = 0;
+    do {  // grid <= tiles: every block has a tile; nk >= 2 (K % 64 == 0)
+        int abn, bbn, m0n, n0n;
+        bases(jt + 1, abn, bbn, m0n, n0n);
+        int kc = 0;
+        do {
+            const bool last = kc + 2 == nk;
+            // chunk p = 0: every look-ahead load stays inside the tile
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][i][t >> 2][t & 3], b[t & 7][j], acc[i][j], 0, 0, 0);
+                    if (i == 3)  // after the step's last read of slot t % 8
+                        pin([&] {
+                            const int so = t + 8 < 16 ? kc * ldb128 + (t + 8) * ldb * 4 : (kc + 1) * ldb128 + (t - 8) * ldb * 4;
+                            b[t & 7] = bload(rB, voB, bb + so);
+                        });
+                    if (t < 4) pin([&] { a[1][t][i] = bload(rA, voA[t] + 16 * i, ab + (kc + 1) * 128); });
+                }
+            }
+            // chunk p = 1: in the tile's last iteration the look-ahead crosses into the next tile
+            const int aso = last ? abn : ab + (kc + 2) * 128;
+            const int bso = last ? bbn : bb + (kc + 2) * ldb128;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][i][t >> 2][t & 3], b[t & 7][j], acc[i][j], 0, 0, 0);
+                    if (i == 3)
+                        pin([&] {
+                            const int so = t + 8 < 16 ? bb + (kc + 1) * ldb128 + (t + 8) * ldb * 4 : bso + (t - 8) * ldb * 4;
+                            b[t & 7] = bload(rB, voB, so);
+                        });
+                    if (t < 4) pin([&] { a[0][t][i] = bload(rA, voA[t] + 16 * i, aso); });
+                }
+            }
+            kc += 2;
+        } while (kc < nk);
+        // epilogue of tile jt: lane (l32, h) holds column l32 of each N-tile j (= c0 + 4 l32 + j) and rows
+        // 4h + (r & 3) + 8 (r >> 2) of each 32x32 tile, so the 4 N-tiles form one 16-B store; the row goes in soffset
+        const int r0 = m0 + wm * 128, c0 = n0 + wn * 128;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int so = ((r0 + i * 32 + (r & 3) + 8 * (r >> 2)) * ldc + c0) * 4;
+                pcmx::f32x4 v{alpha * acc[i][0][r], alpha * acc[i][1][r], alpha * acc[i][2][r], alpha * acc[i][3][r]};
+                if constexpr (BETA) v += beta * bload(rC, voC, so);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rC, voC, so, 0);
+                __builtin_amdgcn_sched_barrier(0);  // one store at a time: bounded live registers
+            }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0};
+        ab = abn, bb = bbn, m0 = m0n, n0 = n0n;
+        ++jt;
+    } while (xid + jt * grid < ntiles);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Reference-style SIMT kernel (f32 VALU FMAs, 64x64 LDS tiles, 4x4 outputs per thread) — the "CUDA port
 // recompiled" baseline the MFMA kernel is compared against. Any shape.
 constexpr int kSimtT = 64;
@@ -435,6 +584,33 @@ int launch_rs(const float* A, const float* B, float* Cm, int M, int N, int K, in
         sgemm_rs_kernel<false><<<grid, C::kThreads, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     return (int)hipGetLastError();
 }
+int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+    return cus[dev] > 0 ? cus[dev] : 256;
+}
+
+// max_blocks <= 0: one block per CU
+int launch_direct(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+                  float beta, int max_blocks, hipStream_t s) {
+    if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 64) return PCMX_ERR_ARG;
+    if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return PCMX_ERR_ARG;
+    // every scalar byte offset (A row base + k, B k-row + column, C row + column) must stay below 2^31
+    if ((long long)M * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31) ||
+        (long long)M * ldc * 4 >= (1LL << 31))
+        return PCMX_ERR_ARG;
+    const int tiles = (M / 256) * (N / 256);
+    int grid = max_blocks > 0 ? max_blocks : device_cus();
+    if (grid > tiles) grid = tiles;
+    if (beta != 0.f)
+        sgemm_direct_kernel<true><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+    else
+        sgemm_direct_kernel<false><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+    return (int)hipGetLastError();
+}
 }  // namespace
 
 extern "C" int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
@@ -443,17 +619,22 @@ extern "C" int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, 
         case 0: return launch_dma<Big>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 1: return launch_dma<Small>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 16: return launch_rs(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 17: return launch_direct(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 0, s);
+        case 18: return launch_direct(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 7, s);
         default: return PCMX_ERR_ARG;
     }
 }
 
 extern "C" int pcmx_sgemm_f32(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
                               float alpha, float beta, hipStream_t s) {
-    // 256x256 tiles when the grid fills the 256 CUs (register-staged variant 16; the LDS-DMA variant 0 when its
-    // 32-bit buffer offsets do not reach), otherwise the 128x128 kernel (4x more tiles).
+    // 256x256 tiles when the grid fills the 256 CUs: the persistent direct-register variant 17 (K % 64 == 0 and
+    // 32-bit scalar offsets), else register-staged variant 16, else the LDS-DMA variant 0; otherwise the 128x128
+    // kernel (4x more tiles).
     const bool big_ok = tile_aligned<Big>(M, N, K) && (long long)(M / 256) * (N / 256) >= 192;
     if (big_ok) {
-        const int rc = launch_rs(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        int rc = launch_direct(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 0, s);
+        if (rc != PCMX_ERR_ARG) return rc;
+        rc = launch_rs(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         return rc == PCMX_ERR_ARG ? launch_dma<Big>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s) : rc;
     }
     return launch_dma<Small>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);

@@ -149,7 +149,7 @@ int launch_dr(const float* A, const float* B, float* Cm, int M, int N, int K, in
 // tile's chunk 0 / steps 0-7, so the next tile starts with its operands in flight and the epilogue's C stores drain
 // under the next tile's MFMAs (no per-tile prologue latency, no chip-wide synchronous store burst). Every
 // tile-dependent address is a scalar byte offset (soffset) over one buffer resource per operand.
-template <bool BETA, int GM>
+template <bool BETA, int GM, int DIAG = 0>  // DIAG 1: no C stores (diagnostic only: wrong results)
 __global__ __launch_bounds__(256, 1) void sgemm_drp_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                            float* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                            int ldc, float alpha, float beta) {
@@ -257,7 +257,11 @@ __global__ __launch_bounds__(256, 1) void sgemm_drp_kernel(const float* __restri
                 const int so = ((r0 + i * 32 + (r & 3) + 8 * (r >> 2)) * ldc + c0) * 4;
                 f32x4 v{alpha * acc[i][0][r], alpha * acc[i][1][r], alpha * acc[i][2][r], alpha * acc[i][3][r]};
                 if constexpr (BETA) v += beta * bload(rC, voC, so);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pcmx_v4u, v), rC, voC, so, 0);
+                if constexpr (DIAG == 1) {
+                    if (v[0] == 1234.5f && v[1] == -1.f) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pcmx_v4u, v), rC, voC, so, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pcmx_v4u, v), rC, voC, so, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);  // one store at a time: bounded live VGPRs (no spills)
             }
 #pragma unroll
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(256, 1) void sgemm_drp_kernel(const float* __restri
     } while (xid + j * grid < ntiles);
 }
 
-template <int GM>
+template <int GM, int DIAG = 0>
 int launch_drp(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                float beta, hipStream_t s) {
     if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 64) return 1;
@@ -282,9 +286,158 @@ int launch_drp(const float* A, const float* B, float* Cm, int M, int N, int K, i
     const int tiles = (M / 256) * (N / 256);
     const int grid = tiles < cus ? tiles : cus;
     if (beta != 0.f)
-        sgemm_drp_kernel<true, GM><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_drp_kernel<true, GM, DIAG><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     else
-        sgemm_drp_kernel<false, GM><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_drp_kernel<false, GM, DIAG><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+    return (int)hipGetLastError();
+}
+// Persistent, v_mfma_f32_16x16x4_f32 form (the shape hipBLASLt's fp32 kernel uses): 8x8 MFMA tiles of 16x16 per
+// 128x128 wave tile (256 accumulators). MFMA step t of a 32-k chunk feeds k-slot g (= lane >> 4) with
+// k = k0 + 8g + t.
+//  * A: lane (l, g) loads A[row l][k0 + 8g + 4q .. +3] (q = 0, 1): one 16-row instruction covers half of each row's
+//    128-B chunk line, the q = 1 load the other half.
+//  * B: N-tile j < 4 owns columns c0 + 4c + j, tile j >= 4 owns c0 + 64 + 4c + (j - 4) (c = lane & 15), so a lane's
+//    two 16-B loads per k-row are 256 contiguous bytes per k-slot each, and the epilogue stores 16 B per lane.
+template <bool BETA, int GM>
+__global__ __launch_bounds__(256, 1) void sgemm_drp16_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                             float* __restrict__ C, int M, int N, int K, int lda, int ldb,
+                                                             int ldc, float alpha, float beta) {
+    const int lane = (int)__lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int g = lane >> 4, l = lane & 15;
+    const int ntiles = (M / 256) * (N / 256), grid = (int)gridDim.x;
+    const int xid = xcd_remap((int)blockIdx.x, grid);
+
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, 0x7fffffff, 0x00020000);
+    const int voA = (l * lda + 8 * g) * 4;        // + tile i: 16 i lda * 4 (SGPR), + q: 16 q (imm)
+    const int voB = (8 * g * ldb + 4 * l) * 4;    // + half: 256 B (imm)
+    const int voC = (4 * g * ldc + 4 * l) * 4;
+    const int nk = K / 32;
+    const int ldb128 = ldb * 128, lda64 = lda * 64;
+
+    auto bases = [&](int j, int& ab, int& bb, int& m0, int& n0) {
+        int T = j * grid + xid;
+        if (T >= ntiles) T = ((ntiles - 1 - xid) / grid) * grid + xid;
+        tile_coords<256, 256, GM>(T, M, N, m0, n0);
+        m0 = __builtin_amdgcn_readfirstlane(m0);
+        n0 = __builtin_amdgcn_readfirstlane(n0);
+        ab = __builtin_amdgcn_readfirstlane((m0 + wm * 128) * lda * 4);
+        bb = __builtin_amdgcn_readfirstlane((n0 + wn * 128) * 4);
+    };
+
+    f32x4 a[2][8][2];  // [chunk parity][tile i][q]
+    f32x4 b[4][2];     // ring: step t's B operands (columns c0+4l.., c0+64+4l..) in slot t % 4
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0};
+    auto pin = [](auto&& f) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        f();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto ldA = [&](int i, int q, int so) { return bload(rA, voA + 16 * q, so + i * lda64); };
+    auto ldB = [&](int half, int so) { return bload(rB, voB + 256 * half, so); };
+
+    int ab, bb, m0, n0;
+    bases(0, ab, bb, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) a[0][i][q] = ldA(i, q, ab);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        pin([&] {
+            b[t][0] = ldB(0, bb + t * ldb * 4);
+            b[t][1] = ldB(1, bb + t * ldb * 4);
+        });
+
+    int jt = 0;
+    do {
+        int abn, bbn, m0n, n0n;
+        bases(jt + 1, abn, bbn, m0n, n0n);
+        int kc = 0;
+        do {
+            const bool last = kc + 2 == nk;
+            const int aso1 = last ? abn : ab + (kc + 2) * 128;
+            const int bso1 = last ? bbn : bb + (kc + 2) * ldb128;
+            auto chunk = [&](auto pc) __attribute__((always_inline)) {
+                constexpr int p = decltype(pc)::value;
+                // look-ahead targets: A of the next chunk; B of step t + 4
+                const int aso = p == 0 ? ab + (kc + 1) * 128 : aso1;
+                const int bcur = bb + (kc + p) * ldb128, bnext = p == 0 ? bb + (kc + 1) * ldb128 : bso1;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p][i][t >> 2][t & 3], b[t & 3][j >> 2][j & 3],
+                                                                             acc[i][j], 0, 0, 0);
+                        if (t < 4 && (i == 1 || i == 4))  // next chunk's A in steps 0-3: >= 4 steps ahead
+                            pin([&] {
+                                const int ti = 2 * t + (i == 4);
+                                a[p ^ 1][ti][0] = ldA(ti, 0, aso);
+                                a[p ^ 1][ti][1] = ldA(ti, 1, aso);
+                            });
+                        if (i == 7)
+                            pin([&] {
+                                const int so = t + 4 < 8 ? bcur + (t + 4) * ldb * 4 : bnext + (t - 4) * ldb * 4;
+                                b[t & 3][0] = ldB(0, so);
+                                b[t & 3][1] = ldB(1, so);
+                            });
+                    }
+                }
+            };
+            chunk(std::integral_constant<int, 0>{});
+            chunk(std::integral_constant<int, 1>{});
+            kc += 2;
+        } while (kc < nk);
+        // epilogue: tile (i, j) lane (l, g) holds column col(j, l), rows 16 i + 4 g + r
+        const int r0 = m0 + wm * 128, c0 = n0 + wn * 128;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    const int so = ((r0 + 16 * i + r) * ldc + c0 + 64 * hf) * 4;
+                    f32x4 v{alpha * acc[i][4 * hf][r], alpha * acc[i][4 * hf + 1][r], alpha * acc[i][4 * hf + 2][r],
+                            alpha * acc[i][4 * hf + 3][r]};
+                    if constexpr (BETA) v += beta * bload(rC, voC, so);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pcmx_v4u, v), rC, voC, so, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0};
+        ab = abn, bb = bbn, m0 = m0n, n0 = n0n;
+        ++jt;
+    } while (xid + jt * grid < ntiles);
+}
+
+template <int GM>
+int launch_drp16(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+                 float beta, hipStream_t s) {
+    if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 64) return 1;
+    if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)Cm) & 15)) return 1;
+    if ((long long)M * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31) ||
+        (long long)M * ldc * 4 >= (1LL << 31))
+        return 1;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int tiles = (M / 256) * (N / 256);
+    const int grid = tiles < cus ? tiles : cus;
+    if (beta != 0.f)
+        sgemm_drp16_kernel<true, GM><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+    else
+        sgemm_drp16_kernel<false, GM><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     return (int)hipGetLastError();
 }
 }  // namespace
@@ -297,6 +450,8 @@ extern "C" int pcmx_sgemm_dr_lab_variant(const float* A, const float* B, float* 
         case 32: return launch_dr<0, 4>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 33: return launch_dr<0, 16>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 34: return launch_drp<8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 35: return launch_drp<8, 1>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 36: return launch_drp16<8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         default: return 1;
     }
 }

@@ -1,5 +1,5 @@
 """SGEMM lab: fixed (K-independent) cost per launch — prologue, epilogue, tail, launch — from a linear fit of
-time vs K at M = N = 8192 (production variant 16, lab variant 19, hipBLASLt)."""
+time vs K at M = N = 8192 (production variant 16, direct-register lab variants 30/34/35, hipBLASLt)."""
 import json
 import sys
 from pathlib import Path
@@ -32,10 +32,11 @@ for rnd in range(3):
         a = torch.rand(n, k, device="cuda") * 2 - 1
         b = torch.rand(k, n, device="cuda") * 2 - 1
         c = torch.empty(n, n, device="cuda")
-        for name, fn in (("v16", lambda: ops.sgemm_out(a, b, c)), ("v19", lambda: _lab.sgemm(a, b, 19, c)),
+        for name, fn in (("v16", lambda: ops.sgemm_out(a, b, c)), ("dr30", lambda: _lab.sgemm_dr(a, b, 30, c)),
+                         ("drp34", lambda: _lab.sgemm_dr(a, b, 34, c)), ("drp35_nostore", lambda: _lab.sgemm_dr(a, b, 35, c)),
                          ("torch", lambda: torch.matmul(a, b, out=c))):
             res.setdefault((name, k), []).append(t_ms(fn))
-for name in ("v16", "v19", "torch"):
+for name in ("v16", "dr30", "drp34", "drp35_nostore", "torch"):
     pts = [(k, min(res[(name, k)])) for k in Ks]
     nk = len(pts)
     mk = sum(k for k, _ in pts) / nk

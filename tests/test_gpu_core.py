@@ -128,7 +128,7 @@ def test_scan_schedules_exact(gpu, variant):
             assert torch.equal(y.double(), want), (m, exclusive)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 16])
+@pytest.mark.parametrize("variant", [0, 1, 16, 17, 18])
 def test_sgemm_identity_asymmetric(gpu, variant):
     # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
     n = 256
@@ -140,7 +140,7 @@ def test_sgemm_identity_asymmetric(gpu, variant):
     assert torch.equal(c2, b)
 
 
-@pytest.mark.parametrize("variant", [0, 16])
+@pytest.mark.parametrize("variant", [0, 16, 17, 18])
 def test_sgemm_register_staged_multitile_vs_fp64(gpu, variant):
     # several tiles in both directions and 2+ LDS stages of prefetch: M != N != K
     g = torch.Generator(device=gpu).manual_seed(variant)
@@ -161,6 +161,25 @@ def test_sgemm_vs_fp64(gpu, shape):
     scale = (a.abs().double() @ b.abs().double())
     err = ((c.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
     assert err < 4e-6 * max(1.0, (k / 256) ** 0.5)
+
+
+@pytest.mark.parametrize("shape", [(768, 1280, 512), (4352, 4096, 128)])
+def test_sgemm_direct_persistent_many_tiles(gpu, shape):
+    """Variant 18 caps the persistent direct kernel at 7 blocks (2-3 tiles per block at 768x1280; the cross-tile
+    look-ahead and the past-the-end clamp); 4352x4096 runs 272 tiles on the production grid (one block per CU, some
+    blocks two tiles). alpha/beta through the same epilogue."""
+    m, n, k = shape
+    g = torch.Generator(device=gpu).manual_seed(m + n)
+    a = torch.rand(m, k, device=gpu, generator=g) * 2 - 1
+    b = torch.rand(k, n, device=gpu, generator=g) * 2 - 1
+    c0 = torch.rand(m, n, device=gpu, generator=g)
+    ref = 1.5 * (a.double() @ b.double()) - 0.25 * c0.double()
+    for variant in (17, 18):
+        out = ops.sgemm_out(a, b, c0.clone(), alpha=1.5, beta=-0.25, variant=variant)
+        err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
+        assert err < 1e-5, (variant, err)
+        plain = ops.sgemm(a, b, variant=variant)
+        assert torch.equal(plain, ops.sgemm(a, b, variant=17 if variant == 18 else 18))  # same sums, any grid
 
 
 def test_sgemm_beta(gpu):
