@@ -21,6 +21,8 @@ by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harne
            ghost exchange (only the x entries each rank's nonzeros reference, grouped per-peer send/recv) chunked
            and overlapped with the product; fp64 check of every rank's rows
   (N > 1)  256 MiB RCCL all-reduce bus bandwidth
+  vendor   every section carries the vendor library on the same data, timed identically: hipBLASLt
+           (torch.matmul), rocPRIM (torch.sum, torch.cumsum), hipSPARSE (torch sparse CSR x vector)
 
 rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra
 fields of the same line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
@@ -136,6 +138,16 @@ def main(argv=None):
             out[f"{name}_{mode}_gbps"] = _r(rep["value"], 1)
             out[f"{name}_{mode}_ms_per_step"] = _r(rep["ms_per_step"])
             out[f"{name}_{mode}_rel_err_vs_fp64"] = ctx.max_over_ranks(w.check()["rel_err_vs_fp64"])
+            if mode == "weak" and not args.no_ref and dev.type == "cuda":
+                # the vendor library on the same per-GPU data, timed exactly like our kernel (rocPRIM behind both)
+                if name == "reduce":
+                    t_ref = timed(ctx, lambda: torch.sum(w.x), K, Wm)
+                    out["torch_sum_gbps"] = _r(world * 4.0 * w.x.numel() * K / t_ref / 1e9, 1)
+                else:
+                    ybuf = torch.empty_like(w.x)
+                    t_ref = timed(ctx, lambda: torch.cumsum(w.x, 0, out=ybuf), K, Wm)
+                    out["torch_cumsum_gbps"] = _r(world * 8.0 * w.x.numel() * K / t_ref / 1e9, 1)
+                    del ybuf
             if name == "scan":  # every timed output checked (not a prefix), rank offsets included
                 out["scan_full_max_rel_err_vs_fp64"] = max(out.get("scan_full_max_rel_err_vs_fp64", 0.0),
                                                            out[f"scan_{mode}_rel_err_vs_fp64"])
@@ -160,14 +172,26 @@ def main(argv=None):
 
     # ---- SpMV 1e8-nnz power-law graph, strong scaling
     if "spmv" in sections:
+        vendor = not args.no_ref and dev.type == "cuda"
         sp = W.SpMV(ctx, n_rows=int(args.spmv_rows), nnz=int(args.spmv_nnz), chunks=args.spmv_chunks,
-                    exchange=args.spmv_exchange)
+                    exchange=args.spmv_exchange, keep_plain=vendor)
         t = timed(ctx, sp.step, K, Wm)
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
                     "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks, "spmv_slices": sp.d.slices,
                     "spmv_exchange": sp.d.exchange if ctx.distributed else None,
                     "spmv_max_rel_err_vs_fp64": sp.check()["max_rel_err_vs_fp64"]})
+        if vendor:  # hipSPARSE (torch sparse CSR x dense vector) on each rank's own rows, the same matrix and x
+            try:
+                A = sp.d.vendor_matrix()
+                yv = torch.mv(A, sp.xp)
+                t_ref = timed(ctx, lambda: torch.mv(A, sp.xp), K, Wm)
+                nnz_all = ctx.scalar(float(sp.d.local_nnz))
+                ctx.all_reduce_(nnz_all)
+                out["torch_sparse_csr_gflops"] = _r(2.0 * nnz_all.item() * K / t_ref / 1e9, 2)
+                del A, yv
+            except Exception as e:  # the line says so instead of dropping the bar
+                out["torch_sparse_csr_gflops"] = f"unsupported on this torch build: {type(e).__name__}: {e}"[:200]
         del sp
         free()
         log(f"spmv {out['spmv_gflops']} GFLOP/s")

@@ -199,12 +199,13 @@ class SpMV(Workload):
     layout with exchange="allgather"). Strong scaling: one fixed matrix."""
 
     def __init__(self, ctx, n_rows=10_000_000, nnz=100_000_000, alpha=2.5, slices=-1, head=0.0625,
-                 balance=0.0, chunks=0, exchange="ghost", **_):
+                 balance=0.0, chunks=0, exchange="ghost", keep_plain=False, **_):
         from ..parallel.spmv import DistributedSpMV
 
         slices = int(slices) if ctx.device.type == "cuda" else 0
         self.d = DistributedSpMV.powerlaw(ctx, n_rows, nnz, alpha, slices=slices, head=float(head),
-                                          balance=float(balance), chunks=int(chunks) or None, exchange=exchange)
+                                          balance=float(balance), chunks=int(chunks) or None, exchange=exchange,
+                                          keep_plain=keep_plain)
         slices = self.d.slices
         super().__init__(ctx, {"n_rows": n_rows, "nnz": nnz, "slices": slices, "head": head,
                                "chunks": self.d.chunks}, "spmv", "GFLOP/s")

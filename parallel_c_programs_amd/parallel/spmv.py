@@ -64,7 +64,7 @@ def auto_slices(n_cols: int) -> int:
 class DistributedSpMV:
     def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
                  head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 0,
-                 exchange: str = "ghost"):
+                 exchange: str = "ghost", keep_plain: bool = False):
         W, dev = ctx.world, ctx.device
         if exchange not in ("ghost", "allgather"):
             raise ValueError("exchange: 'ghost' or 'allgather'")
@@ -91,6 +91,9 @@ class DistributedSpMV:
         else:
             col = self._ghost_layout(col)
         m = CSR(local.row_ptr.to(dev), col, local.val.to(dev), self.n_pad)
+        # keep_plain: the rank's rows as one plain CSR in layout columns (the vendor-library baseline: torch sparse
+        # CSR x dense vector = hipSPARSE on ROCm)
+        self.plain = m if keep_plain else None
         if slices < 0:
             slices = auto_slices(self.n_pad)
         self.slices = slices
@@ -102,7 +105,9 @@ class DistributedSpMV:
             if dev.type == "cuda":
                 part = SlicedCSR(part, slices, head, balance, item_nnz) if self.sliced else part.plan()
             self.parts.append((a, b, part))
-        del m, col
+        del col
+        if not keep_plain:
+            del m
         if self.exchange == "allgather":
             self.send = torch.zeros(C, self.L, dtype=torch.float32, device=dev)  # tails of short chunks stay 0
         self.bufs = [torch.zeros(self.n_pad, dtype=torch.float32, device=dev) for _ in range(2)]
@@ -174,11 +179,19 @@ class DistributedSpMV:
     @staticmethod
     def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
                  slices: int = 0, head: float = 0.0625, balance: float = 0.0,
-                 chunks: int | None = None, item_nnz: int = 0, exchange: str = "ghost") -> "DistributedSpMV":
+                 chunks: int | None = None, item_nnz: int = 0, exchange: str = "ghost",
+                 keep_plain: bool = False) -> "DistributedSpMV":
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)
-        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz, exchange)
+        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz, exchange, keep_plain)
+
+    def vendor_matrix(self) -> torch.Tensor:
+        """This rank's rows as a torch sparse CSR tensor (layout columns): `torch.mv(A, xp)` runs hipSPARSE."""
+        if self.plain is None:
+            raise ValueError("built without keep_plain=True")
+        m = self.plain
+        return torch.sparse_csr_tensor(m.row_ptr.to(torch.int32), m.col, m.val, size=(m.n_rows, m.n_cols))
 
     @property
     def local_nnz(self) -> int:

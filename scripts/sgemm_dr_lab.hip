@@ -149,7 +149,7 @@ int launch_dr(const float* A, const float* B, float* Cm, int M, int N, int K, in
 // tile's chunk 0 / steps 0-7, so the next tile starts with its operands in flight and the epilogue's C stores drain
 // under the next tile's MFMAs (no per-tile prologue latency, no chip-wide synchronous store burst). Every
 // tile-dependent address is a scalar byte offset (soffset) over one buffer resource per operand.
-template <bool BETA, int GM, int DIAG = 0>  // DIAG 1: no C stores (diagnostic only: wrong results)
+template <bool BETA, int GM, int DIAG = 0, int STAGGER = 0>  // DIAG 1: no C stores (diagnostic only: wrong results)
 __global__ __launch_bounds__(256, 1) void sgemm_drp_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                            float* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                            int ldc, float alpha, float beta) {
@@ -195,6 +195,12 @@ __global__ __launch_bounds__(256, 1) void sgemm_drp_kernel(const float* __restri
         __builtin_amdgcn_sched_barrier(0);
     };
 
+    // STAGGER: waves (wm, wn) start (wm + wn) * STAGGER * 64 cycles late, so the two waves sharing an A row panel
+    // (same wm) or a B column panel (same wn) issue their identical loads one offset apart (L1 hits, not two L2
+    // requests in flight for the same line)
+    if constexpr (STAGGER > 0) {
+        for (int z = 0; z < wm + wn; ++z) __builtin_amdgcn_s_sleep(STAGGER);
+    }
     int ab, bb, m0, n0;
     bases(0, ab, bb, m0, n0);
 #pragma unroll
@@ -273,7 +279,7 @@ __global__ __launch_bounds__(256, 1) void sgemm_drp_kernel(const float* __restri
     } while (xid + j * grid < ntiles);
 }
 
-template <int GM, int DIAG = 0>
+template <int GM, int DIAG = 0, int STAGGER = 0>
 int launch_drp(const float* A, const float* B, float* Cm, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                float beta, hipStream_t s) {
     if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 64) return 1;
@@ -286,9 +292,9 @@ int launch_drp(const float* A, const float* B, float* Cm, int M, int N, int K, i
     const int tiles = (M / 256) * (N / 256);
     const int grid = tiles < cus ? tiles : cus;
     if (beta != 0.f)
-        sgemm_drp_kernel<true, GM, DIAG><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_drp_kernel<true, GM, DIAG, STAGGER><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     else
-        sgemm_drp_kernel<false, GM, DIAG><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
+        sgemm_drp_kernel<false, GM, DIAG, STAGGER><<<grid, 256, 0, s>>>(A, B, Cm, M, N, K, lda, ldb, ldc, alpha, beta);
     return (int)hipGetLastError();
 }
 // Persistent, v_mfma_f32_16x16x4_f32 form (the shape hipBLASLt's fp32 kernel uses): 8x8 MFMA tiles of 16x16 per
@@ -451,6 +457,11 @@ extern "C" int pcmx_sgemm_dr_lab_variant(const float* A, const float* B, float* 
         case 33: return launch_dr<0, 16>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 34: return launch_drp<8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 35: return launch_drp<8, 1>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 37: return launch_drp<8, 0, 8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 38: return launch_drp<8, 0, 16>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 39: return launch_drp<8, 0, 40>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 40: return launch_drp<4, 0, 0>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
+        case 41: return launch_drp<16, 0, 0>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 36: return launch_drp16<8>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         default: return 1;
     }
