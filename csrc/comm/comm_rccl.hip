@@ -89,7 +89,7 @@ int r_sync(pcmx_comm_t* c) {
                     comm_timeout());
             ncclCommAbort(r->comm);
             r->comm = nullptr;
-            return -110;
+            return PCMX_ERR_TIMEOUT;
         }
         usleep(50);
     }
@@ -261,7 +261,7 @@ int d_grow(unsigned char* reg, const unsigned char* img, int h, int w, int thr, 
     const long long need = pcmx_region2d_workspace_bytes(h, w);
     if (need > c->ws_bytes) {
         if (c->ws) hipFree(c->ws);
-        if (hipMalloc(&c->ws, need) != hipSuccess) return -1;
+        if (hipMalloc(&c->ws, need) != hipSuccess) return PCMX_ERR_ALLOC;
         c->ws_bytes = need;
     }
     int launches = 0;
@@ -300,18 +300,18 @@ extern "C" int pcmx_comm_init_env_staged(pcmx_comm_t** out) {
     int rc = pcmx_comm_init_env_tcp(&host);
     if (rc) {
         pcmx_comm_destroy(host);
-        return rc;
+        return pcmx_comm_rc(rc);
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || hipSetDevice(host->local_rank % ndev) != hipSuccess) {
         pcmx_comm_destroy(host);
-        return -20;
+        return PCMX_ERR_COMM;
     }
     StagedImpl* s = new StagedImpl;
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
         delete s;
         pcmx_comm_destroy(host);
-        return -22;
+        return PCMX_ERR_COMM;
     }
     pcmx_comm_t* c = static_cast<pcmx_comm_t*>(calloc(1, sizeof(pcmx_comm_t)));
     c->rank = host->rank, c->world = host->world, c->local_rank = host->local_rank % ndev;
@@ -327,26 +327,26 @@ extern "C" int pcmx_comm_init_env_rccl(pcmx_comm_t** out) {
     int rc = pcmx_comm_init_env_tcp(&host);
     if (rc) {
         pcmx_comm_destroy(host);
-        return rc;
+        return pcmx_comm_rc(rc);
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         pcmx_comm_destroy(host);
-        return -20;
+        return PCMX_ERR_COMM;
     }
     const int dev = env_int("LOCAL_RANK", host->rank) % ndev;
     if (hipSetDevice(dev) != hipSuccess) {
         pcmx_comm_destroy(host);
-        return -21;
+        return PCMX_ERR_COMM;
     }
     ncclUniqueId id;
     if (host->rank == 0 && (rc = rc_of(ncclGetUniqueId(&id)))) {
         pcmx_comm_destroy(host);
-        return rc;
+        return pcmx_comm_rc(rc);
     }
     if ((rc = host->ops->bcast(host, &id, sizeof id, 0))) {
         pcmx_comm_destroy(host);
-        return rc;
+        return pcmx_comm_rc(rc);
     }
     RcclImpl* r = new RcclImpl;
     if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -354,7 +354,7 @@ extern "C" int pcmx_comm_init_env_rccl(pcmx_comm_t** out) {
         if (r->stream) hipStreamDestroy(r->stream);
         delete r;
         pcmx_comm_destroy(host);
-        return rc ? rc : -22;
+        return rc ? pcmx_comm_rc(rc) : PCMX_ERR_COMM;
     }
     pcmx_comm_t* c = static_cast<pcmx_comm_t*>(calloc(1, sizeof(pcmx_comm_t)));
     c->rank = host->rank, c->world = host->world, c->local_rank = dev, c->transport = PCMX_TRANSPORT_RCCL;

@@ -64,7 +64,7 @@ static int write_all(int fd, const void* p, size_t n) {
         ssize_t k = write(fd, c, n);
         if (k < 0) {
             if (errno == EINTR || errno == EAGAIN) continue;
-            return -1;
+            return PCMX_ERR_COMM;
         }
         c += k, n -= (size_t)k;
     }
@@ -75,10 +75,10 @@ static int read_all(int fd, void* p, size_t n) {
     char* c = (char*)p;
     while (n) {
         ssize_t k = read(fd, c, n);
-        if (k == 0) return -1;
+        if (k == 0) return PCMX_ERR_COMM;
         if (k < 0) {
             if (errno == EINTR || errno == EAGAIN) continue;
-            return -1;
+            return PCMX_ERR_COMM;
         }
         c += k, n -= (size_t)k;
     }
@@ -87,7 +87,7 @@ static int read_all(int fd, void* p, size_t n) {
 
 static int listen_on(const char* addr, int port, int* bound_port) {
     int fd = socket(AF_INET, SOCK_STREAM, 0);
-    if (fd < 0) return -1;
+    if (fd < 0) return PCMX_ERR_COMM;
     int one = 1;
     setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
     struct sockaddr_in sa;
@@ -97,7 +97,7 @@ static int listen_on(const char* addr, int port, int* bound_port) {
     sa.sin_addr.s_addr = addr ? inet_addr(addr) : htonl(INADDR_ANY);
     if (bind(fd, (struct sockaddr*)&sa, sizeof sa) || listen(fd, 256)) {
         close(fd);
-        return -1;
+        return PCMX_ERR_COMM;
     }
     socklen_t len = sizeof sa;
     getsockname(fd, (struct sockaddr*)&sa, &len);
@@ -119,7 +119,7 @@ static int connect_retry(uint32_t ip_be, int port, double timeout_s) {
             return fd;
         }
         close(fd);
-        if (now_s() - t0 > timeout_s) return -1;
+        if (now_s() - t0 > timeout_s) return PCMX_ERR_COMM;
         usleep(20000);
     }
 }
@@ -422,54 +422,54 @@ int pcmx_comm_init_tcp(int rank, int world, const char* addr, int port, pcmx_com
     struct addrinfo hints, *res = NULL;
     memset(&hints, 0, sizeof hints);
     hints.ai_family = AF_INET;
-    if (getaddrinfo(a, NULL, &hints, &res) || !res) return -2;
+    if (getaddrinfo(a, NULL, &hints, &res) || !res) return PCMX_ERR_COMM;
     const uint32_t master_ip = ((struct sockaddr_in*)res->ai_addr)->sin_addr.s_addr;
     freeaddrinfo(res);
     endpoint_t* table = (endpoint_t*)calloc((size_t)world, sizeof(endpoint_t));
     int rc = 0;
     if (rank == 0) {
         int lfd = listen_on(NULL, port, NULL);
-        if (lfd < 0) return -3;
+        if (lfd < 0) return PCMX_ERR_COMM;
         for (int k = 1; k < world; ++k) {
             struct sockaddr_in peer;
             socklen_t len = sizeof peer;
             int fd = accept(lfd, (struct sockaddr*)&peer, &len);
-            if (fd < 0) return -4;
+            if (fd < 0) return PCMX_ERR_COMM;
             set_opts(fd);
             int32_t hello[2];
-            if (read_all(fd, hello, sizeof hello)) return -5;
-            if (hello[0] <= 0 || hello[0] >= world) return -6;
+            if (read_all(fd, hello, sizeof hello)) return PCMX_ERR_COMM;
+            if (hello[0] <= 0 || hello[0] >= world) return PCMX_ERR_COMM;
             t->fd[hello[0]] = fd;
             table[hello[0]].ip = peer.sin_addr.s_addr;
             table[hello[0]].port = hello[1];
         }
         close(lfd);
         for (int r = 1; r < world; ++r)
-            if (write_all(t->fd[r], table, sizeof(endpoint_t) * (size_t)world)) return -7;
+            if (write_all(t->fd[r], table, sizeof(endpoint_t) * (size_t)world)) return PCMX_ERR_COMM;
     } else {
         int my_port = 0;
         int lfd = listen_on(NULL, 0, &my_port);
-        if (lfd < 0) return -3;
+        if (lfd < 0) return PCMX_ERR_COMM;
         int fd0 = connect_retry(master_ip, port, 120.0);
-        if (fd0 < 0) return -8;
+        if (fd0 < 0) return PCMX_ERR_COMM;
         int32_t hello[2] = {rank, my_port};
-        if (write_all(fd0, hello, sizeof hello)) return -7;
-        if (read_all(fd0, table, sizeof(endpoint_t) * (size_t)world)) return -5;
+        if (write_all(fd0, hello, sizeof hello)) return PCMX_ERR_COMM;
+        if (read_all(fd0, table, sizeof(endpoint_t) * (size_t)world)) return PCMX_ERR_COMM;
         t->fd[0] = fd0;
         /* connect to lower ranks >= 1, then accept from higher ranks */
         for (int j = 1; j < rank; ++j) {
             int fd = connect_retry(table[j].ip, table[j].port, 120.0);
-            if (fd < 0) return -8;
+            if (fd < 0) return PCMX_ERR_COMM;
             int32_t me = rank;
-            if (write_all(fd, &me, sizeof me)) return -7;
+            if (write_all(fd, &me, sizeof me)) return PCMX_ERR_COMM;
             t->fd[j] = fd;
         }
         for (int k = rank + 1; k < world; ++k) {
             int fd = accept(lfd, NULL, NULL);
-            if (fd < 0) return -4;
+            if (fd < 0) return PCMX_ERR_COMM;
             set_opts(fd);
             int32_t who;
-            if (read_all(fd, &who, sizeof who) || who <= rank || who >= world) return -6;
+            if (read_all(fd, &who, sizeof who) || who <= rank || who >= world) return PCMX_ERR_COMM;
             t->fd[who] = fd;
         }
         close(lfd);
@@ -505,24 +505,24 @@ int pcmx_comm_init_env_tcp(pcmx_comm_t** out) {
 void pcmx_comm_destroy(pcmx_comm_t* c) {
     if (c) c->ops->destroy(c);
 }
-int pcmx_comm_group_start(pcmx_comm_t* c) { return c->ops->group_start(c); }
-int pcmx_comm_group_end(pcmx_comm_t* c) { return c->ops->group_end(c); }
-int pcmx_comm_send(pcmx_comm_t* c, const void* b, size_t n, int p) { return c->ops->send(c, b, n, p); }
-int pcmx_comm_recv(pcmx_comm_t* c, void* b, size_t n, int p) { return c->ops->recv(c, b, n, p); }
-int pcmx_comm_allreduce(pcmx_comm_t* c, void* b, size_t n, int dt, int op) { return c->ops->allreduce(c, b, n, dt, op); }
-int pcmx_comm_bcast(pcmx_comm_t* c, void* b, size_t n, int root) { return c->ops->bcast(c, b, n, root); }
-int pcmx_comm_sync(pcmx_comm_t* c) { return c->ops->sync(c); }
-int pcmx_comm_allgather(pcmx_comm_t* c, const void* s, void* r, size_t n) { return c->ops->allgather(c, s, r, n); }
-int pcmx_comm_gather(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) { return c->ops->gather(c, s, r, n, root); }
+int pcmx_comm_group_start(pcmx_comm_t* c) { return pcmx_comm_rc(c->ops->group_start(c)); }
+int pcmx_comm_group_end(pcmx_comm_t* c) { return pcmx_comm_rc(c->ops->group_end(c)); }
+int pcmx_comm_send(pcmx_comm_t* c, const void* b, size_t n, int p) { return pcmx_comm_rc(c->ops->send(c, b, n, p)); }
+int pcmx_comm_recv(pcmx_comm_t* c, void* b, size_t n, int p) { return pcmx_comm_rc(c->ops->recv(c, b, n, p)); }
+int pcmx_comm_allreduce(pcmx_comm_t* c, void* b, size_t n, int dt, int op) { return pcmx_comm_rc(c->ops->allreduce(c, b, n, dt, op)); }
+int pcmx_comm_bcast(pcmx_comm_t* c, void* b, size_t n, int root) { return pcmx_comm_rc(c->ops->bcast(c, b, n, root)); }
+int pcmx_comm_sync(pcmx_comm_t* c) { return pcmx_comm_rc(c->ops->sync(c)); }
+int pcmx_comm_allgather(pcmx_comm_t* c, const void* s, void* r, size_t n) { return pcmx_comm_rc(c->ops->allgather(c, s, r, n)); }
+int pcmx_comm_gather(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) { return pcmx_comm_rc(c->ops->gather(c, s, r, n, root)); }
 int pcmx_comm_scatter(pcmx_comm_t* c, const void* s, void* r, size_t n, int root) {
-    return c->ops->scatter(c, s, r, n, root);
+    return pcmx_comm_rc(c->ops->scatter(c, s, r, n, root));
 }
-int pcmx_comm_alltoall(pcmx_comm_t* c, const void* s, void* r, size_t n) { return c->ops->alltoall(c, s, r, n); }
+int pcmx_comm_alltoall(pcmx_comm_t* c, const void* s, void* r, size_t n) { return pcmx_comm_rc(c->ops->alltoall(c, s, r, n)); }
 int pcmx_comm_barrier(pcmx_comm_t* c) {
     int rc = c->ops->sync(c);
-    if (rc) return rc;
+    if (rc) return pcmx_comm_rc(rc);
     int one = 1;
-    return c->host->ops->allreduce(c->host, &one, 1, PCMX_I32, PCMX_SUM);
+    return pcmx_comm_rc(c->host->ops->allreduce(c->host, &one, 1, PCMX_I32, PCMX_SUM));
 }
 
 /* ------------------------------------------------------------------ Cartesian topology */

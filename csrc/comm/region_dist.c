@@ -149,11 +149,11 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
     const int root = c->rank == 0;
     /* shape is known on root only (ref reads the BMP on rank 0): broadcast over the host side-channel */
     int hw[2] = {H, W};
-    if (c->host->ops->bcast(c->host, hw, sizeof hw, 0)) return -1;
+    if (c->host->ops->bcast(c->host, hw, sizeof hw, 0)) return PCMX_ERR_COMM;
     H = hw[0], W = hw[1];
     pcmx_cart_t topo;
     pcmx_cart_init(&topo, c->world, dims);
-    if (topo.dims[0] * topo.dims[1] != c->world) return -2;
+    if (topo.dims[0] * topo.dims[1] != c->world) return PCMX_ERR_ARG;
     int tile[4], nb[4];
     pcmx_cart_tile(&topo, c->rank, H, W, tile);
     pcmx_cart_neighbours(&topo, c->rank, nb);
@@ -178,7 +178,7 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
     recvb = (unsigned char*)be->alloc((size_t)nedge, ctx);
     flag = (int*)be->alloc(sizeof(int), ctx);
     if (!img_p || !reg_p || !sendb || !recvb || !flag) {
-        rc = -3;
+        rc = PCMX_ERR_ALLOC;
         goto done;
     }
 
@@ -197,7 +197,7 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
         stage = (unsigned char*)be->alloc(total, ctx);
         if (!full_p || !stage) {
             free(padded);
-            rc = -3;
+            rc = PCMX_ERR_ALLOC;
             goto done;
         }
         rc = be->h2d(full_p, padded, (size_t)(H + 2) * pw, ctx);
@@ -353,7 +353,7 @@ done:
 int pcmx_token_ring(pcmx_comm_t* c, void* tok, const pcmx_region_backend_t* be, int verbose) {
     const int rank = c->rank, size = c->world;
     int msg = 0, rc = 0;
-    if (be->h2d(tok, &msg, sizeof msg, be->ctx)) return -1;
+    if (be->h2d(tok, &msg, sizeof msg, be->ctx)) return PCMX_ERR_COMM;
     if (rank != 0) {
         if ((rc = pcmx_comm_recv(c, tok, sizeof msg, rank - 1)) || (rc = pcmx_comm_sync(c))) return rc;
         be->d2h(&msg, tok, sizeof msg, be->ctx);

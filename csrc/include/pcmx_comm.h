@@ -15,6 +15,8 @@
 #define PCMX_COMM_H
 #include <stddef.h>
 
+#include "pcmx_errors.h" /* every pcmx_comm_* returns 0 or a PCMX_ERR_* code */
+
 #ifdef __cplusplus
 extern "C" {
 #endif

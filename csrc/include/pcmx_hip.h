@@ -25,17 +25,13 @@
 #include <stdint.h>
 #include <hip/hip_runtime_api.h>
 
+#include "pcmx_errors.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-/* ---------------------------------------------------------------- error codes (pcmx_error_string names them) */
-enum {
-    PCMX_ERR_ARG = -1,           /* shape / alignment / argument precondition */
-    PCMX_ERR_NOT_CONVERGED = -2, /* an iterate-to-fixpoint loop ran out of max_launches with work left */
-    PCMX_ERR_TIMEOUT = -3,       /* a bounded device-side wait gave up (result invalid) */
-    PCMX_ERR_COMM = -4           /* a transport / collective failed */
-};
+/* ---------------------------------------------------------------- error codes: pcmx_errors.h */
 
 /* ---------------------------------------------------------------- runtime / device info */
 int pcmx_device_count(void);

@@ -18,8 +18,9 @@ extern "C" const char* pcmx_error_string(int err) {
     switch (err) {
         case PCMX_ERR_ARG: return "pcmx: shape/alignment/argument precondition violated";
         case PCMX_ERR_NOT_CONVERGED: return "pcmx: not converged within max_launches (result incomplete)";
-        case PCMX_ERR_TIMEOUT: return "pcmx: bounded device wait timed out (result invalid)";
+        case PCMX_ERR_TIMEOUT: return "pcmx: bounded wait timed out (result invalid)";
         case PCMX_ERR_COMM: return "pcmx: communication failed";
+        case PCMX_ERR_ALLOC: return "pcmx: allocation failed";
         default: return err < 0 ? "pcmx: unknown error" : hipGetErrorString((hipError_t)err);
     }
 }

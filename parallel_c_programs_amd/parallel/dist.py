@@ -56,45 +56,64 @@ class Context:
             dist.broadcast(t, src)
         return t
 
-    def neighbour_exchange(self, pairs, async_op: bool = False) -> list:
-        """Sends / receives with a few peers: pairs = [(peer, send tensor, recv tensor)], each peer at most once,
-        tensors contiguous. On RCCL this is ONE list all_to_all (empty tensors for the other ranks; RCCL groups the
-        sends and receives over the point-to-point xGMI links): ~19 us of host time, against ~10 us per op for a
-        batch_isend_irecv of P2P ops (scripts/host_overhead_lab.py). gloo has no list all_to_all: a P2P batch.
-        Returns the works to wait on (empty when async_op is False: already complete on the stream)."""
-        if not self.distributed or not pairs:
+    def exchange(self, outs: list, ins: list, async_op: bool = False) -> list:
+        """The one all-to-all primitive every N > 1 exchange goes through (halo rows, z-slab planes, SpMV ghost
+        entries): ins[q] is sent to rank q, outs[q] is received from rank q; zero-size entries (non-neighbours, self)
+        move nothing. RCCL: ONE list all_to_all (grouped per-peer sends/receives over the point-to-point xGMI links,
+        ~19 us of host time against ~10 us per op for a batch of P2P ops, scripts/host_overhead_lab.py). gloo has
+        no list all_to_all: a P2P batch over the non-empty entries, host-staged for CUDA tensors (gloo's P2P ops
+        are not stream-ordered: the transport that lets several ranks share one GPU in tests).
+        Every rank must call it (collective), also with nothing to send. Returns the works to wait on (empty when
+        async_op is False)."""
+        if not self.distributed:
             return []
+        if len(outs) != self.world or len(ins) != self.world:
+            raise ValueError("exchange: one (possibly empty) tensor per rank")
         if self.backend == "nccl":
-            empty = pairs[0][1].new_empty(0)
-            ins, outs = [empty] * self.world, [empty] * self.world
-            for peer, snd, rcv in pairs:
-                ins[peer], outs[peer] = snd, rcv
             w = dist.all_to_all(outs, ins, async_op=True)
-        elif pairs[0][1].is_cuda:
-            # gloo's point-to-point ops on CUDA tensors are not stream-ordered (the transport reads/writes the
-            # device buffers from the host, racing the kernels around them): stage through host tensors
-            # (synchronous copies), the test transport that lets several ranks share one GPU
-            ops, staged = [], []
-            for peer, snd, rcv in pairs:
-                buf = torch.empty(rcv.shape, dtype=rcv.dtype)
-                ops += [dist.P2POp(dist.isend, snd.cpu(), peer), dist.P2POp(dist.irecv, buf, peer)]
-                staged.append((rcv, buf))
-            for x in dist.batch_isend_irecv(ops):
-                x.wait()
-            for rcv, buf in staged:
-                rcv.copy_(buf)
-            return []
         else:
-            ops = []
-            for peer, snd, rcv in pairs:
-                ops += [dist.P2POp(dist.isend, snd, peer), dist.P2POp(dist.irecv, rcv, peer)]
-            w = dist.batch_isend_irecv(ops)
+            staged_io = any(t.is_cuda for t in outs + ins)
+            ops, staged = [], []
+            for q in range(self.world):
+                if q == self.rank:
+                    if outs[q].numel():
+                        outs[q].copy_(ins[q])
+                    continue
+                if ins[q].numel():
+                    ops.append(dist.P2POp(dist.isend, ins[q].cpu() if staged_io else ins[q], q))
+                if outs[q].numel():
+                    buf = torch.empty(outs[q].shape, dtype=outs[q].dtype) if staged_io else outs[q]
+                    ops.append(dist.P2POp(dist.irecv, buf, q))
+                    staged.append((outs[q], buf))
+            w = dist.batch_isend_irecv(ops) if ops else []
+            if staged_io:
+                for x in w:
+                    x.wait()
+                for dst, buf in staged:
+                    if buf is not dst:
+                        dst.copy_(buf)
+                return []
         works = w if isinstance(w, list) else [w]
         if async_op:
             return works
         for x in works:
             x.wait()
         return []
+
+    def neighbour_exchange(self, pairs, async_op: bool = False) -> list:
+        """Sends / receives with a few peers: pairs = [(peer, send tensor, recv tensor)], each peer at most once,
+        tensors contiguous (possibly no pairs: the rank still takes part in the collective)."""
+        if not self.distributed:
+            return []
+        peers = [p for p, _, _ in pairs]
+        if len(set(peers)) != len(peers):
+            raise ValueError(f"neighbour_exchange: peer listed twice in {peers}")
+        like = pairs[0][1] if pairs else torch.empty(0, device=self.device)
+        empty = like.new_empty(0)
+        ins, outs = [empty] * self.world, [empty] * self.world
+        for peer, snd, rcv in pairs:
+            ins[peer], outs[peer] = snd, rcv
+        return self.exchange(outs, ins, async_op)
 
     def _staged(self, t: torch.Tensor) -> bool:
         """gloo moves CUDA tensors point-to-point without stream ordering: such messages go through host copies."""

@@ -12,7 +12,7 @@ CSR benchmark of ref 3-serial-optimization/spmv.c:170-177, 331-367).
         [chunk 0: ghosts of ranks 0..W-1 except r, in rank order | own rows of chunk 0] [chunk 1: ...] ...
     so one chunk's product is one contiguous own segment and its ghosts one contiguous region: after chunk c's
     product, its send entries (one index list per peer, fixed at set-up) are packed and moved by ONE
-    all_to_all_single (RCCL: grouped per-peer sends over the point-to-point xGMI links, no all-gather of the
+    collective (Context.exchange: RCCL grouped per-peer sends over the point-to-point xGMI links, no all-gather of the
     whole y) straight into the peers' ghost regions, while chunk c+1 is multiplied. The column indices are renumbered
     into this layout once at set-up; on one rank it is the identity.
   * exchange="allgather": the padded replicated layout (every rank holds all of y): entry of global row g
@@ -253,17 +253,22 @@ class DistributedSpMV:
             dst.copy_(spmv(part, xp))
 
     def _post_chunk(self, out: torch.Tensor, c: int):
-        """Ghost exchange of chunk c: pack this rank's send entries, then ONE all_to_all_single (RCCL groups the
-        per-peer sends/receives over the xGMI links) straight into the chunk's ghost region. One collective call
-        instead of a batch of per-peer P2P ops: ~14 us of host time per call vs ~10 us per op (RCCL on MI355X,
-        scripts/host_overhead_lab.py), which at N = 8 would otherwise make the step launch-bound."""
+        """Ghost exchange of chunk c: pack this rank's send entries (one index_select), then ONE collective
+        (Context.exchange: a list all_to_all on RCCL, the per-peer sends/receives grouped over the xGMI links) whose
+        per-peer receive entries are views of the chunk's ghost region (segments in rank order), so the entries
+        land in place. One collective call instead of a batch of per-peer P2P ops keeps the N = 8 step off the
+        host-launch bound (scripts/host_overhead_lab.py)."""
         W, r = self.ctx.world, self.ctx.rank
         if self.send_idx[c].numel():
             torch.index_select(out, 0, self.send_idx[c], out=self.sendbuf[c])
-        recv = [0 if q == r else self.recv_counts[c][q] for q in range(W)]
-        send = [0 if q == r else self.send_counts[c][q] for q in range(W)]
-        g0 = self.ghost0[c]
-        return [dist.all_to_all_single(out[g0:g0 + self.ghost_len[c]], self.sendbuf[c], recv, send, async_op=True)]
+        ins, outs, so = [], [], 0
+        for q in range(W):
+            ns = 0 if q == r else self.send_counts[c][q]
+            ins.append(self.sendbuf[c][so:so + ns])
+            so += ns
+            s0 = self.seg[c * W + q]
+            outs.append(out[s0:s0 + (0 if q == r else self.recv_counts[c][q])])
+        return self.ctx.exchange(outs, ins, async_op=True)
 
     def step_padded(self, xp: torch.Tensor) -> torch.Tensor:
         """xp (this rank's layout) -> A xp in the same layout (own rows + every ghost the next product reads).

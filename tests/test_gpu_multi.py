@@ -225,15 +225,54 @@ e = a.new_empty(0)
 dist.all_to_all([e], [e])  # zero-size entries (non-neighbours) pass through RCCL's grouped send/recv
 torch.cuda.synchronize()
 assert torch.equal(b[2], a[1]) and torch.equal(b[0:2], a[0:2]), b
+c.neighbour_exchange([])  # a rank without neighbours still enters the collective
 print("neighbour_exchange ok")
+# the RCCL call shapes the N > 1 bench paths use, on the same world-1 group:
+# all_to_all_single with explicit split lists (one of them zero) ...
+src = torch.arange(5, dtype=torch.float32, device=dev)
+dst = torch.zeros(5, device=dev)
+dist.all_to_all_single(dst, src, [5], [5])
+z = torch.zeros(0, device=dev)
+dist.all_to_all_single(z, z, [0], [0])
+assert torch.equal(dst, src)
+# ... all_gather_into_tensor into a slice of a bigger tensor (allgather SpMV layout, global_scan totals) ...
+big = torch.zeros(10, device=dev)
+dist.all_gather_into_tensor(big[3:7], src[1:5])
+assert torch.equal(big[3:7], src[1:5]) and float(big.sum()) == float(src[1:5].sum())
+# ... Context.exchange with per-peer views (the ghost exchange) ...
+out = torch.zeros(6, device=dev)
+c.exchange([out[2:5]], [src[0:3]])
+torch.cuda.synchronize()
+assert torch.equal(out[2:5], src[0:3]) and float(out[0:2].sum()) == 0 and float(out[5]) == 0
+print("rccl call shapes ok")
+# ... and the distributed SpMV step (ghost layout set-up exchange, _post_chunk per chunk, step_padded) and the
+# seeded global scan, through a context that takes the N > 1 branches
+from parallel_c_programs_amd.parallel.spmv import DistributedSpMV
+from parallel_c_programs_amd.parallel.collectives import global_scan
+d = DistributedSpMV.powerlaw(c, 200_000, 2_000_000, slices=16, chunks=3)
+assert d.chunks == 3 and c.distributed
+xp = torch.rand(d.n_pad, device=dev)
+for k in range(d.chunks):
+    for w in d._post_chunk(torch.zeros(d.n_pad, device=dev), k):
+        w.wait()
+y = d.step_padded(xp)
+err = d.layout_max_rel_err(y, xp)
+assert err < 1e-5, err
+x = torch.rand(100_000, device=dev)
+ys = global_scan(x, c)
+assert torch.allclose(ys.double(), torch.cumsum(x.double(), 0), rtol=1e-5, atol=1e-2)
+print("distributed spmv/scan branches ok", err)
 dist.destroy_process_group()
 """
 
 
 def test_neighbour_exchange_rccl_call_shape(gpu, tmp_path):
-    """Context.neighbour_exchange on RCCL (one list all_to_all, zero-size entries for non-neighbours) on a world-1
-    NCCL group with the rank as its own neighbour: the call shape the stencil halo, the 2-D region halo and the
-    z-slab exchange use at N > 1."""
+    """The RCCL-only branches of the N > 1 paths on a world-1 NCCL group (RCCL refuses two ranks on one GPU, and
+    the gloo GPU tests take the host-staged branch): Context.exchange / neighbour_exchange (one list all_to_all,
+    zero-size entries for non-neighbours, the rank as its own neighbour, a rank with no neighbours),
+    all_to_all_single with split lists incl. zero, all_gather_into_tensor into a slice, and DistributedSpMV's
+    ghost set-up + _post_chunk + step_padded and the seeded global_scan through a context that takes the
+    distributed branches."""
     from parallel_c_programs_amd.parallel import free_port
 
     script = tmp_path / "nb.py"
@@ -241,3 +280,4 @@ def test_neighbour_exchange_rccl_call_shape(gpu, tmp_path):
     env = dict(cli_env(), PCMX_ROOT=str(ROOT), MASTER_PORT=str(free_port()))
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0 and "neighbour_exchange ok" in r.stdout, r.stderr[-3000:]
+    assert "rccl call shapes ok" in r.stdout and "distributed spmv/scan branches ok" in r.stdout, r.stderr[-3000:]

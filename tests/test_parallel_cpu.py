@@ -122,6 +122,37 @@ def test_halo_exchange_matches_padded_slices(world):
     assert all(res.values()) and len(res) == world
 
 
+def _exchange(ctx, q):
+    """Context.exchange: a dense all-to-all with uneven and zero-size entries (self included), then a
+    neighbour_exchange in which rank 0 has NO pairs (it must still enter the collective), then a duplicate peer."""
+    W, r = ctx.world, ctx.rank
+    ins = [torch.full((q_ * 2 + r,), float(100 * r + q_)) for q_ in range(W)]  # entry for q: 2q + r values
+    outs = [torch.empty(2 * r + q_) for q_ in range(W)]                       # from q: 2r + q values
+    ctx.exchange(outs, ins)
+    ok = all(torch.equal(outs[q_], torch.full((2 * r + q_,), float(100 * q_ + r))) for q_ in range(W))
+    # ring neighbour exchange among ranks 1..W-1 only; rank 0 passes an empty list
+    pairs = []
+    if r > 0:
+        nxt, prv = 1 + (r % (W - 1)), 1 + ((r - 2) % (W - 1))
+        pairs = [(nxt, torch.tensor([float(r)]), torch.empty(1))]
+        if prv != nxt:
+            pairs.append((prv, torch.tensor([float(r)]), torch.empty(1)))
+    ctx.neighbour_exchange(pairs)
+    ok &= all(float(rcv) == float(p) for p, _, rcv in pairs)
+    try:
+        ctx.neighbour_exchange([(0, torch.zeros(1), torch.zeros(1))] * 2)
+        ok = False
+    except ValueError:
+        pass
+    q.put((r, bool(ok)))
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_context_exchange_uneven_empty_and_no_pairs(world):
+    res = _collect(world, _exchange)
+    assert len(res) == world and all(res.values()), res
+
+
 def _reduce_scan(ctx, q):
     g = torch.Generator().manual_seed(10 + ctx.rank)
     x = torch.rand(1000 + 37 * ctx.rank, generator=g)
