@@ -136,6 +136,9 @@ void print_time(struct timeval start, struct timeval end) {
     printf("Time : %f s\n", (double)us / 1e6);
 }
 
+/* the same line for a time measured elsewhere (HIP events of the GPU products) */
+void print_time_seconds(double s) { printf("Time : %f s\n", s); }
+
 /* No auto-vectorisation for the indirect loops: with AVX2 gcc emits vgatherdps, which is microcoded and
  * far slower than scalar loads on current x86 parts (measured 1.4x slower than the reference's SSE build). */
 #define PCMX_SCALAR_GATHER __attribute__((optimize("no-tree-vectorize")))

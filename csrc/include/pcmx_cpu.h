@@ -84,6 +84,7 @@ void print_raw_csr_matrix(csr_matrix_t* m);
 void print_formated_csr_matrix(csr_matrix_t* m);
 void print_vector(float* v, int n, int orientation);
 void print_time(struct timeval start, struct timeval end);
+void print_time_seconds(double seconds); /* "Time : %f s" for a device-timed product */
 void multiply_naive(csr_matrix_t* m, float* v, float* r);
 void compare(float* a, float* b, int n);
 s_matrix_t* create_s_matrix(int dim, int a, int b, int c, int d, int e);

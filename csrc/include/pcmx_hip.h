@@ -182,6 +182,9 @@ int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* va
                      const int* slice_colbase, hipStream_t s);
 int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                      const float* x, float* y, hipStream_t s);
+/* variant 0: one wave per row (strided band loops, global x); 1 (default): LDS-staged x windows, row blocks */
+int pcmx_spmv_banded_variant(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
+                             const float* x, float* y, int variant, hipStream_t s);
 
 /* ---------------------------------------------------------------- halo pack/unpack */
 int pcmx_pack_edges(const void* tile, int elem_bytes, int H, int W, int ld, void* buf, hipStream_t s);

@@ -398,7 +398,122 @@ __global__ __launch_bounds__(256) void spmv_fixup_kernel(const float* __restrict
     if (lane == 0) y[row] += acc;
 }
 
-// one wave per row of the banded matrix
+// Band limits of one row: left outer, left inner, centre, right inner, right outer (ref create_csr_matrix,
+// spmv.c:91-107; clipped to [0, n), empty bands have hi == lo). Non-decreasing in `row`.
+__device__ __forceinline__ void band_limits(int n, int a, int b, int c, int d, int e, int row, int (&lo)[5], int (&hi)[5]) {
+    const int ah = a / 2;
+    const int r5 = ah, r6 = ah + b, r7 = ah + b + c, r8 = ah + b + c + d, r9 = ah + b + c + d + e;
+    lo[0] = max(0, row - r9), hi[0] = max(0, row - r8);
+    lo[1] = max(0, row - r7), hi[1] = max(0, row - r6);
+    lo[2] = max(0, row - r5), hi[2] = min(row + r5 + 1, n);
+    lo[3] = min(n, row + r6 + 1), hi[3] = min(n, row + r7 + 1);
+    lo[4] = min(n, row + r8 + 1), hi[4] = min(n, row + r9 + 1);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) hi[k] = max(hi[k], lo[k]);
+}
+
+// Banded SpMV with implicit column indices (ref s_matrix `multiply`, spmv.c:212-329), one block per R rows.
+//  * x: band k of rows r0..r0+R-1 reads the contiguous window [lo_k(r0), hi_k(r0+R-1)) — one row's band shifted
+//    by up to R-1 — so the block stages the 5 windows in LDS once (coalesced) and every nonzero reads x there.
+//  * values: row i's nonzeros are contiguous; a wave takes whole rows, lane j reads value j + 64m (coalesced
+//    256-B wave loads, all ceil(nnz/64) <= NL of a row issued before use, two rows in flight per wave).
+//  * no per-row metadata: the rows' nonzero counts and band limits are computed in registers (a wave prefix
+//    scan of the R counts gives each row's offset from the block's first row); row_off is read ONCE per block.
+template <int R, int NL>
+__global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __restrict__ vals,
+                                                              const long long* __restrict__ row_off, int n, int a, int b,
+                                                              int c, int d, int e, const float* __restrict__ x,
+                                                              float* __restrict__ y) {
+    extern __shared__ float xw[];
+    static_assert(R <= kWave && R % 4 == 0, "rows per block");
+    const int lane = pcmx::lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+    const int r0 = (int)blockIdx.x * R, nr = min(R, n - r0);
+    int wlo[5], wbase[5], total = 0;
+    {
+        int lo0[5], hi0[5], lo1[5], hi1[5];
+        band_limits(n, a, b, c, d, e, r0, lo0, hi0);
+        band_limits(n, a, b, c, d, e, r0 + nr - 1, lo1, hi1);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            wlo[k] = lo0[k], wbase[k] = total;
+            total += max(0, hi1[k] - lo0[k]);
+        }
+    }
+    for (int i = (int)threadIdx.x; i < total; i += 256) {
+        const int k = (i >= wbase[1]) + (i >= wbase[2]) + (i >= wbase[3]) + (i >= wbase[4]);
+        int wl = wlo[0], wb = wbase[0];
+#pragma unroll
+        for (int q = 1; q < 5; ++q)
+            if (k == q) wl = wlo[q], wb = wbase[q];
+        xw[i] = x[wl + i - wb];
+    }
+    // nonzeros of the block's rows (lane l = row r0 + l) and their exclusive prefix
+    int my = 0;
+    if (lane < nr) {
+        int lo[5], hi[5];
+        band_limits(n, a, b, c, d, e, r0 + lane, lo, hi);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) my += hi[k] - lo[k];
+    }
+    int incl = my;
+#pragma unroll
+    for (int off = 1; off < R; off <<= 1) {
+        const int o = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += o;
+    }
+    const long long boff = row_off[r0];
+    __syncthreads();
+
+    for (int rr = wave; rr < nr; rr += 8) {  // rows rr and rr + 4 of the block
+        float v[2][NL];
+        int off[2][5], cum[2][4], nnz[2];
+        const int cnt = rr + 4 < nr ? 2 : 1;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (u >= cnt) break;
+            const int row = rr + 4 * u;
+            const int row_nnz = __builtin_amdgcn_readlane(my, row);
+            const long long start = boff + (long long)__builtin_amdgcn_readlane(incl - my, row);
+            const float* vr = vals + start;
+#pragma unroll
+            for (int m = 0; m < NL; ++m) {
+                const int j = lane + 64 * m;
+                v[u][m] = (64 * m < row_nnz && j < row_nnz) ? vr[j] : 0.f;
+            }
+            int lo[5], hi[5];
+            band_limits(n, a, b, c, d, e, r0 + row, lo, hi);
+            int cs = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                off[u][k] = wbase[k] + lo[k] - wlo[k] - cs;  // LDS index of nonzero j of band k = j + off
+                cs += hi[k] - lo[k];
+                if (k < 4) cum[u][k] = cs;
+            }
+            nnz[u] = row_nnz;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (u >= cnt) break;
+            float acc = 0.f;
+#pragma unroll
+            for (int m = 0; m < NL; ++m) {
+                if (64 * m >= nnz[u]) break;
+                const int j = lane + 64 * m;
+                const int o = j < cum[u][0] ? off[u][0]
+                            : j < cum[u][1] ? off[u][1]
+                            : j < cum[u][2] ? off[u][2]
+                            : j < cum[u][3] ? off[u][3]
+                                            : off[u][4];
+                if (j < nnz[u]) acc = fmaf(v[u][m], xw[j + o], acc);
+            }
+            acc = pcmx::wave_reduce<float, 0>(acc);
+            if (lane == 0) y[r0 + rr + 4 * u] = acc;
+        }
+    }
+}
+
+// fallback for rows longer than 16 x 64 nonzeros: one wave per row, strided band loops
 __global__ __launch_bounds__(256) void spmv_banded_kernel(const float* __restrict__ vals,
                                                           const long long* __restrict__ row_off, int n, int a, int b,
                                                           int c, int d, int e, const float* __restrict__ x,
@@ -406,19 +521,13 @@ __global__ __launch_bounds__(256) void spmv_banded_kernel(const float* __restric
     const int lane = pcmx::lane_id();
     const int row = blockIdx.x * 4 + threadIdx.x / kWave;
     if (row >= n) return;
-    const int ah = a / 2;
-    const int r5 = ah, r6 = ah + b, r7 = ah + b + c, r8 = ah + b + c + d, r9 = ah + b + c + d + e;
     int lo[5], hi[5];
-    lo[0] = max(0, row - r9), hi[0] = max(0, row - r8);
-    lo[1] = max(0, row - r7), hi[1] = max(0, row - r6);
-    lo[2] = max(0, row - r5), hi[2] = min(row + r5 + 1, n);
-    lo[3] = min(n, row + r6 + 1), hi[3] = min(n, row + r7 + 1);
-    lo[4] = min(n, row + r8 + 1), hi[4] = min(n, row + r9 + 1);
+    band_limits(n, a, b, c, d, e, row, lo, hi);
     const float* v = vals + row_off[row];
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        const int len = hi[k] > lo[k] ? hi[k] - lo[k] : 0;
+        const int len = hi[k] - lo[k];
         for (int j = lane; j < len; j += kWave) acc += v[j] * x[lo[k] + j];
         v += len;
     }
@@ -539,9 +648,27 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
     return (int)hipGetLastError();
 }
 
+extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_off, int n, int a, int b, int c, int d,
+                                        int e, const float* x, float* y, int variant, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (a < 1 || b < 0 || c < 0 || d < 0 || e < 0) return PCMX_ERR_ARG;
+    constexpr int R = 16;
+    const long long maxrow = 2LL * (a / 2) + 1 + 2LL * c + 2LL * e;  // nonzeros of an unclipped row
+    const int nl = (int)((maxrow + 63) / 64);
+    const size_t lds = (size_t)(maxrow + 5 * (R - 1)) * sizeof(float);
+    if (variant == 0 || nl > 16 || lds > 64 * 1024) {
+        spmv_banded_kernel<<<(n + 3) / 4, 256, 0, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
+        return (int)hipGetLastError();
+    }
+    const int grid = (n + R - 1) / R;
+    if (nl <= 4) spmv_banded_lds_kernel<R, 4><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
+    else if (nl <= 8) spmv_banded_lds_kernel<R, 8><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
+    else if (nl <= 12) spmv_banded_lds_kernel<R, 12><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
+    else spmv_banded_lds_kernel<R, 16><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
+    return (int)hipGetLastError();
+}
+
 extern "C" int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                                 const float* x, float* y, hipStream_t s) {
-    if (n <= 0) return 0;
-    spmv_banded_kernel<<<(n + 3) / 4, 256, 0, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
-    return (int)hipGetLastError();
+    return pcmx_spmv_banded_variant(vals, row_off, n, a, b, c, d, e, x, y, 1, s);
 }

@@ -536,12 +536,15 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
 }
 
 at::Tensor spmv_banded(const at::Tensor& vals, const at::Tensor& row_off, int64_t n, int64_t a, int64_t b, int64_t c,
-                       int64_t d, int64_t e, const at::Tensor& x) {
+                       int64_t d, int64_t e, const at::Tensor& x, int64_t variant) {
     check_gpu(vals, "vals", at::kFloat), check_gpu(row_off, "row_off", at::kLong), check_gpu(x, "x", at::kFloat);
+    TORCH_CHECK(vals.is_contiguous() && row_off.is_contiguous() && x.is_contiguous(), "spmv_banded: contiguous tensors");
+    TORCH_CHECK(row_off.numel() >= n && x.numel() >= n, "spmv_banded: row_off and x need n entries");
     const at::DeviceGuard g(vals.device());
     auto y = at::empty({n}, vals.options());
-    check_rc(pcmx_spmv_banded(vals.data_ptr<float>(), (const long long*)row_off.data_ptr<int64_t>(), (int)n, (int)a, (int)b, (int)c, (int)d,
-                              (int)e, x.data_ptr<float>(), y.data_ptr<float>(), cur_stream(vals)),
+    check_rc(pcmx_spmv_banded_variant(vals.data_ptr<float>(), (const long long*)row_off.data_ptr<int64_t>(), (int)n, (int)a,
+                                      (int)b, (int)c, (int)d, (int)e, x.data_ptr<float>(), y.data_ptr<float>(), (int)variant,
+                                      cur_stream(vals)),
              "spmv_banded");
     return y;
 }
@@ -618,7 +621,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("stencil5xT_spans_(Tensor u, Tensor(a!) out, int halo, int steps, int r0a, int r1a, int r0b, int r1b, int global_row0, int global_rows, float k) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
     m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor row_mask, Tensor chunk_base, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None, int mode=0) -> Tensor");
-    m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x) -> Tensor");
+    m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x, int variant=1) -> Tensor");
     m.def("pack_edges(Tensor tile) -> Tensor");
     m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask, Tensor(b!)? changed=None) -> ()");
 }

@@ -322,10 +322,11 @@ def spmv(m: CSR, x: torch.Tensor) -> torch.Tensor:
 
 
 def spmv_banded(vals: torch.Tensor, row_off: torch.Tensor, n: int, a: int, b: int, c: int, d: int, e: int,
-                x: torch.Tensor) -> torch.Tensor:
-    """Banded product with implicit columns (the reference's s_matrix `multiply`, spmv.c:212-329)."""
+                x: torch.Tensor, variant: int = 1) -> torch.Tensor:
+    """Banded product with implicit columns (the reference's s_matrix `multiply`, spmv.c:212-329). GPU variant 1
+    (default): row blocks with the x band windows staged in LDS and in-register band limits; 0: one wave per row."""
     if x.is_cuda:
-        return ops().spmv_banded(vals, row_off, int(n), int(a), int(b), int(c), int(d), int(e), x)
+        return ops().spmv_banded(vals, row_off, int(n), int(a), int(b), int(c), int(d), int(e), x, int(variant))
 
     class SMat(ctypes.Structure):
         _fields_ = [("values", ctypes.c_void_p), ("n", ctypes.c_int), ("a", ctypes.c_int), ("b", ctypes.c_int),
