@@ -499,13 +499,13 @@ __global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __res
 #pragma unroll
             for (int m = 0; m < NL; ++m) {
                 if (64 * m >= nnz[u]) break;
-                const int j = lane + 64 * m;
-                const int o = j < cum[u][0] ? off[u][0]
-                            : j < cum[u][1] ? off[u][1]
-                            : j < cum[u][2] ? off[u][2]
-                            : j < cum[u][3] ? off[u][3]
-                                            : off[u][4];
-                if (j < nnz[u]) acc = fmaf(v[u][m], xw[j + o], acc);
+                // lanes past the row's end read a valid slot (their value is 0): branch-free, a chain of
+                // selects over the row's 5 scalar band offsets (no indexed register array)
+                const int j = min(lane + 64 * m, nnz[u] - 1);
+                const int o = off[u][0] + (j >= cum[u][0] ? off[u][1] - off[u][0] : 0) +
+                              (j >= cum[u][1] ? off[u][2] - off[u][1] : 0) + (j >= cum[u][2] ? off[u][3] - off[u][2] : 0) +
+                              (j >= cum[u][3] ? off[u][4] - off[u][3] : 0);
+                acc = fmaf(v[u][m], xw[j + o], acc);
             }
             acc = pcmx::wave_reduce<float, 0>(acc);
             if (lane == 0) y[r0 + rr + 4 * u] = acc;
