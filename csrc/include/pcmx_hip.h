@@ -182,7 +182,8 @@ int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* va
                      const int* slice_colbase, hipStream_t s);
 int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                      const float* x, float* y, hipStream_t s);
-/* variant 0: one wave per row (strided band loops, global x); 1 (default): LDS-staged x windows, row blocks */
+/* variant 0: one wave per row (strided band loops, global x); 1: LDS-staged x windows, row blocks, 4-B loads;
+ * 2 / 3: the same with 16-B value loads, 2 / 4 rows per wave in flight */
 int pcmx_spmv_banded_variant(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                              const float* x, float* y, int variant, hipStream_t s);
 

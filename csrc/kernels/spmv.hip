@@ -419,7 +419,7 @@ __device__ __forceinline__ void band_limits(int n, int a, int b, int c, int d, i
 //    256-B wave loads, all ceil(nnz/64) <= NL of a row issued before use, two rows in flight per wave).
 //  * no per-row metadata: the rows' nonzero counts and band limits are computed in registers (a wave prefix
 //    scan of the R counts gives each row's offset from the block's first row); row_off is read ONCE per block.
-template <int R, int NL>
+template <int R, int NL, int U = 2>
 __global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __restrict__ vals,
                                                               const long long* __restrict__ row_off, int n, int a, int b,
                                                               int c, int d, int e, const float* __restrict__ x,
@@ -465,12 +465,12 @@ __global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __res
     const long long boff = row_off[r0];
     __syncthreads();
 
-    for (int rr = wave; rr < nr; rr += 8) {  // rows rr and rr + 4 of the block
-        float v[2][NL];
-        int off[2][5], cum[2][4], nnz[2];
-        const int cnt = rr + 4 < nr ? 2 : 1;
+    for (int rr = wave; rr < nr; rr += 4 * U) {  // rows rr, rr + 4, ... (U rows of the wave in flight)
+        float v[U][NL];
+        int off[U][5], cum[U][4], nnz[U];
+        const int cnt = min(U, (nr - rr + 3) / 4);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (u >= cnt) break;
             const int row = rr + 4 * u;
             const int row_nnz = __builtin_amdgcn_readlane(my, row);
@@ -493,7 +493,7 @@ __global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __res
             nnz[u] = row_nnz;
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (u >= cnt) break;
             float acc = 0.f;
 #pragma unroll
@@ -506,6 +506,110 @@ __global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __res
                               (j >= cum[u][1] ? off[u][2] - off[u][1] : 0) + (j >= cum[u][2] ? off[u][3] - off[u][2] : 0) +
                               (j >= cum[u][3] ? off[u][4] - off[u][3] : 0);
                 acc = fmaf(v[u][m], xw[j + o], acc);
+            }
+            acc = pcmx::wave_reduce<float, 0>(acc);
+            if (lane == 0) y[r0 + rr + 4 * u] = acc;
+        }
+    }
+}
+
+// Variant 2: the same row blocks and LDS windows, values read with 16-B loads: a row's values start at any 4-B
+// boundary, so lane l loads the aligned float4 l (+64m) of the span [start & ~3, start + nnz) and handles its 4
+// elements j = 4(l + 64m) + k - lead (lead = start & 3; elements outside the row are masked to 0). NL4 loads per
+// row (ceil((nnz + 3) / 256)), U rows of a wave in flight.
+template <int R, int NL4, int U>
+__global__ __launch_bounds__(256) void spmv_banded_lds4_kernel(const float* __restrict__ vals,
+                                                               const long long* __restrict__ row_off, int n, int a,
+                                                               int b, int c, int d, int e, const float* __restrict__ x,
+                                                               float* __restrict__ y) {
+    extern __shared__ float xw[];
+    static_assert(R <= kWave && R % 4 == 0 && (R / 4) % U == 0, "rows per block");
+    const int lane = pcmx::lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+    const int r0 = (int)blockIdx.x * R, nr = min(R, n - r0);
+    int wlo[5], wbase[5], total = 0;
+    {
+        int lo0[5], hi0[5], lo1[5], hi1[5];
+        band_limits(n, a, b, c, d, e, r0, lo0, hi0);
+        band_limits(n, a, b, c, d, e, r0 + nr - 1, lo1, hi1);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            wlo[k] = lo0[k], wbase[k] = total;
+            total += max(0, hi1[k] - lo0[k]);
+        }
+    }
+    for (int i = (int)threadIdx.x; i < total; i += 256) {
+        const int k = (i >= wbase[1]) + (i >= wbase[2]) + (i >= wbase[3]) + (i >= wbase[4]);
+        const int src = wlo[0] + i - wbase[0] + (k >= 1 ? (wlo[1] - wbase[1]) - (wlo[0] - wbase[0]) : 0) +
+                        (k >= 2 ? (wlo[2] - wbase[2]) - (wlo[1] - wbase[1]) : 0) +
+                        (k >= 3 ? (wlo[3] - wbase[3]) - (wlo[2] - wbase[2]) : 0) +
+                        (k >= 4 ? (wlo[4] - wbase[4]) - (wlo[3] - wbase[3]) : 0);
+        xw[i] = x[src];
+    }
+    int my = 0;
+    if (lane < nr) {
+        int lo[5], hi[5];
+        band_limits(n, a, b, c, d, e, r0 + lane, lo, hi);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) my += hi[k] - lo[k];
+    }
+    int incl = my;
+#pragma unroll
+    for (int off = 1; off < R; off <<= 1) {
+        const int o = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += o;
+    }
+    const long long boff = row_off[r0];
+    __syncthreads();
+
+    for (int rr = wave; rr < nr; rr += 4 * U) {
+        pcmx::f32x4 v[U][NL4];
+        int off[U][5], cum[U][4], nnz[U], lead[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = rr + 4 * u;
+            nnz[u] = 0;
+            if (row >= nr) continue;
+            const int row_nnz = __builtin_amdgcn_readlane(my, row);
+            const long long start = boff + (long long)__builtin_amdgcn_readlane(incl - my, row);
+            const long long a0 = start & ~3LL;
+            lead[u] = (int)(start - a0);
+            const int span = lead[u] + row_nnz;
+            const pcmx::f32x4* vr = reinterpret_cast<const pcmx::f32x4*>(vals + a0);
+#pragma unroll
+            for (int m = 0; m < NL4; ++m) {
+                const int q = lane + 64 * m;
+                v[u][m] = (256 * m < span && 4 * q < span) ? vr[q] : pcmx::f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            int lo[5], hi[5];
+            band_limits(n, a, b, c, d, e, r0 + row, lo, hi);
+            int cs = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                off[u][k] = wbase[k] + lo[k] - wlo[k] - cs;
+                cs += hi[k] - lo[k];
+                if (k < 4) cum[u][k] = cs;
+            }
+            nnz[u] = row_nnz;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (nnz[u] == 0) continue;
+            float acc = 0.f;
+#pragma unroll
+            for (int m = 0; m < NL4; ++m) {
+                if (256 * m >= lead[u] + nnz[u]) break;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int jr = 4 * (lane + 64 * m) + k - lead[u];
+                    const bool in = jr >= 0 && jr < nnz[u];
+                    const int j = min(max(jr, 0), nnz[u] - 1);
+                    const int o = off[u][0] + (j >= cum[u][0] ? off[u][1] - off[u][0] : 0) +
+                                  (j >= cum[u][1] ? off[u][2] - off[u][1] : 0) +
+                                  (j >= cum[u][2] ? off[u][3] - off[u][2] : 0) +
+                                  (j >= cum[u][3] ? off[u][4] - off[u][3] : 0);
+                    acc = fmaf(in ? v[u][m][k] : 0.f, xw[j + o], acc);
+                }
             }
             acc = pcmx::wave_reduce<float, 0>(acc);
             if (lane == 0) y[r0 + rr + 4 * u] = acc;
@@ -652,19 +756,49 @@ extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_
                                         int e, const float* x, float* y, int variant, hipStream_t s) {
     if (n <= 0) return 0;
     if (a < 1 || b < 0 || c < 0 || d < 0 || e < 0) return PCMX_ERR_ARG;
-    constexpr int R = 16;
     const long long maxrow = 2LL * (a / 2) + 1 + 2LL * c + 2LL * e;  // nonzeros of an unclipped row
     const int nl = (int)((maxrow + 63) / 64);
+    // variant 1 (default) R = 16 rows per block, 2 rows per wave in flight; 4: R 32 / U 2; 5: R 16 / U 4;
+    // 6: R 32 / U 4; 7: R 64 / U 2 (scripts/spmv_banded_lab.py); 2 / 3: 16-B value loads
+    const int R = variant == 4 || variant == 6 ? 32 : variant == 7 ? 64 : 16;
     const size_t lds = (size_t)(maxrow + 5 * (R - 1)) * sizeof(float);
     if (variant == 0 || nl > 16 || lds > 64 * 1024) {
         spmv_banded_kernel<<<(n + 3) / 4, 256, 0, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
         return (int)hipGetLastError();
     }
     const int grid = (n + R - 1) / R;
-    if (nl <= 4) spmv_banded_lds_kernel<R, 4><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
-    else if (nl <= 8) spmv_banded_lds_kernel<R, 8><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
-    else if (nl <= 12) spmv_banded_lds_kernel<R, 12><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
-    else spmv_banded_lds_kernel<R, 16><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);
+    const int nl4 = (int)((maxrow + 3 + 255) / 256);
+    if (variant == 2 || variant == 3) {
+        if (nl4 > 4) return PCMX_ERR_ARG;
+        const bool u4 = variant == 3;
+#define PCMX_BANDED4(NL4)                                                                                              \
+    (u4 ? (spmv_banded_lds4_kernel<16, NL4, 4><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y), 0)      \
+        : (spmv_banded_lds4_kernel<16, NL4, 2><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y), 0))
+        if (nl4 <= 1) PCMX_BANDED4(1);
+        else if (nl4 <= 2) PCMX_BANDED4(2);
+        else if (nl4 <= 3) PCMX_BANDED4(3);
+        else PCMX_BANDED4(4);
+#undef PCMX_BANDED4
+        return (int)hipGetLastError();
+    }
+#define PCMX_BANDED(RR, UU)                                                                                            \
+    do {                                                                                                               \
+        if (nl <= 2) spmv_banded_lds_kernel<RR, 2, UU><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);   \
+        else if (nl <= 4) spmv_banded_lds_kernel<RR, 4, UU><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y); \
+        else if (nl <= 6) spmv_banded_lds_kernel<RR, 6, UU><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y); \
+        else if (nl <= 8) spmv_banded_lds_kernel<RR, 8, UU><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y); \
+        else if (nl <= 10) spmv_banded_lds_kernel<RR, 10, UU><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y); \
+        else if (nl <= 12) spmv_banded_lds_kernel<RR, 12, UU><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y); \
+        else spmv_banded_lds_kernel<RR, 16, UU><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y);          \
+    } while (0)
+    switch (variant) {
+        case 4: PCMX_BANDED(32, 2); break;
+        case 5: PCMX_BANDED(16, 4); break;
+        case 6: PCMX_BANDED(32, 4); break;
+        case 7: PCMX_BANDED(64, 2); break;
+        default: PCMX_BANDED(16, 2); break;
+    }
+#undef PCMX_BANDED
     return (int)hipGetLastError();
 }
 
