@@ -291,6 +291,7 @@ extern "C" int pcmx_region_backend_hip(pcmx_region_backend_t* be, void* stream) 
     be->copy2d = d_copy2d, be->grow = d_grow, be->pack = d_pack, be->unpack = d_unpack, be->sync = d_sync;
     be->unpack_changed = d_unpack_changed;
     be->ctx = c;
+    be->stream = stream;
     return 0;
 }
 

@@ -129,6 +129,7 @@ void pcmx_region_backend_host(pcmx_region_backend_t* be) {
     be->copy2d = h_copy2d, be->grow = h_grow, be->pack = h_pack, be->unpack = h_unpack, be->sync = h_sync;
     be->unpack_changed = h_unpack_changed;
     be->ctx = NULL;
+    be->stream = NULL;
 }
 
 /* ------------------------------------------------------------------ distributed region growing */
@@ -263,7 +264,10 @@ int pcmx_region2d_distributed(pcmx_comm_t* c, const pcmx_region_backend_t* be, c
         ++outer;
         if (c->world == 1) break;
         TRY(be->pack(reg_p, h, w, sendb, ctx));
-        TRY(be->sync(ctx));
+        /* the pack and the sends are stream-ordered when the backend runs on the communicator's stream (device
+         * backend + RCCL or staged transport): no host wait per outer step. Only a backend on another stream
+         * (or a host backend feeding a device transport) must finish before the transport reads sendb. */
+        if (!(be->stream && be->stream == c->stream)) TRY(be->sync(ctx));
         TRY(pcmx_comm_group_start(c));
         for (int k = 0; k < 4; ++k) {
             if (nb[k] < 0) continue;

@@ -120,6 +120,9 @@ typedef struct pcmx_region_backend {
                           void* ctx);
     int (*sync)(void* ctx);
     void* ctx;
+    void* stream; /* hipStream_t the backend issues its kernels/copies on (NULL: host backend). When it is the
+                   * communicator's stream (RCCL / staged transports), packs and sends are stream-ordered and
+                   * the exchange needs no host synchronisation. */
 } pcmx_region_backend_t;
 
 #define PCMX_REGION_CHECK_EVERY 2
