@@ -421,8 +421,11 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
     }
 }
 
-template <int T, int kAhead, int RPW = kRowsPerWave>
-__global__ __launch_bounds__(kWaves * 64) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
+// MINW: minimum waves per SIMD the register allocation must allow (__launch_bounds__'s second argument): a short
+// slab has few waves, so fitting one more per SIMD (T=4: 138 -> <= 128 VGPRs, 3 -> 4 waves) can matter more than
+// the few rematerialised values it costs.
+template <int T, int kAhead, int RPW = kRowsPerWave, int MINW = 1>
+__global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
                                                                   unsigned short* __restrict__ out, int rows, int cols,
                                                                   int ld, int halo, RowSpans sp, long long grow0,
                                                                   long long grows, float k) {
@@ -514,8 +517,12 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
     // more waves; scripts/stencil_lab.hip sweep after the trapezoid skip, profiles/r2_stencil/rpw_sweep_trapezoid.txt,
     // 16384 columns, GLUP/s of the best RPW: 2048 rows T=4 24 (3.9k), T=6/8 16 (3.6k/3.4k); 4096 rows 24 (4.4-4.5k);
     // 8192 rows 24-32 (4.9-5.1k); 16384 rows T=6/8 64 (5.4k/5.5k), T=4 24 (4.8k))
+    // Round 3 (profiles/r3_stencil/short_slab_sweep.txt, counters short_slab_pmc.txt): on a 2048-row slab (one rank
+    // at N = 8) T = 4 with an 18-row wave and a 3-row prefetch ring (126 VGPRs: 4 waves per SIMD, 3828 waves in
+    // one round) runs 3.9-4.0k against 3.6-3.9k for 24 rows / 6-row ring (138 VGPRs, 3 waves per SIMD); the waves
+    // are VALU-busy only ~20% of the time, split between load waits and the level-to-level dependency chain.
     const int span_rows = (r1a - r0a) + (r1b - r0b);
-    const int rpw = span_rows < 3072 ? (steps <= 4 ? 24 : 16) : span_rows < 6144 ? 24 : span_rows < 12288 ? 32
+    const int rpw = span_rows < 3072 ? (steps <= 4 ? 18 : 16) : span_rows < 6144 ? 24 : span_rows < 12288 ? 32
                     : (steps <= 4 ? 24 : 64);
     auto launch_dims = [&](int rpw_, RowSpans& sp) {
         const int per = kWaves * rpw_;
@@ -526,7 +533,7 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
 #define PCMX_STENCIL_V2_RPW(T, R)                                                                                   \
     case R: {                                                                                                       \
         const dim3 g = launch_dims(R, sp);                                                                          \
-        stencil5xT2_kernel<T, (T >= 6 && R >= 64 ? 9 : 6), R><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld,     \
+        stencil5xT2_kernel<T, (T >= 6 && R >= 64 ? 9 : R == 18 ? 3 : 6), R><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, \
                                                                                        halo, sp,                    \
                                                                                        global_row0, global_rows, k); \
         break;                                                                                                      \
@@ -534,6 +541,7 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
 #define PCMX_STENCIL_V2(T)                                                                                          \
     switch (rpw) {                                                                                                  \
         PCMX_STENCIL_V2_RPW(T, 16)                                                                                  \
+        PCMX_STENCIL_V2_RPW(T, 18)                                                                                  \
         PCMX_STENCIL_V2_RPW(T, 24)                                                                                  \
         PCMX_STENCIL_V2_RPW(T, 32)                                                                                  \
         PCMX_STENCIL_V2_RPW(T, 64)                                                                                  \

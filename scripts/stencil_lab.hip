@@ -16,7 +16,7 @@
 
 static int g_rows = 16384;  // rows of the slab (STENCIL_ROWS: 2048 = one rank's slab of the 16384^2 grid at N=8)
 
-template <int V, int T, int RPW, int AH = 6>
+template <int V, int T, int RPW, int AH = 6, int MINW = 1>
 void launch(const unsigned short* u, unsigned short* o, int n, int ld, int halo, float k) {
     const int rows = g_rows;
     dim3 grid(strips_for(n), (rows + kWaves * RPW - 1) / (kWaves * RPW));
@@ -24,7 +24,7 @@ void launch(const unsigned short* u, unsigned short* o, int n, int ld, int halo,
     if constexpr (V == 1)
         stencil5xT_kernel<T, 6, RPW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, sp, 0, rows, k);
     else
-        stencil5xT2_kernel<T, AH, RPW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, sp, 0, rows, k);
+        stencil5xT2_kernel<T, AH, RPW, MINW><<<grid, kWaves * 64>>>(u, o, rows, n, ld, halo, sp, 0, rows, k);
 }
 
 template <int T>
@@ -63,6 +63,23 @@ int run(const unsigned short* u, unsigned short* o, unsigned short* ref, int n, 
         if (bad) printf(" (%zu cells differ, first at slab row %zu col %zu: %04x vs %04x)\n", bad, first / ld, first % ld, a[first], b[first]);
         return 0;
     };
+    if (getenv("STENCIL_SWEEP") && !strcmp(getenv("STENCIL_SWEEP"), "short")) {
+        // short slabs (one rank's rows at N = 8): rows per wave x occupancy floor (MINW waves per SIMD)
+#define SHORT_VARIANTS(X)                                                                         \
+        X("rpw24", 24, 6, 1) X("r18a3", 18, 3, 1) X("r24a3", 24, 3, 1) X("r28a3", 28, 3, 1)               \
+        X("rpw30", 30, 6, 1) X("rpw34", 34, 6, 1) X("rpw40", 40, 6, 1) X("rpw48", 48, 6, 1)               \
+        X("r30a3", 30, 3, 1) X("r34a3", 34, 3, 1) X("r40a3", 40, 3, 1) X("r48a3", 48, 3, 1)
+#define SAME(NAME, R, A, M) same(NAME, [&] { launch<2, T, R, A, M>(u, o, n, ld, halo, k); });
+#define TIME(NAME, R, A, M) time(NAME, [&] { launch<2, T, R, A, M>(u, o, n, ld, halo, k); });
+        SHORT_VARIANTS(SAME)
+        for (int rnd = 0; rnd < 3; ++rnd) {
+            SHORT_VARIANTS(TIME)
+        }
+#undef SAME
+#undef TIME
+#undef SHORT_VARIANTS
+        return 0;
+    }
     same("v2", [&] { launch<2, T, 64>(u, o, n, ld, halo, k); });
     same("v2rpw96", [&] { launch<2, T, 96>(u, o, n, ld, halo, k); });
 

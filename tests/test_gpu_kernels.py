@@ -282,6 +282,40 @@ def test_stencil_fused_spans_match_full(gpu, steps, spans):
     assert torch.equal(out[~mask], sentinel[~mask])
 
 
+@pytest.mark.parametrize("dims", [(20000, 41, 20, 10, 20, 5), (333, 41, 20, 10, 20, 5), (50, 9, 3, 5, 2, 3),
+                                  (4000, 1301, 10, 200, 10, 50)])
+def test_spmv_banded_variants_vs_host(gpu, dims):
+    """Every banded kernel variant (0: wave per row; 1/4-7: LDS-staged windows, 4-B loads, block rows x rows in
+    flight; 2/3: 16-B loads) against the host product: interior rows, rows clipped at both matrix edges (n smaller
+    than the band reach), a row block past the last row, and rows longer than 16 x 64 nonzeros (1301 + 400 + 100:
+    the dispatcher falls back to the wave-per-row kernel for the 4-B-load variants)."""
+    n = dims[0]
+    m = ops.banded_csr(*dims)
+    x = ops.create_vector(n)
+    ref = ops.spmv(m, x)
+    vals, ro, xg = m.val.to(gpu), m.row_ptr.to(gpu), x.to(gpu)
+    for v in (0, 1, 2, 3, 4, 5, 6, 7):
+        if v in (2, 3) and dims[1] + 2 * dims[3] + 2 * dims[5] > 1021:
+            continue  # 16-B variants take rows of up to 4 x 256 - 3 nonzeros
+        out = ops.spmv_banded(vals, ro, *dims, xg, variant=v).cpu()
+        assert (out - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item()), (v, dims)
+
+
+def test_scan_check_per_stream(gpu):
+    """scan(check=True) and scan_check wait on (and read the look-back error word of) the CURRENT stream only."""
+    x = torch.rand(3 * 32768 + 11, device=gpu)
+    y = ops.scan(x, check=True)
+    side = torch.cuda.Stream(device=gpu)
+    side.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(side):
+        y2 = ops.scan(x)
+        ops.scan_check(gpu)
+    torch.cuda.current_stream(gpu).wait_stream(side)
+    ops.scan_check(gpu)
+    ref = torch.cumsum(x.double(), 0)
+    assert torch.allclose(y.double(), ref, rtol=1e-5, atol=1e-3) and torch.equal(y, y2)
+
+
 def test_spmv_banded_vs_host(gpu):
     m = ops.banded_csr(20000, 41, 20, 10, 20, 5)
     x = ops.create_vector(20000)
