@@ -62,8 +62,12 @@ def test_raycast_cli_cuda_variant(gpu, tmp_path):
 def test_spmv_cli_gpu(gpu):
     r = run_cli("run_spmv", 20000, 41, 20, 10, 20, 10, "--gpu")
     lines = r.stdout.splitlines()
-    assert sum(ln.startswith("Time : ") for ln in lines) == 2
+    # host naive + host banded, then each GPU product in the reference's format ("Time : %f s" + compare())
+    assert sum(ln.startswith("Time : ") for ln in lines) == 4
     assert any(ln.startswith("GPU CSR-adaptive") for ln in lines)
+    assert any(ln.startswith("GPU banded, implicit columns") for ln in lines)
+    assert sum(ln == "-10 more errors..." for ln in lines) == 3  # compare(): zero errors, all three products
+    assert not any(ln.startswith("Error at:") for ln in lines)
 
 
 @pytest.mark.parametrize("name,cfg,key,tol", [
