@@ -151,7 +151,8 @@ def test_sgemm_register_staged_multitile_vs_fp64(gpu, variant):
     assert ((c.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(256, 256, 256), (512, 768, 1024), (1024, 1024, 2048), (100, 70, 33), (1000, 1000, 1000)])
+@pytest.mark.parametrize("shape", [(256, 256, 256), (512, 768, 1024), (1024, 1024, 2048), (100, 70, 33), (1000, 1000, 1000),
+                                   (3500, 3600, 1000)])  # last: padded to 256-tiles + K % 64 -> direct-register kernel
 def test_sgemm_vs_fp64(gpu, shape):
     m, n, k = shape
     a = torch.rand(m, k, device=gpu) * 2 - 1
