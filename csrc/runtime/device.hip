@@ -50,13 +50,16 @@ extern "C" void pcmx_print_device_info(int device) {
 static int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 extern "C" int pcmx_sgemm_host_arrays(const float* a, const float* b, float* c, int m, int n, int k) {
-    if (pcmx_device_count() == 0) return -1;
-    const int mp = round_up(m, 128), np = round_up(n, 128), kp = round_up(k, 32);
+    if (pcmx_device_count() == 0) return (int)hipErrorNoDevice;
+    // the padding of the kernel pcmx_sgemm_f32 will pick: 256x256 tiles and K % 64 (direct-register variant 17)
+    // when the problem fills the chip with 256-tiles, else 128x128 tiles
+    const bool big = (long long)((m + 255) / 256) * ((n + 255) / 256) >= 192;
+    const int mp = round_up(m, big ? 256 : 128), np = round_up(n, big ? 256 : 128), kp = round_up(k, big ? 64 : 32);
     float *da = nullptr, *db = nullptr, *dc = nullptr;
     int rc = 0;
     if (hipMalloc(&da, sizeof(float) * (size_t)mp * kp) != hipSuccess || hipMalloc(&db, sizeof(float) * (size_t)kp * np) != hipSuccess ||
         hipMalloc(&dc, sizeof(float) * (size_t)mp * np) != hipSuccess) {
-        rc = -2;
+        rc = PCMX_ERR_ALLOC;
         goto done;
     }
     PCMX_HIP_CHECK(hipMemset(da, 0, sizeof(float) * (size_t)mp * kp));
