@@ -22,7 +22,8 @@ by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harne
            and overlapped with the product; fp64 check of every rank's rows
   (N > 1)  256 MiB RCCL all-reduce bus bandwidth
   vendor   every section carries the vendor library on the same data, timed identically: hipBLASLt
-           (torch.matmul), rocPRIM (torch.sum, torch.cumsum), hipSPARSE (torch sparse CSR x vector)
+           (torch.matmul), rocPRIM (torch.sum, torch.cumsum), hipSPARSE (torch sparse CSR x vector) and, at N = 1,
+           rocSPARSE's generic SpMV with its analysis done once (bin/spmv_vendor, a child process)
 
 rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra
 fields of the same line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
@@ -76,6 +77,27 @@ def _r(v, nd=4):
         return None
     v = float(v)
     return round(v, nd) if abs(v) >= 10 ** (3 - nd) else float(f"{v:.4g}")
+
+
+def rocsparse_bar(n_rows: int, nnz: int, reps: int) -> dict:
+    """rocSPARSE's generic SpMV (preprocess once, compute stage timed) on the same power-law matrix: bin/spmv_vendor,
+    a child process on /opt/rocm's rocSPARSE + HIP runtime (torch's sparse CSR path re-analyses the matrix per call).
+    Runs after our sections, this process idle on the GPU meanwhile."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bin", "spmv_vendor")
+    if not os.path.exists(exe):
+        return {"rocsparse_spmv_gflops": "not built (bin/spmv_vendor)"}
+    try:
+        r = subprocess.run([exe, str(n_rows), str(nnz), str(reps)], capture_output=True, text=True, timeout=240)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        res = json.loads(line)
+        algs = {k[:-7]: v for k, v in res.items() if k.endswith("_gflops") and k != "best_gflops"}
+        best = max(algs, key=algs.get)
+        return {"rocsparse_spmv_gflops": res["best_gflops"], "rocsparse_spmv_alg": best,
+                "rocsparse_spmv_max_rel_err": res.get(f"{best}_max_rel_err")}
+    except Exception as e:  # the line says why the bar is missing
+        return {"rocsparse_spmv_gflops": f"failed: {type(e).__name__}: {e}"[:200]}
 
 
 def main(argv=None):
@@ -195,6 +217,8 @@ def main(argv=None):
         del sp
         free()
         log(f"spmv {out['spmv_gflops']} GFLOP/s")
+        if vendor and world == 1:
+            out.update(rocsparse_bar(int(args.spmv_rows), int(args.spmv_nnz), K))
 
     # ---- RCCL all-reduce bus bandwidth over xGMI (N > 1)
     if ctx.distributed and dev.type == "cuda" and ctx.backend == "nccl":

@@ -186,6 +186,8 @@ BIN_TOOLS = {
     # libpcmx_hip + libpcmx_cpu
     "pipeline3d": ("bin/pipeline3d_main.c", "c+hip"),
     "pipeline3d_opencl": ("bin/pipeline3d_main.c", "c+hip"),
+    # vendor-library baseline (rocSPARSE generic SpMV): a standalone process on /opt/rocm's rocSPARSE + HIP runtime
+    "spmv_vendor": ("bin/spmv_vendor_main.cpp", "rocm"),
 }
 
 
@@ -211,6 +213,10 @@ def build_bin(force=False, jobs=8):
         elif kind == "c":
             todo.append(["gcc", "-O2", "-std=gnu11", "-fopenmp", variant, f"-I{CSRC / 'include'}", str(s),
                          "-o", str(out), f"-L{LIB}", "-lpcmx_cpu", "-lm", rpath])
+        elif kind == "rocm":
+            todo.append([HIPCC, "-O2", "-std=c++17", "-Wno-deprecated-declarations", f"-I{CSRC / 'include'}", str(s),
+                         "-o", str(out), f"-L{LIB}", f"-L{ROCM / 'lib'}", "-lrocsparse", "-lpcmx_cpu", rpath,
+                         f"-Wl,-rpath,{ROCM / 'lib'}"])
         else:
             todo.append([HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", variant, f"-I{CSRC / 'include'}",
                          str(s), "-o", str(out), f"-L{LIB}", f"-L{tlib}", "-lpcmx_hip", "-lpcmx_cpu", "-lamdhip64",
