@@ -303,6 +303,17 @@ __device__ __forceinline__ int tex_slot(int j) { return j ^ ((j >> 3) & 3); }
 // distinct 16-B slots (t mod 4 left 2-way conflicts: 2.1e7 per 512^3 pack, r2_pmc/raycast.md); the read-back
 // still only permutes slots inside aligned groups of 8
 __device__ __forceinline__ int tex_slot8(int j) { return j ^ ((j >> 3) & 7); }
+// narrow texel pairs: slot of pair p (texels 2p, 2p+1) of the block's 512 — lane t writes pairs 4t..4t+3
+// (ds_write_b128, conflict-free: the rotation by p >> 3 spreads an 8-lane group over 8 distinct slots mod 8) and
+// lane j reads pair j back (ds_read_b128; only permutes inside aligned groups of 4)
+__device__ __forceinline__ int pair_slot(int p) { return 4 * (p >> 2) + (((p & 3) + (p >> 3)) & 3); }
+// The 1 GiB of texels is written once and read back only by the later march (more than the 256-MiB Infinity
+// Cache holds): nontemporal 16-B stores took the 512^3 pack from ~300 to ~206 us (profiles/r3_raycast/pack_nt.txt;
+// the same loads with ordinary 16-B stores: 300 us, so the write-allocate path, not the stores' count, was the cost)
+using u32x4_t = unsigned __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_nt16(uint4 t, uint4* p) {
+    __builtin_nontemporal_store(u32x4_t{t.x, t.y, t.z, t.w}, reinterpret_cast<u32x4_t*>(p));
+}
 
 // A block covers 1024 consecutive texels of one z-plane in row-major (y, x) order (rows of several y when
 // dim < 1024; dim % 4 == 0 keeps a thread's 4 texels in one row), so every thread is busy (one block per row
@@ -376,7 +387,8 @@ __global__ __launch_bounds__(128) void brick_pack8_kernel(const unsigned char* _
     // the loads in flight of one plane per block, (ZP+1)/(2 ZP) of the row loads). The pack is latency-bound, not
     // VALU- or bandwidth-bound: 1 GiB of texels took ~370 us with ZP = 1 against a 155-us 1-GiB fill (counters:
     // 130 MB fetched); a byte-transpose (v_perm) assembly and an XCD-contiguous unit order changed nothing.
-    // Measured at 512^3: ZP 1 / 2 / 4 / 8 = 367 / 301 / 285 / 283 us (LDS-free direct stores: 537 us).
+    // Measured at 512^3: ZP 1 / 2 / 4 / 8 = 367 / 301 / 285 / 283 us (LDS-free direct stores: 537 us); with
+    // nontemporal 16-B stores ZP 2 / 4 / 8 = 207 / 206 / 209 us (round 3).
     const int lane = pcmx::lane_id();
     const size_t P = (size_t)dim * dim;
     const size_t lin0 = (size_t)blockIdx.x * 1024;
@@ -416,28 +428,152 @@ __global__ __launch_bounds__(128) void brick_pack8_kernel(const unsigned char* _
         const int z = zb + k;
         if (z >= dim) break;  // block-uniform
         if (k) __syncthreads();  // the previous plane's stage has been read back
+        unsigned w[8][4];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const unsigned r0 = pair8(r[k][0], rn[k][0], r[k][1], rn[k][1], i);
             const unsigned r1 = pair8(r[k + 1][0], rn[k + 1][0], r[k + 1][1], rn[k + 1][1], i);
             const unsigned d0 = pair8(d[k][0], dn[k][0], d[k][1], dn[k][1], i);
             const unsigned d1 = pair8(d[k + 1][0], dn[k + 1][0], d[k + 1][1], dn[k + 1][1], i);
-            stage[tex_slot8(threadIdx.x * 8 + i)] =
-                wide ? make_uint4(d0, d1, r0, r1) : make_uint4(d0 | (r0 << 7), d1 | (r1 << 7), 0u, 0u);
+            w[i][0] = wide ? d0 : d0 | (r0 << 7);
+            w[i][1] = wide ? d1 : d1 | (r1 << 7);
+            w[i][2] = r0, w[i][3] = r1;
         }
-        __syncthreads();
+        if (wide) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int j = i * 128 + threadIdx.x;
-            if (lin0 + j >= P) continue;
-            const uint4 t = stage[tex_slot8(j)];
-            const size_t o = (size_t)z * P + lin0 + j;
-            if (wide)
-                reinterpret_cast<uint4*>(tex)[o] = t;
-            else
-                reinterpret_cast<uint2*>(tex)[o] = make_uint2(t.x, t.y);
+            for (int i = 0; i < 8; ++i) stage[tex_slot8(threadIdx.x * 8 + i)] = make_uint4(w[i][0], w[i][1], w[i][2], w[i][3]);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int j = i * 128 + threadIdx.x;
+                if (lin0 + j >= P) continue;
+                const uint4 t = stage[tex_slot8(j)];
+                store_nt16(t, reinterpret_cast<uint4*>(tex) + (size_t)z * P + lin0 + j);
+            }
+        } else {  // narrow: texel PAIRS (2 x 8 B) per 16-B slot and store
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                stage[pair_slot(threadIdx.x * 4 + m)] = make_uint4(w[2 * m][0], w[2 * m][1], w[2 * m + 1][0], w[2 * m + 1][1]);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = i * 128 + threadIdx.x;  // pair j = texels lin0 + 2j, lin0 + 2j + 1 (P is even)
+                if (lin0 + 2 * j >= P) continue;
+                store_nt16(stage[pair_slot(j)], reinterpret_cast<uint4*>(tex) + ((size_t)z * P + lin0) / 2 + j);
+            }
         }
     }
+}
+
+// Production pack for 16 <= dim <= 1024, dim % 8 == 0 (round 3). Differences to brick_pack8_kernel:
+//  * one 12-B buffer load per source row (bytes x .. x+11: the 8 texel bytes AND the next byte, no byte loads,
+//    no lane shift; lanes at a row's right edge load x-4 .. x+7 and clamp the next byte onto x+7);
+//  * ZP = 2 planes per block (60 VGPRs, 8 waves per SIMD: the loads run from cold HBM after the previous frame's
+//    march, where occupancy, not instruction count, sets the rate; profiles/r3_raycast/pack_nt.txt);
+//  * nontemporal 16-B stores of texel pairs;
+//  * no format pre-pass: the narrow kernel ORs the data bytes it loads anyway and raises the wide flag itself; a
+//    small wide kernel launched behind it returns at once unless the flag is set, and then rewrites every texel
+//    in the 16-B format (the data_hibit_kernel scan of the whole volume, 25 us per frame, is gone).
+using u32x3_t = unsigned __attribute__((ext_vector_type(3)));
+template <int ZP, bool kWide>
+__device__ __forceinline__ bool pack12_unit(const unsigned char* __restrict__ data,
+                                            const unsigned char* __restrict__ region, int dim, void* __restrict__ tex,
+                                            unsigned unit, int zb, uint4* stage) {
+    const unsigned P = (unsigned)dim * (unsigned)dim;
+    const unsigned lin0 = unit * 1024u;
+    const unsigned lin = min(lin0 + threadIdx.x * 8u, P - 8u);
+    const int y = (int)(lin / (unsigned)dim), x = (int)(lin % (unsigned)dim);
+    const int y1 = min(y + 1, dim - 1);
+    const bool edge = x + 8 >= dim;
+    const unsigned nbytes = P * (unsigned)dim;
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(data), (short)0, (int)nbytes, 0x00020000);
+    const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(region), (short)0, (int)nbytes, 0x00020000);
+    u32x3_t dw[ZP + 1][2], rw[ZP + 1][2];
+#pragma unroll
+    for (int j = 0; j <= ZP; ++j) {
+        const unsigned pl = (unsigned)min(zb + j, dim - 1) * P;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const unsigned o = pl + (unsigned)(e ? y1 : y) * (unsigned)dim + (unsigned)x - (edge ? 4u : 0u);
+            dw[j][e] = __builtin_amdgcn_raw_buffer_load_b96(rd, o, 0, 0);
+            rw[j][e] = __builtin_amdgcn_raw_buffer_load_b96(rr, o, 0, 0);
+        }
+    }
+    unsigned long long d[ZP + 1][2], r[ZP + 1][2], hi = 0;
+    unsigned dn[ZP + 1][2], rn[ZP + 1][2];
+#pragma unroll
+    for (int j = 0; j <= ZP; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const u32x3_t a = dw[j][e], b = rw[j][e];
+            d[j][e] = edge ? ((unsigned long long)a.z << 32 | a.y) : ((unsigned long long)a.y << 32 | a.x);
+            hi |= d[j][e];
+            const unsigned long long rb = edge ? ((unsigned long long)b.z << 32 | b.y) : ((unsigned long long)b.y << 32 | b.x);
+            dn[j][e] = edge ? (a.z >> 24) : (a.z & 0xffu);
+            rn[j][e] = (edge ? (b.z >> 24) : (b.z & 0xffu)) ? 1u : 0u;
+            r[j][e] = nz_bytes64(rb);
+        }
+#pragma unroll
+    for (int k = 0; k < ZP; ++k) {
+        const int z = zb + k;
+        if (z >= dim) break;  // block-uniform
+        __syncthreads();      // the previous plane's (or unit's) stage has been read back
+        unsigned w[8][4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const unsigned r0 = pair8(r[k][0], rn[k][0], r[k][1], rn[k][1], i);
+            const unsigned r1 = pair8(r[k + 1][0], rn[k + 1][0], r[k + 1][1], rn[k + 1][1], i);
+            const unsigned d0 = pair8(d[k][0], dn[k][0], d[k][1], dn[k][1], i);
+            const unsigned d1 = pair8(d[k + 1][0], dn[k + 1][0], d[k + 1][1], dn[k + 1][1], i);
+            w[i][0] = kWide ? d0 : d0 | (r0 << 7);
+            w[i][1] = kWide ? d1 : d1 | (r1 << 7);
+            w[i][2] = r0, w[i][3] = r1;
+        }
+        if constexpr (kWide) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) stage[tex_slot8(threadIdx.x * 8 + i)] = make_uint4(w[i][0], w[i][1], w[i][2], w[i][3]);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const unsigned j = i * 128u + threadIdx.x;
+                if (lin0 + j >= P) continue;
+                store_nt16(stage[tex_slot8(j)], reinterpret_cast<uint4*>(tex) + (size_t)z * P + lin0 + j);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                stage[pair_slot(threadIdx.x * 4 + m)] = make_uint4(w[2 * m][0], w[2 * m][1], w[2 * m + 1][0], w[2 * m + 1][1]);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const unsigned j = i * 128u + threadIdx.x;  // pair j = texels lin0 + 2j, lin0 + 2j + 1 (P is even)
+                if (lin0 + 2 * j >= P) continue;
+                store_nt16(stage[pair_slot(j)], reinterpret_cast<uint4*>(tex) + ((size_t)z * P + lin0) / 2 + j);
+            }
+        }
+    }
+    return (hi & 0x8080808080808080ull) != 0;
+}
+
+template <int ZP>
+__global__ __launch_bounds__(128) void brick_pack12_narrow_kernel(const unsigned char* __restrict__ data,
+                                                                  const unsigned char* __restrict__ region, int dim,
+                                                                  void* __restrict__ tex, int* __restrict__ wide_flag) {
+    __shared__ uint4 stage[512];
+    const bool hi = pack12_unit<ZP, false>(data, region, dim, tex, blockIdx.x, (int)blockIdx.y * ZP, stage);
+    if (__syncthreads_or(hi) && threadIdx.x == 0) atomicOr(wide_flag, 1);
+}
+
+// grid-stride over (unit, plane group); every block returns at once while the flag is clear (the common case)
+template <int ZP>
+__global__ __launch_bounds__(128) void brick_pack12_wide_kernel(const unsigned char* __restrict__ data,
+                                                                const unsigned char* __restrict__ region, int dim,
+                                                                void* __restrict__ tex, const int* __restrict__ wide_flag,
+                                                                unsigned units, unsigned groups) {
+    if (__hip_atomic_load(wide_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    __shared__ uint4 stage[1024];
+    for (unsigned t = blockIdx.x; t < units * groups; t += gridDim.x)
+        pack12_unit<ZP, true>(data, region, dim, tex, t % units, (int)(t / units) * ZP, stage);
 }
 
 __device__ __forceinline__ float bilerp4(unsigned w, float ax, float ay) {
@@ -670,9 +806,16 @@ extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* r
     const size_t nvox = (size_t)dim * dim * dim;
     int* wide = reinterpret_cast<int*>(reinterpret_cast<char*>(tex) + nvox * 16);  // format flag behind the texels
     PCMX_HIP_RET(hipMemsetAsync(wide, 0, sizeof(int), s));
-    data_hibit_kernel<<<1024, 256, 0, s>>>(data, nvox, wide);
     const dim3 units((unsigned)(((size_t)dim * dim + 1023) / 1024), dim);  // 1024-texel units of each z-plane
     const size_t align = reinterpret_cast<size_t>(data) | reinterpret_cast<size_t>(region);
+    if (dim % 8 == 0 && dim >= 16 && dim <= 1024 && align % 4 == 0) {  // 32-bit buffer offsets: dim^3 <= 2^30
+        constexpr int ZP = 2;
+        const unsigned groups = (unsigned)(dim + ZP - 1) / ZP;
+        brick_pack12_narrow_kernel<ZP><<<dim3(units.x, groups), 128, 0, s>>>(data, region, dim, tex, wide);
+        brick_pack12_wide_kernel<ZP><<<1024, 128, 0, s>>>(data, region, dim, tex, wide, units.x, groups);
+        return (int)hipGetLastError();
+    }
+    data_hibit_kernel<<<1024, 256, 0, s>>>(data, nvox, wide);
     if (dim % 8 == 0 && align % 8 == 0)
         brick_pack8_kernel<4><<<dim3(units.x, (dim + 3) / 4), 128, 0, s>>>(data, region, dim, tex, wide);
     else if (dim % 4 == 0 && align % 4 == 0)

@@ -706,7 +706,9 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
     meta.item0[n_slices] = slice_item0[n_slices];
     for (int k = 0; k < n_slices; ++k) meta.colbase[k] = slice_colbase ? slice_colbase[k] : 0;
     so.out0[n_slices] = slice_out0[n_slices];
-    if (most > 0) {
+    // bit 4: products only (no combine / fix-up), bit 5: combine + fix-up only — a row-chunked caller runs chunk
+    // q's combine on a second stream while chunk q + 1's products run
+    if (most > 0 && !(mode & 32)) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -739,6 +741,7 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         }
 #undef PCMX_SLICED
     }
+    if (mode & 16) return (int)hipGetLastError();
     const unsigned cb = (unsigned)((n_rows + 2047) / 2048) * 8;  // 4 waves of 64 rows per block, 8k blocks
     switch (n_slices) {
         case 8: spmv_combine_kernel<8><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;

@@ -1,10 +1,13 @@
 // Brick-pack lab: where do the 288 us of brick_pack8_kernel<4> (512^3 narrow texels, 1 GiB written) go?
 // Includes the production kernels and adds variants on the same 1024-texel units x 4-plane grid:
-//   prod      production kernel (8-B texel stores, LDS stage of uint4 slots)
+//   prod      production kernel (round 3: texel pairs, nontemporal 16-B stores; was 8-B texel stores, ~300 us)
 //   st16      same loads, texel PAIRS staged as uint4 and stored 16 B per lane (half the store instructions)
 //   store8    stores only (8 B per lane, no loads, no LDS)           -> write roofline of this grid/store width
 //   store16   stores only (16 B per lane)
 //   loads     loads + texel assembly only, nothing stored (one conditional store keeps the work alive)
+//   st16nt    st16 with nontemporal stores (-> 206 us: adopted as prod)
+//   v2*       one 12-B buffer load per source row instead of 8-B + byte loads; z2/z8 = 2/8 planes per block
+//   st16ntS   nontemporal 16-B stores only
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/kernels -Icsrc/runtime \
 //          scripts/pack_lab.hip -o build/pack_lab
 #include "../csrc/kernels/raycast.hip"
@@ -16,9 +19,7 @@
 namespace lab {
 using namespace std;
 
-// pair slot p (texels 2p, 2p+1) of the block's 512: conflict-free ds_write_b128 for lanes writing pairs 4t..4t+3
-// (t = lane) and ds_read_b128 for lane j reading pair j (only permutes inside aligned groups of 4)
-__device__ __forceinline__ int pair_slot(int p) { return 4 * (p >> 2) + (((p & 3) + (p >> 3)) & 3); }
+// pair_slot (the narrow texel-pair LDS slot) comes from csrc/kernels/raycast.hip
 
 template <int ZP, int MODE>  // MODE 0 = st16, 1 = store8, 2 = store16, 3 = loads only
 __global__ __launch_bounds__(128) void pack_variant(const unsigned char* __restrict__ data,
@@ -113,6 +114,190 @@ __global__ __launch_bounds__(128) void pack_variant(const unsigned char* __restr
     }
     if (MODE == 3 && acc == 0x9e3779b9u) reinterpret_cast<unsigned*>(tex)[threadIdx.x] = acc;
 }
+
+// v2: one 12-B buffer load per source row (bytes x .. x+11: the texel bytes AND the next byte, no byte loads and no
+// lane shift; lanes at the row's right edge load x-4 .. x+7 and clamp the next byte onto x+7) -> 10 instead of 40
+// load instructions per thread per 4-plane block. NT: nontemporal 16-B texel-pair stores. LOADS_ONLY: no stores.
+using u32x3 = unsigned __attribute__((ext_vector_type(3)));
+using u32x4 = unsigned __attribute__((ext_vector_type(4)));
+template <int ZP, bool NT, bool LOADS_ONLY>
+__global__ __launch_bounds__(128) void pack_v2(const unsigned char* __restrict__ data,
+                                               const unsigned char* __restrict__ region, int dim,
+                                               void* __restrict__ tex) {
+    const size_t P = (size_t)dim * dim;
+    const size_t lin0 = (size_t)blockIdx.x * 1024;
+    const int zb = blockIdx.y * ZP;
+    const size_t lin = min(lin0 + (size_t)threadIdx.x * 8, P - 8);
+    const int y = (int)(lin / dim), x = (int)(lin % dim);
+    const int y1 = min(y + 1, dim - 1);
+    const bool edge = x + 8 >= dim;
+    const unsigned nbytes = (unsigned)(P * (size_t)dim);
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(data), (short)0, (int)nbytes, 0x00020000);
+    const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(region), (short)0, (int)nbytes, 0x00020000);
+    u32x3 dw[ZP + 1][2], rw[ZP + 1][2];
+#pragma unroll
+    for (int j = 0; j <= ZP; ++j) {
+        const unsigned pl = (unsigned)min(zb + j, dim - 1) * (unsigned)P;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const unsigned o = pl + (unsigned)(e ? y1 : y) * (unsigned)dim + (unsigned)x - (edge ? 4u : 0u);
+            dw[j][e] = __builtin_amdgcn_raw_buffer_load_b96(rd, o, 0, 0);
+            rw[j][e] = __builtin_amdgcn_raw_buffer_load_b96(rr, o, 0, 0);
+        }
+    }
+    unsigned long long d[ZP + 1][2], r[ZP + 1][2];
+    unsigned dn[ZP + 1][2], rn[ZP + 1][2];
+#pragma unroll
+    for (int j = 0; j <= ZP; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const u32x3 a = dw[j][e], b = rw[j][e];
+            d[j][e] = edge ? ((unsigned long long)a.z << 32 | a.y) : ((unsigned long long)a.y << 32 | a.x);
+            const unsigned long long rb = edge ? ((unsigned long long)b.z << 32 | b.y) : ((unsigned long long)b.y << 32 | b.x);
+            dn[j][e] = edge ? (a.z >> 24) : (a.z & 0xffu);
+            rn[j][e] = (edge ? (b.z >> 24) : (b.z & 0xffu)) ? 1u : 0u;
+            r[j][e] = nz_bytes64(rb);
+        }
+    __shared__ uint4 stage[512];
+    unsigned acc = 0;
+#pragma unroll
+    for (int k = 0; k < ZP; ++k) {
+        const int z = zb + k;
+        if (z >= dim) break;
+        if (!LOADS_ONLY && k) __syncthreads();
+        unsigned w[8][2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const unsigned r0 = pair8(r[k][0], rn[k][0], r[k][1], rn[k][1], i);
+            const unsigned r1 = pair8(r[k + 1][0], rn[k + 1][0], r[k + 1][1], rn[k + 1][1], i);
+            const unsigned d0 = pair8(d[k][0], dn[k][0], d[k][1], dn[k][1], i);
+            const unsigned d1 = pair8(d[k + 1][0], dn[k + 1][0], d[k + 1][1], dn[k + 1][1], i);
+            w[i][0] = d0 | (r0 << 7);
+            w[i][1] = d1 | (r1 << 7);
+        }
+        if (LOADS_ONLY) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc ^= w[i][0] + w[i][1];
+            continue;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            stage[pair_slot(threadIdx.x * 4 + m)] = make_uint4(w[2 * m][0], w[2 * m][1], w[2 * m + 1][0], w[2 * m + 1][1]);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = i * 128 + threadIdx.x;  // pair j = texels lin0 + 2j, lin0 + 2j + 1
+            if (lin0 + 2 * j >= P) continue;
+            uint4* dst = reinterpret_cast<uint4*>(tex) + ((size_t)z * P + lin0) / 2 + j;
+            if (NT) {
+                const uint4 t = stage[pair_slot(j)];
+                __builtin_nontemporal_store(u32x4{t.x, t.y, t.z, t.w}, reinterpret_cast<u32x4*>(dst));
+            } else
+                *dst = stage[pair_slot(j)];
+        }
+    }
+    if (LOADS_ONLY && acc == 0x9e3779b9u) reinterpret_cast<unsigned*>(tex)[threadIdx.x] = acc;
+}
+
+// rolling: ZP planes per block, source planes loaded PD ahead through a register ring (PD + 2 planes of raw
+// 12-B rows live) instead of all ZP + 1 up front -> deep ZP (fewer re-read planes) at a small VGPR count
+template <int ZP, int PD>
+__global__ __launch_bounds__(128) void pack_roll(const unsigned char* __restrict__ data,
+                                                 const unsigned char* __restrict__ region, int dim,
+                                                 void* __restrict__ tex, int* __restrict__ flag) {
+    const unsigned P = (unsigned)dim * (unsigned)dim;
+    const unsigned lin0 = blockIdx.x * 1024u;
+    const unsigned lin = min(lin0 + threadIdx.x * 8u, P - 8u);
+    const int y = (int)(lin / (unsigned)dim), x = (int)(lin % (unsigned)dim);
+    const int y1 = min(y + 1, dim - 1), zb = (int)blockIdx.y * ZP;
+    const bool edge = x + 8 >= dim;
+    const unsigned nbytes = P * (unsigned)dim;
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(data), (short)0, (int)nbytes, 0x00020000);
+    const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(region), (short)0, (int)nbytes, 0x00020000);
+    const unsigned o0 = (unsigned)y * (unsigned)dim + (unsigned)x - (edge ? 4u : 0u);
+    const unsigned o1 = (unsigned)y1 * (unsigned)dim + (unsigned)x - (edge ? 4u : 0u);
+    constexpr int R = PD + 2;
+    u32x3 dw[R][2], rw[R][2];
+    auto load = [&](int j) __attribute__((always_inline)) {
+        const unsigned pl = (unsigned)min(zb + j, dim - 1) * P;
+        dw[j % R][0] = __builtin_amdgcn_raw_buffer_load_b96(rd, pl + o0, 0, 0);
+        rw[j % R][0] = __builtin_amdgcn_raw_buffer_load_b96(rr, pl + o0, 0, 0);
+        dw[j % R][1] = __builtin_amdgcn_raw_buffer_load_b96(rd, pl + o1, 0, 0);
+        rw[j % R][1] = __builtin_amdgcn_raw_buffer_load_b96(rr, pl + o1, 0, 0);
+    };
+#pragma unroll
+    for (int j = 0; j <= PD; ++j) load(j);
+    __shared__ uint4 stage[512];
+    unsigned long long hi = 0;
+#pragma unroll
+    for (int k = 0; k < ZP; ++k) {
+        if (k + PD + 1 <= ZP) load(k + PD + 1);
+        const int z = zb + k;
+        if (z >= dim) break;
+        unsigned long long d[2][2], r[2][2];
+        unsigned dn[2][2], rn[2][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const u32x3 a = dw[(k + q) % R][e], b = rw[(k + q) % R][e];
+                d[q][e] = edge ? ((unsigned long long)a.z << 32 | a.y) : ((unsigned long long)a.y << 32 | a.x);
+                if (q == 0) hi |= d[q][e];
+                const unsigned long long rb = edge ? ((unsigned long long)b.z << 32 | b.y) : ((unsigned long long)b.y << 32 | b.x);
+                dn[q][e] = edge ? (a.z >> 24) : (a.z & 0xffu);
+                rn[q][e] = (edge ? (b.z >> 24) : (b.z & 0xffu)) ? 1u : 0u;
+                r[q][e] = nz_bytes64(rb);
+            }
+        unsigned w[8][2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const unsigned r0 = pair8(r[0][0], rn[0][0], r[0][1], rn[0][1], i);
+            const unsigned r1 = pair8(r[1][0], rn[1][0], r[1][1], rn[1][1], i);
+            w[i][0] = pair8(d[0][0], dn[0][0], d[0][1], dn[0][1], i) | (r0 << 7);
+            w[i][1] = pair8(d[1][0], dn[1][0], d[1][1], dn[1][1], i) | (r1 << 7);
+        }
+        if (k) __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            stage[pair_slot(threadIdx.x * 4 + m)] = make_uint4(w[2 * m][0], w[2 * m][1], w[2 * m + 1][0], w[2 * m + 1][1]);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const unsigned j = i * 128u + threadIdx.x;
+            if (lin0 + 2 * j >= P) continue;
+            const uint4 t = stage[pair_slot(j)];
+            __builtin_nontemporal_store(u32x4{t.x, t.y, t.z, t.w}, reinterpret_cast<u32x4*>(tex) + ((size_t)z * P + lin0) / 2 + j);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (__syncthreads_or((hi & 0x8080808080808080ull) != 0) && threadIdx.x == 0) atomicOr(flag, 1);
+}
+
+__global__ __launch_bounds__(256) void read_flush(const uint4* __restrict__ p, size_t n, unsigned* __restrict__ sink) {
+    unsigned acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const uint4 v = p[i];
+        acc ^= v.x + v.y + v.z + v.w;
+    }
+    if (acc == 0x9e3779b9u) sink[threadIdx.x] = acc;
+}
+
+// stores only, nontemporal 16 B
+template <int ZP>
+__global__ __launch_bounds__(128) void store16_nt(int dim, void* __restrict__ tex) {
+    const size_t P = (size_t)dim * dim;
+    const size_t lin0 = (size_t)blockIdx.x * 1024;
+    const int zb = blockIdx.y * ZP;
+#pragma unroll
+    for (int k = 0; k < ZP; ++k) {
+        const int z = zb + k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = i * 128 + threadIdx.x;
+            __builtin_nontemporal_store(u32x4{(unsigned)j, (unsigned)z, (unsigned)j, (unsigned)z}, reinterpret_cast<u32x4*>(tex) + ((size_t)z * P + lin0) / 2 + j);
+        }
+    }
+}
 }  // namespace lab
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
@@ -125,14 +310,14 @@ int main() {
     int* flag;
     CK(hipMalloc(&data, n));
     CK(hipMalloc(&region, n));
-    CK(hipMalloc(&tex, n * 8));
+    CK(hipMalloc(&tex, n * 16 + 16));
     CK(hipMalloc(&tex2, n * 8));
     CK(hipMalloc(&flag, 4));
     CK(hipMemset(flag, 0, 4));
     CK((hipError_t)pcmx_volume_gen_u8(data, dim, 0, 0));
     volume_gen_kernel<<<dim3((dim + 255) / 256, dim, dim), 256>>>(region, dim, 7);  // any bytes: region != 0 test
     CK(hipDeviceSynchronize());
-    const dim3 grid((unsigned)((size_t)dim * dim / 1024), dim / 4);
+    const dim3 grid((unsigned)((size_t)dim * dim / 1024), dim / 4), grid2(grid.x, dim / 2), grid8(grid.x, dim / 8), grid16(grid.x, dim / 16), grid32(grid.x, dim / 32);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
@@ -147,20 +332,93 @@ int main() {
         printf("%-8s %7.1f us  (%.2f TB/s of texel writes)\n", name, ms * 100.f, (double)n * 8 / (ms / 10 * 1e-3) / 1e12);
         fflush(stdout);
     };
+    // cold: a 1-GiB READ between launches evicts the inputs from L2 / Infinity Cache without leaving dirty lines
+    // (as the march's texel reads do between the frames' packs in the ray-cast workload); only the pack is timed
+    void* flush;
+    CK(hipMalloc(&flush, (size_t)1 << 30));
+    hipEvent_t c0[10], c1[10];
+    for (int i = 0; i < 10; ++i) hipEventCreate(&c0[i]), hipEventCreate(&c1[i]);
+    auto cold = [&](const char* name, auto launch) {
+        launch();
+        for (int i = 0; i < 10; ++i) {
+            lab::read_flush<<<4096, 256>>>(reinterpret_cast<const uint4*>(flush), ((size_t)1 << 30) / 16,
+                                           reinterpret_cast<unsigned*>(flush));
+            hipEventRecord(c0[i]);
+            launch();
+            hipEventRecord(c1[i]);
+        }
+        hipDeviceSynchronize();
+        float tot = 0;
+        for (int i = 0; i < 10; ++i) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, c0[i], c1[i]);
+            tot += ms;
+        }
+        printf("cold %-8s %7.1f us\n", name, tot * 100.f);
+        fflush(stdout);
+    };
     for (int round = 0; round < 2; ++round) {
-        time("prod", [&] { brick_pack8_kernel<4><<<grid, 128>>>(data, region, dim, tex, flag); });
+        cold("prod", [&] { pcmx_brick_pack(data, region, dim, tex, 0); });
+        cold("pack8", [&] { brick_pack8_kernel<4><<<grid, 128>>>(data, region, dim, tex, flag); });
+        cold("p12n_z2", [&] { brick_pack12_narrow_kernel<2><<<grid2, 128>>>(data, region, dim, tex2, flag); });
+        cold("p12n_z4", [&] { brick_pack12_narrow_kernel<4><<<grid, 128>>>(data, region, dim, tex2, flag); });
+        cold("p12n_z8", [&] { brick_pack12_narrow_kernel<8><<<grid8, 128>>>(data, region, dim, tex2, flag); });
+        cold("p12n_z16", [&] { brick_pack12_narrow_kernel<16><<<grid16, 128>>>(data, region, dim, tex2, flag); });
+        cold("roll8_1", [&] { lab::pack_roll<8, 1><<<grid8, 128>>>(data, region, dim, tex2, flag); });
+        cold("roll8_2", [&] { lab::pack_roll<8, 2><<<grid8, 128>>>(data, region, dim, tex2, flag); });
+        cold("roll16_1", [&] { lab::pack_roll<16, 1><<<grid16, 128>>>(data, region, dim, tex2, flag); });
+        cold("roll16_2", [&] { lab::pack_roll<16, 2><<<grid16, 128>>>(data, region, dim, tex2, flag); });
+        cold("roll16_3", [&] { lab::pack_roll<16, 3><<<grid16, 128>>>(data, region, dim, tex2, flag); });
+        cold("roll32_2", [&] { lab::pack_roll<32, 2><<<grid32, 128>>>(data, region, dim, tex2, flag); });
+        cold("gate", [&] { brick_pack12_wide_kernel<2><<<1024, 128>>>(data, region, dim, tex2, flag, grid.x, dim / 2); });
+        cold("memset4", [&] { hipMemsetAsync(flag, 0, 4); });
+        cold("st16nt", [&] { lab::pack_v2<4, true, false><<<grid, 128>>>(data, region, dim, tex2); });
+        cold("v2_z2nt", [&] { lab::pack_v2<2, true, false><<<grid2, 128>>>(data, region, dim, tex2); });
+        cold("v2_z8nt", [&] { lab::pack_v2<8, true, false><<<grid8, 128>>>(data, region, dim, tex2); });
+        cold("v2loads", [&] { lab::pack_v2<4, false, true><<<grid, 128>>>(data, region, dim, tex2); });
+        cold("loads", [&] { lab::pack_variant<4, 3><<<grid, 128>>>(data, region, dim, tex2); });
+        cold("st16ntS", [&] { lab::store16_nt<4><<<grid, 128>>>(dim, tex2); });
+    }
+    for (int round = 0; round < 2; ++round) {
+        time("prod", [&] { pcmx_brick_pack(data, region, dim, tex, 0); });
+        time("pack8", [&] { brick_pack8_kernel<4><<<grid, 128>>>(data, region, dim, tex, flag); });
         time("st16", [&] { lab::pack_variant<4, 0><<<grid, 128>>>(data, region, dim, tex2); });
         time("store8", [&] { lab::pack_variant<4, 1><<<grid, 128>>>(data, region, dim, tex2); });
         time("store16", [&] { lab::pack_variant<4, 2><<<grid, 128>>>(data, region, dim, tex2); });
         time("loads", [&] { lab::pack_variant<4, 3><<<grid, 128>>>(data, region, dim, tex2); });
+        time("st16nt", [&] { lab::pack_v2<4, true, false><<<grid, 128>>>(data, region, dim, tex2); });
+        time("v2", [&] { lab::pack_v2<4, false, false><<<grid, 128>>>(data, region, dim, tex2); });
+        time("v2_z2nt", [&] { lab::pack_v2<2, true, false><<<grid2, 128>>>(data, region, dim, tex2); });
+        time("v2_z8nt", [&] { lab::pack_v2<8, true, false><<<grid8, 128>>>(data, region, dim, tex2); });
+        time("v2loads", [&] { lab::pack_v2<4, false, true><<<grid, 128>>>(data, region, dim, tex2); });
+        time("st16ntS", [&] { lab::store16_nt<4><<<grid, 128>>>(dim, tex2); });
     }
     // st16 must produce the production texels byte for byte
-    brick_pack8_kernel<4><<<grid, 128>>>(data, region, dim, tex, flag);
+    pcmx_brick_pack(data, region, dim, tex, 0);
     lab::pack_variant<4, 0><<<grid, 128>>>(data, region, dim, tex2);
     CK(hipDeviceSynchronize());
     std::vector<unsigned char> a(n * 8), b(n * 8);
     CK(hipMemcpy(a.data(), tex, n * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(b.data(), tex2, n * 8, hipMemcpyDeviceToHost));
     printf("st16 identical to prod: %s\n", memcmp(a.data(), b.data(), n * 8) == 0 ? "yes" : "NO");
+    for (int v = 3; v < 6; ++v) {
+        CK(hipMemset(tex2, 0xab, n * 8));
+        if (v == 3) lab::pack_roll<8, 1><<<grid8, 128>>>(data, region, dim, tex2, flag);
+        if (v == 4) lab::pack_roll<16, 2><<<grid16, 128>>>(data, region, dim, tex2, flag);
+        if (v == 5) lab::pack_roll<32, 2><<<grid32, 128>>>(data, region, dim, tex2, flag);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(b.data(), tex2, n * 8, hipMemcpyDeviceToHost));
+        printf("roll variant %d identical to prod: %s\n", v, memcmp(a.data(), b.data(), n * 8) == 0 ? "yes" : "NO");
+    }
+    for (int v = 0; v < 3; ++v) {
+        CK(hipMemset(tex2, 0xab, n * 8));
+        if (v == 0) lab::pack_v2<4, true, false><<<grid, 128>>>(data, region, dim, tex2);
+        if (v == 1) lab::pack_v2<2, true, false><<<grid2, 128>>>(data, region, dim, tex2);
+        if (v == 2) lab::pack_v2<8, true, false><<<grid8, 128>>>(data, region, dim, tex2);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(b.data(), tex2, n * 8, hipMemcpyDeviceToHost));
+        printf("v2 (ZP %d, nt) identical to prod: %s\n", v == 0 ? 4 : v == 1 ? 2 : 8,
+               memcmp(a.data(), b.data(), n * 8) == 0 ? "yes" : "NO");
+    }
     return 0;
 }

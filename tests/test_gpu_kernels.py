@@ -131,11 +131,12 @@ def test_raycast_texture_close(gpu):
     assert abs(a.mean().item() - b.mean().item()) < 3.0
 
 
-@pytest.mark.parametrize("dim", [20, 21, 64, 72])
+@pytest.mark.parametrize("dim", [8, 16, 20, 21, 64, 72])
 @pytest.mark.parametrize("hi", [128, 256])
 def test_brick_pack_texels(gpu, dim, hi):
     # texel = 2x2x2 footprint of data then region, edge-clamped; narrow 8-B texels (region in bit 7) when every
-    # data value < 128, else 16-B texels; vector (dim % 4 == 0) and scalar pack kernels vs a plain torch gather
+    # data value < 128, else 16-B texels; 12-B-row (dim % 8 == 0, >= 16: narrow kernel + flag-gated wide kernel),
+    # vector (dim % 4 == 0) and scalar pack kernels vs a plain torch gather
     g = torch.Generator().manual_seed(dim + hi)
     d = torch.randint(0, hi, (dim, dim, dim), dtype=torch.uint8, generator=g)
     r = (torch.rand(dim, dim, dim, generator=g) < 0.3).to(torch.uint8) * 7
