@@ -468,8 +468,10 @@ __global__ __launch_bounds__(128) void brick_pack8_kernel(const unsigned char* _
 // Production pack for 16 <= dim <= 1024, dim % 8 == 0 (round 3). Differences to brick_pack8_kernel:
 //  * one 12-B buffer load per source row (bytes x .. x+11: the 8 texel bytes AND the next byte, no byte loads,
 //    no lane shift; lanes at a row's right edge load x-4 .. x+7 and clamp the next byte onto x+7);
-//  * ZP = 2 planes per block (60 VGPRs, 8 waves per SIMD: the loads run from cold HBM after the previous frame's
-//    march, where occupancy, not instruction count, sets the rate; profiles/r3_raycast/pack_nt.txt);
+//  * ZP = 8 planes per block, all 9 source planes' rows loaded up front (152 VGPRs, 3 waves per SIMD): the loads
+//    run from cold HBM after the previous frame's march, and the deeper block re-reads 1/8 instead of 1/2 of the
+//    planes: cold pack ZP 2 / 4 / 8 / 16 = 245-261 / 232-245 / 225-237 / 271-282 us; a rolling register ring
+//    (planes loaded 1-3 ahead, ZP 8-32) 239-400 us (profiles/r3_raycast/pack_cold_zp.txt);
 //  * nontemporal 16-B stores of texel pairs;
 //  * no format pre-pass: the narrow kernel ORs the data bytes it loads anyway and raises the wide flag itself; a
 //    small wide kernel launched behind it returns at once unless the flag is set, and then rewrites every texel
@@ -809,10 +811,9 @@ extern "C" int pcmx_brick_pack(const unsigned char* data, const unsigned char* r
     const dim3 units((unsigned)(((size_t)dim * dim + 1023) / 1024), dim);  // 1024-texel units of each z-plane
     const size_t align = reinterpret_cast<size_t>(data) | reinterpret_cast<size_t>(region);
     if (dim % 8 == 0 && dim >= 16 && dim <= 1024 && align % 4 == 0) {  // 32-bit buffer offsets: dim^3 <= 2^30
-        constexpr int ZP = 2;
-        const unsigned groups = (unsigned)(dim + ZP - 1) / ZP;
-        brick_pack12_narrow_kernel<ZP><<<dim3(units.x, groups), 128, 0, s>>>(data, region, dim, tex, wide);
-        brick_pack12_wide_kernel<ZP><<<1024, 128, 0, s>>>(data, region, dim, tex, wide, units.x, groups);
+        constexpr int ZP = 8, ZPW = 2;  // wide rewrite: 2 planes per unit (its 16-B texels double the stores)
+        brick_pack12_narrow_kernel<ZP><<<dim3(units.x, (dim + ZP - 1) / ZP), 128, 0, s>>>(data, region, dim, tex, wide);
+        brick_pack12_wide_kernel<ZPW><<<512, 128, 0, s>>>(data, region, dim, tex, wide, units.x, (dim + ZPW - 1) / ZPW);
         return (int)hipGetLastError();
     }
     data_hibit_kernel<<<1024, 256, 0, s>>>(data, nvox, wide);
