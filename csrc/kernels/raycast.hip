@@ -13,7 +13,7 @@
 //    Rays are clipped analytically to the volume and only the steps inside are visited (prefetched in
 //    batches of 16 steps; only the raw texels stay live across a batch) and every 16x4 ray patch is split over
 //    4 waves by step range (partial colours composed in ray order). 512^2 image of the 512^3 reference volume:
-//    march 2.7 -> 1.16 -> 0.83 ms; frame (pack + march) 3.18 -> 1.66 -> ~1.14 ms.
+//    march 2.7 -> 1.16 -> 0.83 ms; frame (pack + march) 3.18 -> 1.66 -> 1.18 -> 1.07 ms.
 //  * raycast_global marches positions by repeated f32 adds exactly like the reference, but skips sampling
 //    while the ray is outside the volume's bounding box (the adds still run, so positions are unchanged)
 //    and stops once the ray has left it (a convex box cannot be re-entered): identical images, far fewer
