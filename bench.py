@@ -26,7 +26,8 @@ by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harne
            rocSPARSE's generic SpMV with its analysis done once (bin/spmv_vendor, a child process)
 
 rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra
-fields of the same line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
+fields of the same line. A section after SGEMM that raises is reported as "<section>_error" in the line (its
+fields missing) instead of costing the line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
 """
 from __future__ import annotations
 
@@ -144,11 +145,21 @@ def main(argv=None):
         free()
         log(f"sgemm {tflops:.1f} TFLOPS")
 
+    def guarded(name, fn):
+        """Runs one extra section; an exception (raised on every rank alike, e.g. a shape or check failure) is
+        recorded as "<name>_error" in the line instead of costing the whole line (the headline SGEMM value and the
+        other sections still report). A section that hangs is not caught: the driver's time limit ends the run."""
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            out[f"{name}_error"] = f"{type(e).__name__}: {e}"[:300]
+            log(f"{name} FAILED: {out[name + '_error']}")
+        free()  # (after the except block: the traceback no longer pins the section's tensors)
+
     # ---- reduce / scan: weak (rn per GPU) and strong (rn in total); identical runs at N = 1
     rn = int(args.reduce_n)
-    for name, cls in (("reduce", W.Reduce), ("scan", W.Scan)):
-        if name not in sections:
-            continue
+
+    def reduce_scan(name, cls):
         for mode, per_rank in (("weak", rn), ("strong", -(-rn // world))):
             if mode == "strong" and world == 1:
                 for k in ("gbps", "ms_per_step", "rel_err_vs_fp64"):
@@ -177,8 +188,12 @@ def main(argv=None):
             free()
         log(f"{name} weak {out[name + '_weak_gbps']} GB/s, strong {out[name + '_strong_gbps']} GB/s")
 
+    for name, cls in (("reduce", W.Reduce), ("scan", W.Scan)):
+        if name in sections:
+            guarded(name, lambda: reduce_scan(name, cls))
+
     # ---- stencil 16384^2 bf16, strong scaling over row slabs with the overlapped fused halo exchange
-    if "stencil" in sections:
+    def stencil():
         s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse)
         t = timed(ctx, s.step, K, Wm)
         rep = s.report(t, K)
@@ -189,11 +204,13 @@ def main(argv=None):
                     "stencil_timed_grid_updates": chk["timed_grid_updates"],
                     "stencil_bit_exact": chk["bit_exact_vs_single_step_oracle"], "stencil_finite": chk["finite"]})
         del s
-        free()
         log(f"stencil {out['stencil_glups']} GLUP/s")
 
+    if "stencil" in sections:
+        guarded("stencil", stencil)
+
     # ---- SpMV 1e8-nnz power-law graph, strong scaling
-    if "spmv" in sections:
+    def spmv():
         vendor = not args.no_ref and dev.type == "cuda"
         sp = W.SpMV(ctx, n_rows=int(args.spmv_rows), nnz=int(args.spmv_nnz), chunks=args.spmv_chunks,
                     exchange=args.spmv_exchange, keep_plain=vendor)
@@ -220,15 +237,20 @@ def main(argv=None):
         if vendor and world == 1:
             out.update(rocsparse_bar(int(args.spmv_rows), int(args.spmv_nnz), K))
 
+    if "spmv" in sections:
+        guarded("spmv", spmv)
+
     # ---- RCCL all-reduce bus bandwidth over xGMI (N > 1)
-    if ctx.distributed and dev.type == "cuda" and ctx.backend == "nccl":
+    def allreduce():
         import torch.distributed as dist
 
         v = torch.ones(64 << 20, device=dev)
         kr = max(3, K // 2)
         t_ar = timed(ctx, lambda: dist.all_reduce(v), kr, 1)
         out["allreduce_256MiB_busbw_gbps"] = _r(v.numel() * 4 * 2 * (world - 1) / world * kr / t_ar / 1e9, 1)
-        del v
+
+    if ctx.distributed and dev.type == "cuda" and ctx.backend == "nccl":
+        guarded("allreduce", allreduce)
 
     if rank == 0:
         line = {

@@ -38,6 +38,7 @@ def _check_line(out, n):
     assert out["stencil_bit_exact"] and out["stencil_finite"]
     assert out["sgemm_max_rel_err_vs_fp64"] < 1e-5 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
     assert out["reduce_strong_rel_err_vs_fp64"] < 1e-5 and out["scan_strong_rel_err_vs_fp64"] < 1e-5
+    assert not [k for k in out if k.endswith("_error")], out
 
 
 def test_bench_small_one_gpu(gpu):

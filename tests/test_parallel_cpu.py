@@ -344,6 +344,27 @@ def test_bench_rehearsal_gloo_world2():
     assert out["stencil_bit_exact"] and out["stencil_finite"]
     assert out["sgemm_max_rel_err_vs_fp64"] < 1e-5 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
     assert out["reduce_strong_rel_err_vs_fp64"] < 1e-5 and out["scan_strong_rel_err_vs_fp64"] < 1e-5
+    assert not [k for k in out if k.endswith("_error")]
+
+
+def test_bench_failed_section_is_reported_not_fatal():
+    """A section that raises (here: an unsupported stencil fuse depth) costs only its own fields: the line still
+    prints once, with "<section>_error", and the later sections still run."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT, cli_env
+
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--small", "--device", "cpu", "--steps", "1",
+                        "--warmup", "0", "--sections", "stencil,spmv", "--stencil-fuse", "99"],
+                       capture_output=True, text=True, timeout=300, env=cli_env(OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["stencil_error"].startswith("ValueError") and "stencil_glups" not in out
+    assert out["spmv_gflops"] > 0 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
 
 
 # ------------------------------------------------------------------ launcher-level (torch.distributed.run)
