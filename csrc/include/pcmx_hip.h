@@ -90,6 +90,10 @@ int pcmx_sgemm_f32(const float* A, const float* B, float* C, int M, int N, int K
  * 1 = LDS-DMA 128x128x32 / 4 waves (the lab variants live in scripts/sgemm_lab.hip) */
 int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
                            int ldc, float alpha, float beta, int variant, hipStream_t s);
+/* fp32 GEMM on the bf16 matrix cores, operands split exactly into 3 bf16 pieces, 6 piece products (fp32
+ * accuracy; sgemm_x6.hip). M, N % 256 == 0, K % 32 == 0. Also reachable as pcmx_sgemm_f32_variant(..., 20). */
+int pcmx_sgemm_f32_x6(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
+                      float alpha, float beta, hipStream_t s);
 /* Reference-style f32 VALU GEMM (one thread per output, LDS tiles) for A/B comparisons. */
 int pcmx_sgemm_f32_simt(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t s);
 

@@ -10,6 +10,8 @@
 //   variant 16  register-staged 256x256x32 tile, 8 waves (2 per SIMD, 64x128 wave tiles) — round-2 production
 //   variant 0   LDS-DMA 256x256x32 tile, 8 waves — fallback when buffer offsets would exceed 2 GiB
 //   variant 1   LDS-DMA 128x128x32 tile, 4 waves — problems with fewer than 192 256x256 tiles (fills 256 CUs)
+//   variant 20  fp32 GEMM on the BF16 matrix cores by exact 3-way operand splitting (sgemm_x6.hip): fp32
+//               accuracy, not the f32 MFMA; reported beside the headline, never as it
 //   simt        reference-style f32 VALU GEMM (the "CUDA port recompiled" baseline), any shape
 //
 // Why this shape (MI355X_MICROARCH.md "Matrix cores", cdna_hip_programming.md §3/§5):
@@ -621,6 +623,7 @@ extern "C" int pcmx_sgemm_f32_variant(const float* A, const float* B, float* C, 
         case 16: return launch_rs(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         case 17: return launch_direct(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 0, s);
         case 18: return launch_direct(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 7, s);
+        case 20: return pcmx_sgemm_f32_x6(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, s);
         default: return PCMX_ERR_ARG;
     }
 }

@@ -31,8 +31,8 @@ def sgemm(a: torch.Tensor, b: torch.Tensor, variant: int = -1) -> torch.Tensor:
         return c
     # pad to the tile of the kernel that will run: 256x256 (K % 64 for the direct-register variant 17 / 18) when the
     # problem fills the chip with 256-tiles (the default dispatch then takes variant 17), else 128x128
-    big = variant in (0, 16, 17, 18) or (variant < 0 and -(-m // 256) * -(-n // 256) >= 192)
-    tile, kq = (256, 64 if variant in (-1, 17, 18) else 32) if big else (128, 32)
+    big = variant in (0, 16, 17, 18, 20) or (variant < 0 and -(-m // 256) * -(-n // 256) >= 192)
+    tile, kq = (256, 64 if variant in (-1, 17, 18) else 32) if big else (128, 32)  # variant 20: K % 32
     mp, np_, kp = _round_up(m, tile), _round_up(n, tile), _round_up(k, kq)
     ac = a if a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0 else a.contiguous()
     bc = b if b.stride(1) == 1 and b.stride(0) % 4 == 0 and b.data_ptr() % 16 == 0 else b.contiguous()

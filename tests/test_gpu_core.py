@@ -140,7 +140,7 @@ def test_sgemm_identity_asymmetric(gpu, variant):
     assert torch.equal(c2, b)
 
 
-@pytest.mark.parametrize("variant", [0, 16, 17, 18])
+@pytest.mark.parametrize("variant", [0, 16, 17, 18, 20])
 def test_sgemm_register_staged_multitile_vs_fp64(gpu, variant):
     # several tiles in both directions and 2+ LDS stages of prefetch: M != N != K
     g = torch.Generator(device=gpu).manual_seed(variant)
@@ -181,6 +181,34 @@ def test_sgemm_direct_persistent_many_tiles(gpu, shape):
         assert err < 1e-5, (variant, err)
         plain = ops.sgemm(a, b, variant=variant)
         assert torch.equal(plain, ops.sgemm(a, b, variant=17 if variant == 18 else 18))  # same sums, any grid
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 32), (512, 768, 96), (1024, 512, 2048), (300, 200, 70)])
+def test_sgemm_x6_elementwise_fp32_accuracy(gpu, shape):
+    """Variant 20 (fp32 GEMM on the bf16 matrix cores, exact 3-way operand split, 6 piece products): per-element
+    error against the fp64 product, in units of sum |a||b|, within the native f32 MFMA kernel's bound."""
+    m, n, k = shape
+    g = torch.Generator(device=gpu).manual_seed(k)
+    a = torch.rand(m, k, device=gpu, generator=g) * 2 - 1
+    b = torch.rand(k, n, device=gpu, generator=g) * 2 - 1
+    c = ops.sgemm(a, b, variant=20)
+    ref = a.double() @ b.double()
+    scale = a.abs().double() @ b.abs().double()
+    err = ((c.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+    assert err < 4e-6 * max(1.0, (k / 256) ** 0.5), err
+
+
+def test_sgemm_x6_split_exact_wide_range(gpu):
+    """The split is exact for |x| >= 2^-110: operands spanning 2^-40 .. 2^40 (one row / column each) multiply to
+    the fp64 result within fp32 rounding, and an identity A reproduces B bit for bit."""
+    n = 256
+    scales = torch.pow(2.0, torch.linspace(-40, 40, n, device=gpu)).float()
+    b = (torch.rand(n, n, device=gpu) * 2 - 1) * scales[None, :]
+    a = torch.eye(n, device=gpu) * scales[:, None]
+    c = ops.sgemm(a, b, variant=20)
+    ref = a.double() @ b.double()
+    assert ((c.double() - ref).abs() / ref.abs().clamp_min(1e-300)).max().item() < 1e-7
+    assert torch.equal(ops.sgemm(torch.eye(n, device=gpu), b, variant=20), b)
 
 
 def test_sgemm_beta(gpu):
