@@ -7,7 +7,9 @@ own correctness check, all timed the same way (W untimed warm-up steps, then EXA
 by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harness.py):
 
   sgemm    (value) 8192^3 fp32 C = A @ B per GPU on the MFMA kernel, weak scaling; fp64 spot check; the
-           hipBLASLt torch.matmul of the same operands is timed alongside for reference
+           hipBLASLt torch.matmul of the same operands is timed alongside for reference, and so is the fp32 GEMM on
+           the bf16 matrix cores (exact 3-way operand split, 6 piece products: fp32 accuracy, its own fp64 check;
+           an extra field, never the headline value)
   reduce   global sum, local HBM reduce + one-scalar RCCL all-reduce: weak (1e9 f32 per GPU) and strong
            (1e9 f32 in total, 1e9/N per GPU); fp64 check
   scan     global inclusive prefix sum over the rank-ordered concatenation (reduce-then-scan): weak and
@@ -61,6 +63,7 @@ def parse(argv=None):
                     help="N>1 vector exchange: only the referenced entries (ghost) or the whole y (allgather)")
     ap.add_argument("--sections", default=",".join(SECTIONS), help="comma list out of " + ",".join(SECTIONS))
     ap.add_argument("--no-ref", action="store_true", help="skip the torch.matmul (hipBLASLt) reference timing")
+    ap.add_argument("--no-x6", action="store_true", help="skip the fp32-via-bf16x6 SGEMM extra (variant 20)")
     ap.add_argument("--small", action="store_true", help="tiny sizes (CPU/gloo rehearsal)")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")
     ap.add_argument("--backend", default=None, choices=("nccl", "gloo"),
@@ -141,6 +144,13 @@ def main(argv=None):
             # the vendor library timed exactly like our kernel (same warm-up and step count)
             t_ref = timed(ctx, lambda: torch.matmul(g.a, g.b, out=g.c), K, Wm)
             out["hipblaslt_torch_matmul_tflops"] = _r(world * g.work_per_step() * K / t_ref / 1e12, 3)
+        if not args.no_x6 and dev.type == "cuda" and n % 256 == 0:
+            # fp32 GEMM on the bf16 matrix cores (exact 3-way operand split, 6 piece products; sgemm_x6.hip): an
+            # fp32-accurate extra, timed identically with its own fp64 check; never the headline value
+            g.variant = 20
+            t_x6 = timed(ctx, g.step, K, Wm)
+            out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * g.work_per_step() * K / t_x6 / 1e12, 3)
+            out["sgemm_fp32_via_bf16x6_max_rel_err_vs_fp64"] = ctx.max_over_ranks(g.check()["max_rel_err_vs_fp64"])
         del g
         free()
         log(f"sgemm {tflops:.1f} TFLOPS")

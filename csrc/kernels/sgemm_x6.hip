@@ -74,6 +74,42 @@ __device__ __forceinline__ void split_b(const f32x4 (&r)[8], int j, Planes& o) {
     split8(x, o);
 }
 
+// The same split as f32x4 arithmetic (the residual subtractions become v_pk_add_f32 on register pairs):
+// A tile: r[q] holds k = 4q .. 4q+3; words d = 2q, 2q+1 of each level come from r[q].
+__device__ __forceinline__ void split_a4(f32x4 (&r)[2], Planes& o) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        f32x2 x0 = {r[q][0], r[q][1]}, x1 = {r[q][2], r[q][3]};
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            const unsigned w0 = cvt2(x0[0], x0[1]), w1 = cvt2(x1[0], x1[1]);
+            o.p[l][2 * q] = w0, o.p[l][2 * q + 1] = w1;
+            if (l < 2) x0 -= f32x2{lo16(w0), hi16(w0)}, x1 -= f32x2{lo16(w1), hi16(w1)};
+        }
+    }
+}
+// B: word d (k rows 2d, 2d+1) of every level for all 4 N-tiles; r[e] holds k row e of the 4 N-tiles' columns.
+__device__ __forceinline__ void split_b_word(const f32x4 (&r)[8], int d, Planes (&o)[4]) {
+    f32x2 x[2][2];  // [row 2d / 2d+1][N-tile pair]
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) x[e][jp] = f32x2{r[2 * d + e][2 * jp], r[2 * d + e][2 * jp + 1]};
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+        unsigned w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j].p[l][d] = w[j] = cvt2(x[0][j >> 1][j & 1], x[1][j >> 1][j & 1]);
+        if (l < 2) {
+#pragma unroll
+            for (int jp = 0; jp < 2; ++jp) {
+                x[0][jp] -= f32x2{lo16(w[2 * jp]), lo16(w[2 * jp + 1])};
+                x[1][jp] -= f32x2{hi16(w[2 * jp]), hi16(w[2 * jp + 1])};
+            }
+        }
+    }
+}
+
 // products (level of A, level of B), smallest first
 constexpr int kPA[6] = {2, 1, 0, 1, 0, 0};
 constexpr int kPB[6] = {0, 1, 2, 0, 1, 0};
@@ -84,7 +120,7 @@ __device__ __forceinline__ f32x16 mfma(const u32x4& a, const u32x4& b, const f32
 }
 
 template <bool BETA>
-__global__ __launch_bounds__(256, 1) void sgemm_x6_kernel(const float* __restrict__ A, const float* __restrict__ B,
+__global__ __launch_bounds__(256, 1) void sgemm_x6a_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                           float* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                           int ldc, float alpha, float beta) {
     const int lane = pcmx::lane_id();
@@ -204,21 +240,171 @@ __global__ __launch_bounds__(256, 1) void sgemm_x6_kernel(const float* __restric
             __builtin_amdgcn_sched_barrier(0);
         }
 }
+template <bool BETA, int VPM>
+__global__ __launch_bounds__(256, 1) void sgemm_x6_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                          float* __restrict__ C, int M, int N, int K, int lda, int ldb,
+                                                          int ldc, float alpha, float beta) {
+    const int lane = pcmx::lane_id();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+    // tile of this block: XCD remap, then column strips 8 tile-rows tall (as sgemm.hip tile_coords)
+    const int tiles_m = M / 256, tiles_n = N / 256;
+    const int t = pcmx::xcd_remap((int)blockIdx.x, tiles_m * tiles_n);
+    const int per_group = 8 * tiles_n, first_m = (t / per_group) * 8;
+    const int gsz = min(tiles_m - first_m, 8);
+    const int m0 = __builtin_amdgcn_readfirstlane((first_m + (t % per_group) % gsz) * 256);
+    const int n0 = __builtin_amdgcn_readfirstlane(((t % per_group) / gsz) * 256);
+
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, 0x7fffffff, 0x00020000);
+    int voA[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) voA[i] = ((32 * i + l32) * lda + 8 * h) * 4;
+    const int voB = (8 * h * ldb + 4 * l32) * 4;
+    const int voC = (4 * h * ldc + 4 * l32) * 4;
+    const int ab = __builtin_amdgcn_readfirstlane((m0 + wm * 128) * lda * 4);
+    const int bb = __builtin_amdgcn_readfirstlane((n0 + wn * 128) * 4);
+    const int ns = K / 16, last = ns - 1;
+    const int bstep = ldb * 64;  // bytes per 16 k-rows of B
+    auto ld = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+    };
+    auto load_a = [&](f32x4 (&dst)[2], int i, int s) __attribute__((always_inline)) {
+        const int so = ab + min(s, last) * 64;
+        dst[0] = ld(rA, voA[i], so);
+        dst[1] = ld(rA, voA[i] + 16, so);
+    };
+    auto load_b = [&](f32x4 (&dst)[8], int s) __attribute__((always_inline)) {
+        const int so = bb + min(s, last) * bstep;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dst[e] = ld(rB, voB, so + e * ldb * 4);
+    };
+
+    f32x4 ra[4][2];     // raw A of each M-tile, one step ahead of its split
+    f32x4 rb[2][8];     // raw B: [step parity][k row e]
+    Planes pa[2];       // A planes of the current / next M-tile
+    Planes pb[2][4];    // B planes: [step parity][N-tile]
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0};
+
+    // Prologue. Per step s the loop issues A1(s+1) A2(s+1) A3(s+1) A0(s+2) B(s+3); the prologue leaves the same
+    // sequence in flight (B(1) | A1(0) A2(0) A3(0) A0(1) B(2)), so the waits the compiler derives at the loop
+    // header (merged over the prologue and the back edge) count only loads issued after the awaited one.
+    load_a(ra[0], 0, 0);
+    load_b(rb[0], 0);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) split_b_word(rb[0], d, pb[0]);
+    split_a4(ra[0], pa[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    load_b(rb[1], 1);
+#pragma unroll
+    for (int i = 1; i < 4; ++i) load_a(ra[i], i, 0);
+    load_a(ra[0], 0, 1);
+    load_b(rb[0], 2);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // One 16-k step with compile-time parity P. Region i (one per M-tile) runs tile i's 24 MFMAs and, in their
+    // shadow, the split of the next A tile and of word i of the B planes for step s+1 (72 VALU ops: 3 per MFMA,
+    // interleaved by sched_group_barrier when VPM > 0).
+    auto step = [&](int s, auto P_) __attribute__((always_inline)) {
+        constexpr int P = decltype(P_)::value;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_sched_barrier(0);  // one scheduling region per M-tile: loads stay in issue order
+            const Planes& cur = pa[i & 1];
+            const int in = (i + 1) & 3;  // next A tile: i+1 of this step, or tile 0 of step s+1
+            split_a4(ra[in], pa[in & 1]);
+            load_a(ra[in], in, i < 3 ? s + 1 : s + 2);
+            split_b_word(rb[P ^ 1], i, pb[P ^ 1]);  // word i of every N-tile's planes for step s+1
+            if (i == 3) load_b(rb[P ^ 1], s + 3);
+#pragma unroll
+            for (int p = 0; p < 6; ++p)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = mfma(cur.p[kPA[p]], pb[P][j].p[kPB[p]], acc[i][j]);
+            if constexpr (VPM > 0) {
+#pragma unroll
+                for (int m = 0; m < 24; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // 1 MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);  // VPM VALU
+                }
+            }
+        }
+    };
+    for (int s = 0; s < ns; s += 2) {  // ns even (K % 32 == 0)
+        step(s, std::integral_constant<int, 0>{});
+        step(s + 1, std::integral_constant<int, 1>{});
+    }
+
+    // epilogue: lane (l32, h) holds column c0 + 4 l32 + j of N-tile j and rows 4h + (r & 3) + 8 (r >> 2) of each
+    // 32x32 tile: the 4 N-tiles form one 16-B store
+    const int r0 = m0 + wm * 128, c0 = n0 + wn * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int so = ((r0 + i * 32 + (r & 3) + 8 * (r >> 2)) * ldc + c0) * 4;
+            f32x4 v{alpha * acc[i][0][r], alpha * acc[i][1][r], alpha * acc[i][2][r], alpha * acc[i][3][r]};
+            if constexpr (BETA) v += beta * ld(rC, voC, so);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rC, voC, so, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+}
 }  // namespace
 
 // C = alpha * A @ B + beta * C, fp32 operands and result, computed on the bf16 matrix cores with exact 3-way
 // operand splitting (fp32 accuracy). M, N % 256 == 0, K % 32 == 0, 16-B aligned rows, 32-bit byte offsets.
-extern "C" int pcmx_sgemm_f32_x6(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
-                                 int ldc, float alpha, float beta, hipStream_t s) {
+namespace {
+template <class F>
+int launch_x6(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc, F&& go) {
     if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || K % 32) return PCMX_ERR_ARG;
     if ((lda | ldb | ldc) & 3 || (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15)) return PCMX_ERR_ARG;
     if ((long long)M * lda * 4 >= (1LL << 31) || (long long)K * ldb * 4 >= (1LL << 31) ||
         (long long)M * ldc * 4 >= (1LL << 31))
         return PCMX_ERR_ARG;
-    const int tiles = (M / 256) * (N / 256);
-    if (beta != 0.f)
-        sgemm_x6_kernel<true><<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta);
-    else
-        sgemm_x6_kernel<false><<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta);
+    go((M / 256) * (N / 256));
     return (int)hipGetLastError();
+}
+}  // namespace
+
+// Lab knob: 0 = production schedule, 1 = first (round-3) schedule, 2..4 = VALU ops per MFMA in the interleave
+// pattern, 5 = compiler-scheduled regions.
+extern "C" int pcmx_sgemm_f32_x6_variant(const float* A, const float* B, float* C, int M, int N, int K, int lda,
+                                         int ldb, int ldc, float alpha, float beta, int v, hipStream_t s) {
+    return launch_x6(A, B, C, M, N, K, lda, ldb, ldc, [&](int tiles) {
+#define PCMX_X6(...)                                                                                       \
+    (beta != 0.f ? __VA_ARGS__(true)<<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta)   \
+                 : __VA_ARGS__(false)<<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta))
+#define X6A(b) sgemm_x6a_kernel<b>
+#define X6V(n) X6V_##n
+#define X6V_2(b) sgemm_x6_kernel<b, 2>
+#define X6V_3(b) sgemm_x6_kernel<b, 3>
+#define X6V_4(b) sgemm_x6_kernel<b, 4>
+#define X6V_0(b) sgemm_x6_kernel<b, 0>
+        switch (v) {
+            case 1: PCMX_X6(X6A); break;
+            case 2: PCMX_X6(X6V_2); break;
+            case 4: PCMX_X6(X6V_4); break;
+            case 5: PCMX_X6(X6V_0); break;
+            default: PCMX_X6(X6V_3); break;
+        }
+#undef X6A
+#undef X6V
+#undef X6V_0
+#undef X6V_2
+#undef X6V_3
+#undef X6V_4
+#undef PCMX_X6
+    });
+}
+
+// C = alpha * A @ B + beta * C, fp32 operands and result, computed on the bf16 matrix cores with exact 3-way
+// operand splitting (fp32 accuracy). M, N % 256 == 0, K % 32 == 0, 16-B aligned rows, 32-bit byte offsets.
+extern "C" int pcmx_sgemm_f32_x6(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
+                                 int ldc, float alpha, float beta, hipStream_t s) {
+    return pcmx_sgemm_f32_x6_variant(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, 0, s);
 }
