@@ -72,12 +72,15 @@ for v in xv:
     x6(a, b, c, v)
     print(json.dumps({"x6_schedule": v, "n": n, "max_rel_err_vs_fp64": err(c, a, b, rows)}), flush=True)
 flop = 2.0 * n ** 3
+ah, bh, ch = a.bfloat16(), b.bfloat16(), torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
 res = {}
 for _ in range(rounds):
     res.setdefault("v17_native_f32", []).append(t_ms(lambda: ops.sgemm_out(a, b, c, variant=17), K))
     for v in xv:
         res.setdefault(f"x6_sched{v}", []).append(t_ms(lambda: x6(a, b, c, v), K))
     res.setdefault("hipblaslt", []).append(t_ms(lambda: torch.matmul(a, b, out=c), K))
+    # calibration: the vendor's plain bf16 GEMM rate on this box (x6 does 6x its MFMA work per fp32 GEMM)
+    res.setdefault("hipblaslt_bf16_x6_equiv", []).append(6 * t_ms(lambda: torch.matmul(ah, bh, out=ch), K))
 for k_, v in res.items():
     print(json.dumps({"cfg": k_, "n": n, "ms_all": [round(x, 4) for x in v], "best_tflops": round(flop / min(v) / 1e9, 2),
                       "median_tflops": round(flop / sorted(v)[len(v) // 2] / 1e9, 2)}), flush=True)
