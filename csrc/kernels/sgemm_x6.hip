@@ -21,11 +21,13 @@
 //  * k step of 16: lane (l32, h) needs A[row l32][k0 + 8h + e] and B[k0 + 8h + e][col] for e = 0..7:
 //    A = two 16-B loads of its row; B = eight 16-B loads of B[k0 + 8h + e][c0 + 4 l32 .. +3], i.e. N-tile j owns
 //    columns c0 + 4c + j (one 16-B load feeds 4 N-tiles; the epilogue stores 16 B per lane).
-//  * Split cost: 9 VALU ops per pair of elements (3 v_cvt_pk_bf16_f32, 4 unpacks, 2 subtractions), 288 per wave
-//    per 16-k step against 96 MFMAs (3072 cycles): ~3 ops in each MFMA gap, issued in the MFMA shadow.
-//  * Raw fp32 operands are prefetched two steps ahead in a 2-slot ring per operand (slot = step parity); the
-//    split planes of A tile i+1 are produced while tile i's MFMAs run, the planes of B for step s+1 while the last
-//    tile of step s runs (N-tile j's planes are rebuilt right after its last MFMA of the step).
+//  * Split cost: 11 VALU ops per pair of elements (3 v_cvt_pk_bf16_f32, 4 unpacks, 4 subtractions), 352 per wave
+//    per 16-k step against 96 MFMAs (3072 cycles): 3-4 ops in every MFMA gap (sched_group_barrier pattern), issued
+//    in the MFMA shadow. Raw A is loaded one step ahead of its split, raw B two (2-slot ring); each M-tile's region
+//    splits the next A tile and one k-word of all four B tiles for the next step (B planes double-buffered).
+//  * Measured (profiles/r3_sgemm_x6/): 8192^3 in 4.11-4.15 ms = 265-267 TFLOPS, 1.73x hipBLASLt's fp32 GEMM, MFMA
+//    busy 89% of the active cycles; the 6x bf16 work runs at 1.60 PF, above hipBLASLt's own bf16 GEMM on the box
+//    (1.41 PF): the kernel is bound by the power-limited clock under dense bf16 MFMA, not by issue.
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 #include <type_traits>
@@ -49,33 +51,9 @@ __device__ __forceinline__ unsigned cvt2(float a, float b) {
 __device__ __forceinline__ float lo16(unsigned w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi16(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
 
-// Elements x[e], e = 0..7 (k order) -> three bf16x8 planes with x[e] == p0[e] + p1[e] + p2[e].
-__device__ __forceinline__ void split8(const float (&x)[8], Planes& o) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        float a = x[2 * d], b = x[2 * d + 1];
-        unsigned w = cvt2(a, b);
-        o.p[0][d] = w;
-        a -= lo16(w), b -= hi16(w);
-        w = cvt2(a, b);
-        o.p[1][d] = w;
-        a -= lo16(w), b -= hi16(w);
-        o.p[2][d] = cvt2(a, b);
-    }
-}
-__device__ __forceinline__ void split_a(const f32x4 (&r)[2], Planes& o) {
-    const float x[8] = {r[0][0], r[0][1], r[0][2], r[0][3], r[1][0], r[1][1], r[1][2], r[1][3]};
-    split8(x, o);
-}
-__device__ __forceinline__ void split_b(const f32x4 (&r)[8], int j, Planes& o) {
-    float x[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = r[e][j];
-    split8(x, o);
-}
-
-// The same split as f32x4 arithmetic (the residual subtractions become v_pk_add_f32 on register pairs):
-// A tile: r[q] holds k = 4q .. 4q+3; words d = 2q, 2q+1 of each level come from r[q].
+// Split of 8 elements (k order) into three bf16x8 planes, x == p0 + p1 + p2: per pair of elements 3
+// v_cvt_pk_bf16_f32, 2 unpacks and 2 residual subtractions for each of 2 levels (f32x2 arithmetic; the compiler
+// unpacks v_pk_add_f32 in the MFMA shadow). A tile: r[q] holds k = 4q .. 4q+3; words d = 2q, 2q+1 of each level come from r[q].
 __device__ __forceinline__ void split_a4(f32x4 (&r)[2], Planes& o) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -119,127 +97,6 @@ __device__ __forceinline__ f32x16 mfma(const u32x4& a, const u32x4& b, const f32
                                                    0, 0);
 }
 
-template <bool BETA>
-__global__ __launch_bounds__(256, 1) void sgemm_x6a_kernel(const float* __restrict__ A, const float* __restrict__ B,
-                                                          float* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                                          int ldc, float alpha, float beta) {
-    const int lane = pcmx::lane_id();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int h = lane >> 5, l32 = lane & 31;
-    // tile of this block: XCD remap, then column strips 8 tile-rows tall (as sgemm.hip tile_coords)
-    const int tiles_m = M / 256, tiles_n = N / 256;
-    const int t = pcmx::xcd_remap((int)blockIdx.x, tiles_m * tiles_n);
-    const int per_group = 8 * tiles_n, first_m = (t / per_group) * 8;
-    const int gsz = min(tiles_m - first_m, 8);
-    const int m0 = __builtin_amdgcn_readfirstlane((first_m + (t % per_group) % gsz) * 256);
-    const int n0 = __builtin_amdgcn_readfirstlane(((t % per_group) / gsz) * 256);
-
-    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, 0x7fffffff, 0x00020000);
-    int voA[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) voA[i] = ((32 * i + l32) * lda + 8 * h) * 4;
-    const int voB = (8 * h * ldb + 4 * l32) * 4;
-    const int voC = (4 * h * ldc + 4 * l32) * 4;
-    const int ab = __builtin_amdgcn_readfirstlane((m0 + wm * 128) * lda * 4);
-    const int bb = __builtin_amdgcn_readfirstlane((n0 + wn * 128) * 4);
-    const int ns = K / 16, last = ns - 1;
-    const int bstep = ldb * 64;  // bytes per 16 k-rows of B
-    auto ld = [](__amdgpu_buffer_rsrc_t r, int vo, int so) {
-        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
-    };
-    auto load_a = [&](f32x4 (&dst)[2], int i, int s) __attribute__((always_inline)) {
-        const int so = ab + min(s, last) * 64;
-        dst[0] = ld(rA, voA[i], so);
-        dst[1] = ld(rA, voA[i] + 16, so);
-    };
-    auto load_b = [&](f32x4 (&dst)[8], int s) __attribute__((always_inline)) {
-        const int so = bb + min(s, last) * bstep;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dst[e] = ld(rB, voB, so + e * ldb * 4);
-    };
-
-    f32x4 ra[2][4][2];  // raw A: [step parity][M-tile][half]
-    f32x4 rb[2][8];     // raw B: [step parity][k row e]
-    Planes pa[2];       // A planes of the current / next M-tile
-    Planes pb[4];       // B planes of the 4 N-tiles (current step)
-    f32x16 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0};
-
-    // Prologue. The loop issues its loads in the order A1(s+2) A2(s+2) A3(s+2) B(s+3) A0(s+3) per step s; the
-    // prologue leaves the same sequence in flight (for steps -2 and -1), so the waits the compiler derives at the
-    // loop header (merged over the prologue and the back edge) count only loads issued after the awaited one.
-    load_a(ra[0][0], 0, 0);
-    load_b(rb[0], 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) split_b(rb[0], j, pb[j]);
-    split_a(ra[0][0], pa[0]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int i = 1; i < 4; ++i) load_a(ra[s][i], i, s);
-        load_b(rb[s ^ 1], s + 1);
-        load_a(ra[s ^ 1][0], 0, s + 1);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-
-    // one 16-k step with compile-time parity P (ring slot of step s)
-    auto step = [&](int s, auto P_) __attribute__((always_inline)) {
-        constexpr int P = decltype(P_)::value;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            __builtin_amdgcn_sched_barrier(0);  // one scheduling region per M-tile: loads stay in issue order
-            const Planes& cur = pa[i & 1];
-            if (i < 3) {  // planes of tile i+1 (this step) while tile i's MFMAs run
-                split_a(ra[P][i + 1], pa[(i + 1) & 1]);
-                load_a(ra[P][i + 1], i + 1, s + 2);
-            }
-            if (i < 3) {
-#pragma unroll
-                for (int p = 0; p < 6; ++p)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[i][j] = mfma(cur.p[kPA[p]], pb[j].p[kPB[p]], acc[i][j]);
-            } else {
-                // last tile: N-tile by N-tile, rebuilding its planes for step s+1 right after its last use
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                    for (int p = 0; p < 6; ++p) acc[3][j] = mfma(cur.p[kPA[p]], pb[j].p[kPB[p]], acc[3][j]);
-                    split_b(rb[P ^ 1], j, pb[j]);
-                }
-                load_b(rb[P ^ 1], s + 3);
-                __builtin_amdgcn_sched_barrier(0);
-                split_a(ra[P ^ 1][0], pa[0]);
-                load_a(ra[P ^ 1][0], 0, s + 3);
-            }
-        }
-    };
-    for (int s = 0; s < ns; s += 2) {  // ns even (K % 32 == 0)
-        step(s, std::integral_constant<int, 0>{});
-        step(s + 1, std::integral_constant<int, 1>{});
-    }
-
-    // epilogue: lane (l32, h) holds column c0 + 4 l32 + j of N-tile j and rows 4h + (r & 3) + 8 (r >> 2) of each
-    // 32x32 tile: the 4 N-tiles form one 16-B store
-    const int r0 = m0 + wm * 128, c0 = n0 + wn * 128;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int so = ((r0 + i * 32 + (r & 3) + 8 * (r >> 2)) * ldc + c0) * 4;
-            f32x4 v{alpha * acc[i][0][r], alpha * acc[i][1][r], alpha * acc[i][2][r], alpha * acc[i][3][r]};
-            if constexpr (BETA) v += beta * ld(rC, voC, so);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rC, voC, so, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-}
 template <bool BETA, int VPM>
 __global__ __launch_bounds__(256, 1) void sgemm_x6_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                           float* __restrict__ C, int M, int N, int K, int lda, int ldb,
@@ -356,8 +213,6 @@ __global__ __launch_bounds__(256, 1) void sgemm_x6_kernel(const float* __restric
 }
 }  // namespace
 
-// C = alpha * A @ B + beta * C, fp32 operands and result, computed on the bf16 matrix cores with exact 3-way
-// operand splitting (fp32 accuracy). M, N % 256 == 0, K % 32 == 0, 16-B aligned rows, 32-bit byte offsets.
 namespace {
 template <class F>
 int launch_x6(const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb, int ldc, F&& go) {
@@ -371,33 +226,22 @@ int launch_x6(const float* A, const float* B, float* C, int M, int N, int K, int
 }
 }  // namespace
 
-// Lab knob: 0 = production schedule, 1 = first (round-3) schedule, 2..4 = VALU ops per MFMA in the interleave
-// pattern, 5 = compiler-scheduled regions.
+// Lab knob: 0 = production schedule (3 VALU per MFMA), 2 / 4 = 2 / 4 VALU per MFMA in the interleave pattern,
+// 5 = compiler-scheduled regions. Measured at 8192^3 (profiles/r3_sgemm_x6/ab_schedules.log): 4.15 / 4.35 / 4.20 /
+// 4.49 ms; the first form (B planes rebuilt only in the last M-tile's region, compiler-scheduled) 4.73 ms.
 extern "C" int pcmx_sgemm_f32_x6_variant(const float* A, const float* B, float* C, int M, int N, int K, int lda,
                                          int ldb, int ldc, float alpha, float beta, int v, hipStream_t s) {
     return launch_x6(A, B, C, M, N, K, lda, ldb, ldc, [&](int tiles) {
-#define PCMX_X6(...)                                                                                       \
-    (beta != 0.f ? __VA_ARGS__(true)<<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta)   \
-                 : __VA_ARGS__(false)<<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta))
-#define X6A(b) sgemm_x6a_kernel<b>
-#define X6V(n) X6V_##n
-#define X6V_2(b) sgemm_x6_kernel<b, 2>
-#define X6V_3(b) sgemm_x6_kernel<b, 3>
-#define X6V_4(b) sgemm_x6_kernel<b, 4>
-#define X6V_0(b) sgemm_x6_kernel<b, 0>
+#define PCMX_X6(VPM)                                                                                                  \
+    (beta != 0.f                                                                                                      \
+         ? sgemm_x6_kernel<true, VPM><<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta)             \
+         : sgemm_x6_kernel<false, VPM><<<tiles, 256, 0, s>>>(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta))
         switch (v) {
-            case 1: PCMX_X6(X6A); break;
-            case 2: PCMX_X6(X6V_2); break;
-            case 4: PCMX_X6(X6V_4); break;
-            case 5: PCMX_X6(X6V_0); break;
-            default: PCMX_X6(X6V_3); break;
+            case 2: PCMX_X6(2); break;
+            case 4: PCMX_X6(4); break;
+            case 5: PCMX_X6(0); break;
+            default: PCMX_X6(3); break;
         }
-#undef X6A
-#undef X6V
-#undef X6V_0
-#undef X6V_2
-#undef X6V_3
-#undef X6V_4
 #undef PCMX_X6
     });
 }
