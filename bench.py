@@ -16,7 +16,7 @@ by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harne
            strong like reduce; fp64 check of EVERY output of every rank incl. its rank offset, after the stream's
            look-back error word (scan_check)
   stencil  16384^2 bf16 5-point stencil, strong scaling: row slabs, T fused updates per kernel (T by slab
-           height: 8 / 6 / 6 / 4 at N = 1 / 2 / 4 / 8) and one T-row halo exchange per neighbour overlapped with
+           height: 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8) and one T-row halo exchange per neighbour overlapped with
            the interior update; bit-exact checks: the timed grid itself (all warm-up + timed updates) against a
            plain-PyTorch single-step oracle, and a small grid through the same distributed path
   spmv     power-law CSR, 1e8 nnz / 1e7 rows, strong scaling: nnz-balanced row blocks, XCD-sliced kernel,
@@ -55,7 +55,7 @@ def parse(argv=None):
     ap.add_argument("--reduce-n", type=float, default=1e9, help="f32 elements (per GPU weak, in total strong)")
     ap.add_argument("--stencil-n", type=int, default=16384)
     ap.add_argument("--stencil-fuse", type=int, default=0,
-                    help="fused updates per kernel / halo depth (0: by slab height, 8 / 6 / 6 / 4 at N = 1 / 2 / 4 / 8)")
+                    help="fused updates per kernel / halo depth (0: by slab height, 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8)")
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
     ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")

@@ -153,77 +153,97 @@ __global__ __launch_bounds__(kWaves * 64) void stencil5_kernel(const unsigned sh
 //    computed from zero-initialised windows and never reach a stored value.
 //  * Slab: (rows + 2*halo) x ld, local row r at slab row r + halo. Rows within T of a rank boundary read T
 //    halo rows (halo >= T, checked by the launcher); at a GLOBAL edge the clamped rows only feed Dirichlet rows.
-constexpr int kOutCols = kStripCols - 16;  // 496 output columns per wave strip
-// Strip x loads columns [x*496, x*496 + 512): lanes 1..62 store [x*496 + 8, x*496 + 504). A lane whose first or last
-// column is a GLOBAL edge column (Dirichlet, never changes) stays exact at every level, so lane 0 of strip 0 and a
-// lane 63 ending at column cols-1 store too: 16384 columns = 504 + 31 x 496 + 504, 33 strips instead of 34.
-__device__ __forceinline__ int strip_c0(int lane) { return (int)blockIdx.x * kOutCols + lane * 8; }
-__device__ __forceinline__ bool strip_store_lane(int lane, int c0, int cols, bool in_grid) {
-    return in_grid && ((lane >= 1 && lane <= 62) || c0 == 0 || c0 + 8 == cols);
-}
-
-__device__ __forceinline__ void unpack8(const u32x4& w, float (&v)[8]) {
-    v[0] = lo(w.x), v[1] = hi(w.x), v[2] = lo(w.y), v[3] = hi(w.y);
-    v[4] = lo(w.z), v[5] = hi(w.z), v[6] = lo(w.w), v[7] = hi(w.w);
-}
-
-// one update of a lane's 8 columns (rounded to bf16, returned packed and as floats). Dirichlet handling:
-// `fixed_row` is wave-uniform (a scalar branch, taken on 2 rows of the whole grid); columns 0 / cols-1 can
-// only be element 0 / 7 of a lane (cols % 8 == 0), so they are per-lane flags.
-// ---- packed-f32 row arithmetic (the fused kernel is VALU-bound: one wave64 VALU op per 4 cycles per SIMD)
-// A lane's 8 columns live as 4 PAIRS p[k] = (e_k, e_{k+4}), so every v_pk_* op works on aligned register
-// pairs: the west neighbours of pair k are pair k-1 and the east neighbours pair k+1; only pair 0's west
-// and pair 3's east need a lane shift (DPP). Per 8 cells: 24 packed flops, 4 shifts/moves, 12 ops of
-// bf16 rounding (v_cvt_pk_bf16_f32 + unpack) — ~40 VALU ops instead of ~100 for the scalar form.
-typedef float f2 __attribute__((ext_vector_type(2)));
-struct Row8 {
-    f2 p[4];
+// LANE GEOMETRY. A lane holds CPL consecutive columns (8: one 16-B row load, as above; 4: one 8-B load, twice the
+// waves and half the registers per wave, for short slabs that fill the chip with too few waves). The values of the
+// first / last L = ceil(T / CPL) lanes of a strip go stale (one column per level from the strip edge), so lanes
+// L .. 63-L store: a strip loads 64*CPL columns and stores OUT = (64 - 2L)*CPL. Strip x loads
+// [x*OUT, x*OUT + 64*CPL). At a GLOBAL edge column (Dirichlet, never changes) nothing goes stale: strip 0 stores its
+// lanes 0 .. L-1 and the strip holding column cols-1 its lanes beyond 63-L. 8 columns, T <= 8: 16384 columns =
+// 504 + 31 x 496 + 504, 33 strips.
+template <int CPL, int T>
+struct Geo {
+    static constexpr int NP = CPL / 2;  // column pairs per lane
+    static constexpr int L = (T + CPL - 1) / CPL;
+    static constexpr int OUT = (64 - 2 * L) * CPL;
+    static_assert(CPL == 4 || CPL == 8, "4 or 8 columns per lane");
+    static_assert(L >= 1 && 2 * L < 64, "stale lanes");
+    __device__ static int c0(int lane) { return (int)blockIdx.x * OUT + lane * CPL; }
+    __device__ static bool store_lane(int lane, int cols, bool in_grid) {
+        const int x0 = (int)blockIdx.x * OUT;
+        return in_grid && (lane >= L || x0 == 0) && (lane <= 63 - L || x0 + 64 * CPL >= cols);
+    }
 };
-__device__ __forceinline__ Row8 unpack_pairs(const u32x4& w) {  // words: (e0|e1) (e2|e3) (e4|e5) (e6|e7)
-    Row8 r;
-    r.p[0] = f2{lo(w.x), lo(w.z)};
-    r.p[1] = f2{hi(w.x), hi(w.z)};
-    r.p[2] = f2{lo(w.y), lo(w.w)};
-    r.p[3] = f2{hi(w.y), hi(w.w)};
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+template <int NP>
+struct RawT;
+template <>
+struct RawT<2> {
+    typedef u32x2 type;
+};
+template <>
+struct RawT<4> {
+    typedef u32x4 type;
+};
+
+// ---- packed-f32 row arithmetic (the fused kernel is VALU-bound: one wave64 VALU op per 4 cycles per SIMD)
+// A lane's CPL columns live as NP = CPL/2 PAIRS p[q] = (e_q, e_{q+NP}), so every v_pk_* op works on aligned register
+// pairs: the west neighbours of pair q are pair q-1 and the east neighbours pair q+1; only pair 0's west and pair
+// NP-1's east need a lane shift (DPP). Per 8 cells: 24 packed flops, 4 shifts/moves, 12 ops of bf16 rounding
+// (v_cvt_pk_bf16_f32 + unpack) — ~40 VALU ops instead of ~100 for the scalar form.
+typedef float f2 __attribute__((ext_vector_type(2)));
+template <int NP>
+struct RowP {
+    f2 p[NP];
+};
+using Row8 = RowP<4>;
+// raw words w[d] = (e_2d | e_2d+1) <-> pairs
+template <int NP>
+__device__ __forceinline__ RowP<NP> unpack_pairs(const typename RawT<NP>::type& w) {
+    auto elem = [&](int i) { return (i & 1) ? hi(w[i >> 1]) : lo(w[i >> 1]); };
+    RowP<NP> r;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) r.p[q] = f2{elem(q), elem(q + NP)};
     return r;
 }
-__device__ __forceinline__ u32x4 pack_pairs(const Row8& r) {
-    u32x4 w;
-    w.x = pack2bf(r.p[0].x, r.p[1].x);
-    w.y = pack2bf(r.p[2].x, r.p[3].x);
-    w.z = pack2bf(r.p[0].y, r.p[1].y);
-    w.w = pack2bf(r.p[2].y, r.p[3].y);
+template <int NP>
+__device__ __forceinline__ typename RawT<NP>::type pack_pairs(const RowP<NP>& r) {
+    auto elem = [&](int i) { return i < NP ? r.p[i].x : r.p[i - NP].y; };
+    typename RawT<NP>::type w;
+#pragma unroll
+    for (int d = 0; d < NP; ++d) w[d] = pack2bf(elem(2 * d), elem(2 * d + 1));
     return w;
 }
 
-// One update of a lane's 8 columns in pair layout; returns the bf16 row (packed) and, via nx, its exact float
-// values for the next level. fixed_row is wave-uniform (a scalar branch, taken on 2 rows of the grid);
-// columns 0 / cols-1 can only be element 0 / 7 of a lane (cols % 8 == 0): per-lane flags.
-__device__ __forceinline__ u32x4 update_pairs(const Row8& n, const Row8& c, const Row8& s, bool fixed_row, bool fix0,
-                                              bool fix7, float k, Row8& nx) {
-    u32x4 pk;
+// One update of a lane's columns in pair layout; returns the bf16 row (packed) and, via nx, its exact float values
+// for the next level. fixed_row is wave-uniform (a scalar branch, taken on 2 rows of the grid); columns 0 / cols-1
+// can only be the first / last element of a lane (cols % 8 == 0): per-lane flags.
+template <int NP>
+__device__ __forceinline__ typename RawT<NP>::type update_pairs(const RowP<NP>& n, const RowP<NP>& c,
+                                                                const RowP<NP>& s, bool fixed_row, bool fix0,
+                                                                bool fixl, float k, RowP<NP>& nx) {
+    typename RawT<NP>::type pk;
     if (fixed_row) {
-        pk = pack_pairs(c);
+        pk = pack_pairs<NP>(c);
     } else {
-        // west pair of pair 0 = (e_{-1}, e_3), east pair of pair 3 = (e_4, e_8)
-        const f2 w0 = f2{pcmx::wave_from_prev(c.p[3].y), c.p[3].x};
-        const f2 e3 = f2{c.p[0].y, pcmx::wave_from_next(c.p[0].x)};
+        // west pair of pair 0 = (e_{-1}, e_{NP-1}), east pair of pair NP-1 = (e_NP, e_{2NP})
+        const f2 w0 = f2{pcmx::wave_from_prev(c.p[NP - 1].y), c.p[NP - 1].x};
+        const f2 eL = f2{c.p[0].y, pcmx::wave_from_next(c.p[0].x)};
         const f2 kk = f2{k, k}, m4 = f2{-4.f, -4.f};
-        Row8 o;
+        RowP<NP> o;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NP; ++q) {
             const f2 w = q == 0 ? w0 : c.p[q - 1];
-            const f2 e = q == 3 ? e3 : c.p[q + 1];
+            const f2 e = q == NP - 1 ? eL : c.p[q + 1];
             const f2 t3 = (n.p[q] + s.p[q]) + (w + e);
             // t3 - 4c with 4c exact == fma(c, -4, t3): one rounding, bit-identical to the reference
             const f2 lap = __builtin_elementwise_fma(c.p[q], m4, t3);
             o.p[q] = c.p[q] + kk * lap;
         }
         o.p[0].x = fix0 ? c.p[0].x : o.p[0].x;
-        o.p[3].y = fix7 ? c.p[3].y : o.p[3].y;
-        pk = pack_pairs(o);
+        o.p[NP - 1].y = fixl ? c.p[NP - 1].y : o.p[NP - 1].y;
+        pk = pack_pairs<NP>(o);
     }
-    nx = unpack_pairs(pk);
+    nx = unpack_pairs<NP>(pk);
     return pk;
 }
 
@@ -246,36 +266,38 @@ __device__ __forceinline__ void wave_rows(const RowSpans& sp, int wave, int& rs,
     re = min(lim, rs + RPW);
 }
 
-template <int T, int kAhead, int RPW = kRowsPerWave>
+template <int T, int kAhead, int RPW = kRowsPerWave, int CPL = 8>
 __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict__ u, unsigned short* __restrict__ out,
                                                 int rows, int cols, int ld, int halo, int rs, int re, long long grow0,
                                                 long long grows, float k) {
-    static_assert(T >= 1 && T <= 8, "lanes 1..62 stay exact for at most 8 levels");
+    using G = Geo<CPL, T>;
+    constexpr int NP = G::NP;
+    using W = typename RawT<NP>::type;
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63;
-    const int c0 = strip_c0(lane);  // first column of this lane
+    const int c0 = G::c0(lane);  // first column of this lane
     if (rs >= re) return;
-    const bool in_grid = c0 + 8 <= cols;  // cols % 8 == 0
-    const bool store_lane = strip_store_lane(lane, c0, cols, in_grid);
-    const bool fix0 = c0 == 0, fix7 = c0 + 8 == cols;
+    const bool in_grid = c0 + CPL <= cols;  // cols % 8 == 0
+    const bool store_lane = G::store_lane(lane, cols, in_grid);
+    const bool fix0 = c0 == 0, fixl = c0 + CPL == cols;
     const int slab_rows = rows + 2 * halo;
     const unsigned short* base = u + (in_grid ? c0 : 0);
     auto fetch = [&](int r) __attribute__((always_inline)) {  // local row r, clamped into the slab
         const int sr = min(max(r + halo, 0), slab_rows - 1);
-        u32x4 w = *reinterpret_cast<const u32x4*>(base + (size_t)sr * ld);
-        if (!in_grid) w = u32x4{0u, 0u, 0u, 0u};
+        W w = *reinterpret_cast<const W*>(base + (size_t)sr * ld);
+        if (!in_grid) w = W{0u};
         return w;
     };
     // ring[t][slot]: level t (0 = u) row with (row index - first) % 3 == slot, as exact floats in pair layout
-    Row8 ring[T][3];
+    RowP<NP> ring[T][3];
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
 #pragma unroll
-            for (int p = 0; p < 4; ++p) ring[t][q].p[p] = f2{0.f, 0.f};
+            for (int p = 0; p < NP; ++p) ring[t][q].p[p] = f2{0.f, 0.f};
     const int i0 = rs - T, i1 = re + T;  // u rows consumed: [i0, i1)
-    u32x4 pre[kAhead];
+    W pre[kAhead];
 #pragma unroll
     for (int j = 0; j < kAhead; ++j) pre[j] = fetch(min(i0 + j, i1 - 1));
     for (int ib = i0; ib < i1; ib += kAhead) {
@@ -284,7 +306,7 @@ __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict
             const int i = ib + j;
             if (i < i1) {
                 const int m0 = j % 3, m1 = (j + 2) % 3, m2 = (j + 1) % 3;  // slots of rows i, i-1, i-2
-                ring[0][m0] = unpack_pairs(pre[j]);
+                ring[0][m0] = unpack_pairs<NP>(pre[j]);
                 pre[j] = fetch(min(i + kAhead, i1 - 1));
                 // level t+1 row i-t-1 from level t rows (i-t-2, i-t-1, i-t): slots (m2, m1, m0) of level t;
                 // it lands in slot m0 of level t+1 (its row index i-t-1 is "newest" for that level)
@@ -295,13 +317,13 @@ __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict
                     // every level lie outside the wave's trapezoid (level T: rows above rs; same results)
                     if (i - i0 <= 2 * t + 1) continue;
                     const long long g = grow0 + r;
-                    Row8 nx;
-                    const u32x4 pk = update_pairs(ring[t][m2], ring[t][m1], ring[t][m0], g == 0 || g == grows - 1,
-                                                  fix0, fix7, k, nx);
+                    RowP<NP> nx;
+                    const W pk = update_pairs<NP>(ring[t][m2], ring[t][m1], ring[t][m0], g == 0 || g == grows - 1,
+                                                  fix0, fixl, k, nx);
                     if (t + 1 < T) {
                         ring[t + 1 < T ? t + 1 : 0][m0] = nx;
                     } else if (r >= rs && store_lane) {
-                        __builtin_nontemporal_store(pk, reinterpret_cast<u32x4*>(out + (size_t)(r + halo) * ld + c0));
+                        __builtin_nontemporal_store(pk, reinterpret_cast<W*>(out + (size_t)(r + halo) * ld + c0));
                     }
                 }
             }
@@ -325,10 +347,10 @@ __global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned 
 //  * buffer loads/stores with a per-wave descriptor: the row offset is an SGPR soffset, a lane's column offset
 //    a constant voffset, and lanes outside the grid get an out-of-range voffset, so the hardware returns 0 /
 //    drops the store (no per-row address VALU, no select);
-//  * the two lane-edge neighbours enter as DPP-sourced scalar adds (w + e of pair 0 and pair 3 built directly
+//  * the two lane-edge neighbours enter as DPP-sourced scalar adds (w + e of pair 0 and pair NP-1 built directly
 //    in their packed registers: no DPP move + pair-forming moves + packed add);
 //  * an intermediate level is rounded to bf16 AS FLOATS with one v_cvt_pk_bf16_f32 per value (low half 0),
-//    instead of pack (4) + unpack (8); only the stored last level is packed;
+//    instead of pack + unpack; only the stored last level is packed;
 //  * no Dirichlet handling on the fast path: the few waves that hold column 0 / cols-1 or compute a level row on
 //    global row 0 / grows-1 (a block column at each side, a wave or two at the top and bottom of the grid) run
 //    the v1 pipeline instead (kept as a separate loop: one kernel, two code paths chosen per wave).
@@ -347,49 +369,68 @@ __device__ __forceinline__ float add_scalar(float a, float b) {
     return r;
 }
 
-template <bool kLast>
-__device__ __forceinline__ void level_pairs(const Row8& n, const Row8& c, const Row8& s, float k, Row8& nx, u32x4& pk) {
+template <bool kLast, int NP>
+__device__ __forceinline__ void level_pairs(const RowP<NP>& n, const RowP<NP>& c, const RowP<NP>& s, float k,
+                                            RowP<NP>& nx, typename RawT<NP>::type& pk) {
     const f2 kk = f2{k, k}, m4 = f2{-4.f, -4.f};
-    f2 we[4];
-    const float em1 = pcmx::wave_from_prev(c.p[3].y);  // e_{-1}: previous lane's e7
-    const float e8 = pcmx::wave_from_next(c.p[0].x);   // e_8: next lane's e0
-    we[0] = f2{add_scalar(em1, c.p[1].x), add_scalar(c.p[3].x, c.p[1].y)};  // (e_{-1} + e1, e3 + e5)
-    we[1] = c.p[0] + c.p[2];
-    we[2] = c.p[1] + c.p[3];
-    we[3] = f2{add_scalar(c.p[2].x, c.p[0].y), add_scalar(c.p[2].y, e8)};   // (e2 + e4, e6 + e8)
-    Row8 o;
+    f2 we[NP];
+    const float em1 = pcmx::wave_from_prev(c.p[NP - 1].y);  // e_{-1}: previous lane's last element
+    const float eL = pcmx::wave_from_next(c.p[0].x);        // e_{2NP}: next lane's first element
+    // pair 0: (e_{-1} + e_1, e_{NP-1} + e_{NP+1}); pair NP-1: (e_{NP-2} + e_NP, e_{2NP-2} + e_{2NP})
+    we[0] = f2{add_scalar(em1, c.p[1].x), add_scalar(c.p[NP - 1].x, c.p[1].y)};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 1; q < NP - 1; ++q) we[q] = c.p[q - 1] + c.p[q + 1];
+    we[NP - 1] = f2{add_scalar(c.p[NP - 2].x, c.p[0].y), add_scalar(c.p[NP - 2].y, eL)};
+    RowP<NP> o;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
         const f2 t3 = (n.p[q] + s.p[q]) + we[q];
         const f2 lap = __builtin_elementwise_fma(c.p[q], m4, t3);
         o.p[q] = c.p[q] + kk * lap;
     }
     if constexpr (kLast) {
-        pk = pack_pairs(o);
+        pk = pack_pairs<NP>(o);
     } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) nx.p[q] = f2{round_bf16(o.p[q].x), round_bf16(o.p[q].y)};
+        for (int q = 0; q < NP; ++q) nx.p[q] = f2{round_bf16(o.p[q].x), round_bf16(o.p[q].y)};
     }
 }
 
+template <int NP>
+__device__ __forceinline__ typename RawT<NP>::type buffer_load_row(__amdgpu_buffer_rsrc_t r, unsigned vo, int so) {
+    if constexpr (NP == 4)
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+    else
+        return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+}
+template <int NP>
+__device__ __forceinline__ void buffer_store_row(const typename RawT<NP>::type& w, __amdgpu_buffer_rsrc_t r, unsigned vo,
+                                                 int so) {
+    if constexpr (NP == 4)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pcmx::i32x4, w), r, vo, so, 2);
+    else
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, w), r, vo, so, 2);
+}
+
 // The row pipeline of one interior wave (no Dirichlet row or column in reach).
-template <int T, int kAhead>
+template <int T, int kAhead, int NP>
 __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, const __amdgpu_buffer_rsrc_t ro, unsigned vld,
                                             unsigned vst, int sr0, int pitch, int slab_rows, int halo, int rs, int i0,
                                             int i1, float k) {
+    using W = typename RawT<NP>::type;
     auto fetch = [&](int r) __attribute__((always_inline)) {  // local row r, clamped into the slab
         const int sr = min(max(r + halo, 0), slab_rows - 1);
-        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, vld, (sr - sr0) * pitch, 0));
+        return buffer_load_row<NP>(ru, vld, (sr - sr0) * pitch);
     };
     // ring[t][slot]: level t (0 = u) row with (row index - first) % 3 == slot, as exact floats in pair layout
-    Row8 ring[T][3];
+    RowP<NP> ring[T][3];
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
 #pragma unroll
-            for (int p = 0; p < 4; ++p) ring[t][q].p[p] = f2{0.f, 0.f};
-    u32x4 pre[kAhead];
+            for (int p = 0; p < NP; ++p) ring[t][q].p[p] = f2{0.f, 0.f};
+    W pre[kAhead];
 #pragma unroll
     for (int j = 0; j < kAhead; ++j) pre[j] = fetch(min(i0 + j, i1 - 1));
     for (int ib = i0; ib < i1; ib += kAhead) {
@@ -398,22 +439,21 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
             const int i = ib + j;
             if (i < i1) {
                 const int m0 = j % 3, m1 = (j + 2) % 3, m2 = (j + 1) % 3;  // slots of rows i, i-1, i-2
-                ring[0][m0] = unpack_pairs(pre[j]);
+                ring[0][m0] = unpack_pairs<NP>(pre[j]);
                 pre[j] = fetch(min(i + kAhead, i1 - 1));
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
                     const int r = i - t - 1;
                     if (t + 1 < T) {
                         if (i - i0 <= 2 * t + 1) continue;  // outside the wave's trapezoid (see stencil5xT_body)
-                        u32x4 unused;
-                        level_pairs<false>(ring[t][m2], ring[t][m1], ring[t][m0], k, ring[t + 1 < T ? t + 1 : 0][m0],
-                                           unused);
+                        W unused;
+                        level_pairs<false, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k,
+                                               ring[t + 1 < T ? t + 1 : 0][m0], unused);
                     } else if (r >= rs) {
-                        u32x4 pk;
-                        Row8 unused;
-                        level_pairs<true>(ring[t][m2], ring[t][m1], ring[t][m0], k, unused, pk);
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pcmx::i32x4, pk), ro, vst,
-                                                               (r + halo - sr0) * pitch, 2);
+                        W pk;
+                        RowP<NP> unused;
+                        level_pairs<true, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k, unused, pk);
+                        buffer_store_row<NP>(pk, ro, vst, (r + halo - sr0) * pitch);
                     }
                 }
             }
@@ -424,22 +464,22 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
 // MINW: minimum waves per SIMD the register allocation must allow (__launch_bounds__'s second argument): a short
 // slab has few waves, so fitting one more per SIMD (T=4: 138 -> <= 128 VGPRs, 3 -> 4 waves) can matter more than
 // the few rematerialised values it costs.
-template <int T, int kAhead, int RPW = kRowsPerWave, int MINW = 1>
+template <int T, int kAhead, int RPW = kRowsPerWave, int MINW = 1, int CPL = 8>
 __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
                                                                   unsigned short* __restrict__ out, int rows, int cols,
                                                                   int ld, int halo, RowSpans sp, long long grow0,
                                                                   long long grows, float k) {
-    static_assert(T >= 1 && T <= 8, "lanes 1..62 stay exact for at most 8 levels");
+    using G = Geo<CPL, T>;
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int c0 = strip_c0(lane);  // first column of this lane
+    const int c0 = G::c0(lane);  // first column of this lane
     int rs, re;
     wave_rows<RPW>(sp, wave, rs, re);
     if (rs >= re) return;
-    const bool in_grid = c0 + 8 <= cols;  // cols % 8 == 0
-    const bool store_lane = strip_store_lane(lane, c0, cols, in_grid);
-    const bool fix0 = c0 == 0, fix7 = c0 + 8 == cols;
+    const bool in_grid = c0 + CPL <= cols;  // cols % 8 == 0
+    const bool store_lane = G::store_lane(lane, cols, in_grid);
+    const bool fix0 = c0 == 0, fixl = c0 + CPL == cols;
     const int slab_rows = rows + 2 * halo;
     const int i0 = rs - T, i1 = re + T;  // u rows consumed: [i0, i1); level rows computed: [i0 - T, i1 - 1)
     // the wave's slab rows [sr0, sr1) (clamped like the fetch); one descriptor per buffer over exactly them
@@ -453,11 +493,11 @@ __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const un
     const unsigned vst = store_lane ? (unsigned)c0 * 2 : 0x80000000u;  // out of range: the store is dropped
     const long long g0 = grow0 + i0 - T, g1 = grow0 + i1 - 2;          // global rows of computed level rows
     const bool edge_rows = (g0 <= 0 && 0 <= g1) || (g0 <= grows - 1 && grows - 1 <= g1);
-    const bool slow = edge_rows || __builtin_amdgcn_ballot_w64(fix0 || fix7) != 0;
+    const bool slow = edge_rows || __builtin_amdgcn_ballot_w64(fix0 || fixl) != 0;
     if (slow)  // a few waves per grid: the v1 pipeline (per-column selects, per-row Dirichlet test; same results)
-        stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
+        stencil5xT_body<T, kAhead, RPW, CPL>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
     else
-        pipeline_v2<T, kAhead>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
+        pipeline_v2<T, kAhead, G::NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
 }
 #pragma clang fp contract(on)
 }  // namespace
@@ -477,12 +517,14 @@ extern "C" int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, 
 }
 
 namespace {
-// strips covering `cols` columns (see strip_c0): strip x ends at x*496 + 504, or at x*496 + 512 == cols
-int strips_for(int cols) {
-    int n = 1;
-    while ((n - 1) * kOutCols + 504 < cols && (n - 1) * kOutCols + 512 != cols) ++n;
-    return n;
+// strips covering `cols` columns (see Geo): the first strip whose loaded range [x*OUT, x*OUT + 64*CPL) reaches cols
+// is the last one
+int strips_for(int cols, int cpl, int steps) {
+    const int L = (steps + cpl - 1) / cpl, out = (64 - 2 * L) * cpl;
+    return cols <= 64 * cpl ? 1 : 1 + (cols - 64 * cpl + out - 1) / out;
 }
+// lab override of the launch shape (0 = production rule): columns per lane, rows per wave
+int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0;
 // the halo rule of one row range: rows within `steps` of a non-global slab edge read `steps` halo rows
 bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row0, long long global_rows) {
     const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
@@ -522,46 +564,81 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
     // one round) runs 3.9-4.0k against 3.6-3.9k for 24 rows / 6-row ring (138 VGPRs, 3 waves per SIMD); the waves
     // are VALU-busy only ~20% of the time, split between load waits and the level-to-level dependency chain.
     const int span_rows = (r1a - r0a) + (r1b - r0b);
-    const int rpw = span_rows < 3072 ? (steps <= 4 ? 18 : 16) : span_rows < 6144 ? 24 : span_rows < 12288 ? 32
-                    : (steps <= 4 ? 24 : 64);
-    auto launch_dims = [&](int rpw_, RowSpans& sp) {
+    // Lanes and rows per wave (round 3, scripts/stencil_lanes_lab.py, profiles/r3_stencil/lanes_*.txt): 4 columns per
+    // lane (twice the waves, half the registers) pays at T >= 6 below 12288 rows; an EDGE launch (the two halo
+    // bands of a distributed step, <= 2T rows) is a few waves whose row pipeline is the whole cost, so it runs
+    // 2-row waves of 4 columns per lane (shorter dependency chains, 8-16x the waves).
+    const bool edge = span_rows <= 64;
+    int cpl, rpw;
+    if (edge)
+        cpl = 4, rpw = 2;
+    else if (span_rows < 3072)
+        cpl = steps >= 6 ? 4 : 8, rpw = steps == 6 ? 18 : 24;
+    else if (span_rows < 6144)
+        cpl = steps >= 6 ? 4 : 8, rpw = steps == 8 ? 32 : 24;
+    else if (span_rows < 12288)
+        cpl = steps == 8 ? 4 : 8, rpw = 32;
+    else
+        cpl = 8, rpw = steps <= 4 ? 24 : 64;
+    if (edge ? g_lab_edge_cpl : g_lab_cpl) cpl = edge ? g_lab_edge_cpl : g_lab_cpl;
+    if (edge ? g_lab_edge_rpw : g_lab_rpw) rpw = edge ? g_lab_edge_rpw : g_lab_rpw;
+    auto launch_dims = [&](int rpw_, int cpl_, RowSpans& sp) {
         const int per = kWaves * rpw_;
         sp = RowSpans{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per};
-        return dim3(strips_for(cols), sp.nby_a + (r1b - r0b + per - 1) / per);
+        return dim3(strips_for(cols, cpl_, steps), sp.nby_a + (r1b - r0b + per - 1) / per);
     };
     RowSpans sp;
-#define PCMX_STENCIL_V2_RPW(T, R)                                                                                   \
+#define PCMX_STENCIL_V2_RPW(T, R, C)                                                                                \
     case R: {                                                                                                       \
-        const dim3 g = launch_dims(R, sp);                                                                          \
-        stencil5xT2_kernel<T, (T >= 6 && R >= 64 ? 9 : R == 18 ? 3 : 6), R><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, \
-                                                                                       halo, sp,                    \
-                                                                                       global_row0, global_rows, k); \
+        const dim3 g = launch_dims(R, C, sp);                                                                       \
+        stencil5xT2_kernel<T, (T >= 6 && R >= 64 ? 9 : R == 18 || R <= 4 ? 3 : 6), R, 1, C><<<g, kWaves * 64, 0, s>>>( \
+            ui, uo, rows, cols, ld, halo, sp, global_row0, global_rows, k);                                         \
         break;                                                                                                      \
     }
-#define PCMX_STENCIL_V2(T)                                                                                          \
+#define PCMX_STENCIL_V2C(T, C)                                                                                      \
     switch (rpw) {                                                                                                  \
-        PCMX_STENCIL_V2_RPW(T, 16)                                                                                  \
-        PCMX_STENCIL_V2_RPW(T, 18)                                                                                  \
-        PCMX_STENCIL_V2_RPW(T, 24)                                                                                  \
-        PCMX_STENCIL_V2_RPW(T, 32)                                                                                  \
-        PCMX_STENCIL_V2_RPW(T, 64)                                                                                  \
+        PCMX_STENCIL_V2_RPW(T, 2, C)                                                                                \
+        PCMX_STENCIL_V2_RPW(T, 4, C)                                                                                \
+        PCMX_STENCIL_V2_RPW(T, 16, C)                                                                               \
+        PCMX_STENCIL_V2_RPW(T, 18, C)                                                                               \
+        PCMX_STENCIL_V2_RPW(T, 24, C)                                                                               \
+        PCMX_STENCIL_V2_RPW(T, 32, C)                                                                               \
+        PCMX_STENCIL_V2_RPW(T, 64, C)                                                                               \
         default: return -1;                                                                                         \
+    }
+#define PCMX_STENCIL_V2(T)                                                                                          \
+    if (cpl == 4) {                                                                                                 \
+        PCMX_STENCIL_V2C(T, 4)                                                                                      \
+    } else {                                                                                                        \
+        PCMX_STENCIL_V2C(T, 8)                                                                                      \
     }
     switch (steps) {
         case 2: {
-            const dim3 g = launch_dims(kRowsPerWave, sp);
+            const dim3 g = launch_dims(kRowsPerWave, 8, sp);
             stencil5xT_kernel<2, 6><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0, global_rows, k);
             break;
         }
-        case 3: PCMX_STENCIL_V2(3) break;
+        case 3: PCMX_STENCIL_V2C(3, 8) break;
         case 4: PCMX_STENCIL_V2(4) break;
         case 6: PCMX_STENCIL_V2(6) break;
         case 8: PCMX_STENCIL_V2(8) break;
         default: return -1;
     }
 #undef PCMX_STENCIL_V2
+#undef PCMX_STENCIL_V2C
 #undef PCMX_STENCIL_V2_RPW
     return (int)hipGetLastError();
+}
+
+// Lab knob (scripts/stencil_lanes_lab.py): force columns per lane (4 / 8) and rows per wave (2 / 4 / 16 / 18 / 24 /
+// 32 / 64) of the fused v2 launches over more than 64 rows (which = 0) or of edge launches (which = 1); 0 restores
+// the production rule. Host-global, not thread-safe: labs only.
+extern "C" int pcmx_stencil_lab_set(int which, int cpl, int rpw) {
+    const bool rpw_ok = rpw == 0 || rpw == 2 || rpw == 4 || rpw == 16 || rpw == 18 || rpw == 24 || rpw == 32 || rpw == 64;
+    if ((cpl != 0 && cpl != 4 && cpl != 8) || !rpw_ok || (which != 0 && which != 1)) return -1;
+    (which ? g_lab_edge_cpl : g_lab_cpl) = cpl;
+    (which ? g_lab_edge_rpw : g_lab_rpw) = rpw;
+    return 0;
 }
 
 // T fused updates over local rows [r0, r1) of a slab with `halo` rows above and below (T = 2, 3, 4, 6, 8).

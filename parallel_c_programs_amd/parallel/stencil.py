@@ -28,10 +28,12 @@ from .topology import split
 
 def auto_fuse(slab_rows: int) -> int:
     """Fused updates per kernel for a rank's slab height: the fused kernel is VALU-bound and every wave recomputes
-    its T-row trapezoid overlap, so deep fusion pays on tall slabs and short slabs want shallow fusion
-    (scripts/stencil_lab.hip, profiles/r2_stencil/rpw_sweep_trapezoid.txt, 16384 columns, best GLUP/s: 16384 rows
-    T=8 5.5k / T=6 5.4k; 8192 T=6 5.1k; 4096 T=6 4.5k; 2048 T=4 3.9k / T=6 3.6k)."""
-    return 8 if slab_rows >= 12288 else 6 if slab_rows >= 4096 else 4
+    its T-row trapezoid overlap, so deep fusion pays on tall slabs and short slabs want shallower fusion. Measured as
+    the distributed step shape (interior launch + the two-span edge launch, 16384 columns, round-3 lane geometries:
+    4 columns per lane at T >= 6 below 12288 rows, 2-row edge waves; scripts/stencil_lanes_lab.py,
+    profiles/r3_stencil/lanes_*.txt), GLUP/s: 16384 rows T=8 5.5k; 8192 T=8 4.9k / T=6 4.8k; 4096 T=6 4.4k / T=8 4.2k
+    / T=4 3.9k; 2048 T=6 3.4k / T=8 3.3k / T=4 3.3k."""
+    return 8 if slab_rows >= 6144 else 6
 
 
 class StencilSlab:

@@ -221,9 +221,10 @@ def test_stencil_row_range_split(gpu):
                                    (12400, 600)])
 def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
     """Temporal-blocking kernel == `steps` single steps (bf16 bits); random data so every lane/strip-overlap
-    path counts; column counts that are not multiples of the 496-column output strip; the row counts cover every
-    rows-per-wave launch (16/24 under 3072 rows, 24 under 6144, 32 under 12288, 64 (T >= 6) / 24 above; interior
-    waves: v2 fast path with the trapezoid skip, edge waves: v1 pipeline)."""
+    path counts; column counts that are not multiples of the 496 / 248 / 240-column output strips; the row counts
+    cover every production launch shape (edge launches of <= 64 rows: 4 columns per lane, 2-row waves; under 3072
+    rows 8 columns x 24 rows at T <= 4, 4 columns x 18 / 24 at T = 6 / 8; under 6144 and 12288 the 24 / 32-row
+    shapes; 64 (T >= 6) / 24 above; interior waves: v2 fast path with the trapezoid skip, edge waves: v1 pipeline)."""
     rows, cols = shape
     g = torch.Generator().manual_seed(rows + steps)
     u = (torch.rand(rows + 2, cols, generator=g) * 4 - 2).to(torch.bfloat16)
@@ -234,6 +235,34 @@ def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
     b = a.clone()
     ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps)
     assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16))
+
+
+@pytest.mark.parametrize("steps", [3, 4, 6, 8])
+@pytest.mark.parametrize("shape", [(515, 1000), (70, 2056), (200, 264)])
+def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
+    """Every launch shape the stencil lab knob can force (4 or 8 columns per lane x 2..64 rows per wave, for full
+    and edge launches) gives the bits of `steps` single steps: ragged column counts (stale-lane rule of 4-column lanes
+    at T = 8: two stale lanes per strip side), Dirichlet rows and columns, strips ending inside a lane range."""
+    import ctypes  # noqa: F401
+    from parallel_c_programs_amd._native import hip_lib
+
+    rows, cols = shape
+    g = torch.Generator().manual_seed(rows + cols + steps)
+    u = (torch.rand(rows + 2, cols, generator=g) * 4 - 2).to(torch.bfloat16)
+    ref = u
+    for _ in range(steps):
+        ref = ops.stencil5_reference(ref, 0, rows)
+    a = u.to(gpu)
+    lib = hip_lib()
+    try:
+        for cpl in (4, 8):
+            for rpw in (2, 4, 16, 18, 24, 32, 64):
+                assert lib.pcmx_stencil_lab_set(0, cpl, rpw) == 0 and lib.pcmx_stencil_lab_set(1, cpl, rpw) == 0
+                b = torch.zeros_like(a)
+                ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps)
+                assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16)), (cpl, rpw)
+    finally:
+        lib.pcmx_stencil_lab_set(0, 0, 0), lib.pcmx_stencil_lab_set(1, 0, 0)
 
 
 @pytest.mark.parametrize("steps", [2, 4, 6])
