@@ -198,6 +198,17 @@ def test_sgemm_x6_elementwise_fp32_accuracy(gpu, shape):
     assert err < 4e-6 * max(1.0, (k / 256) ** 0.5), err
 
 
+def test_sgemm_x6_alpha_beta(gpu):
+    """Variant 20 through the alpha/beta epilogue (C read back, scaled, added) on a 4x2-tile problem."""
+    g = torch.Generator(device=gpu).manual_seed(20)
+    a = torch.rand(1024, 320, device=gpu, generator=g) * 2 - 1
+    b = torch.rand(320, 512, device=gpu, generator=g) * 2 - 1
+    c0 = torch.rand(1024, 512, device=gpu, generator=g)
+    ref = 1.5 * (a.double() @ b.double()) - 0.25 * c0.double()
+    out = ops.sgemm_out(a, b, c0.clone(), alpha=1.5, beta=-0.25, variant=20)
+    assert ((out.double() - ref).abs().max() / ref.abs().max()).item() < 1e-6
+
+
 def test_sgemm_x6_split_exact_wide_range(gpu):
     """The split is exact for |x| >= 2^-110: operands spanning 2^-40 .. 2^40 (one row / column each) multiply to
     the fp64 result within fp32 rounding, and an identity A reproduces B bit for bit."""
