@@ -220,7 +220,8 @@ def test_sgemm_x6_split_exact_wide_range(gpu):
     c = ops.sgemm(a, b, variant=20)
     ref = a.double() @ b.double()
     assert ((c.double() - ref).abs() / ref.abs().clamp_min(1e-300)).max().item() < 2.5e-7
-    p2 = torch.pow(2.0, torch.randint(-40, 41, (n,), device=gpu).float())
+    # exact powers of two (torch.pow(2., x) on the GPU is an exp2 approximation: 2^29 -> 536870880)
+    p2 = torch.tensor([2.0 ** e for e in torch.randint(-40, 41, (n,)).tolist()], device=gpu)
     exact = torch.eye(n, device=gpu) * p2[:, None]
     assert torch.equal(ops.sgemm(exact, b, variant=20), p2[:, None] * b)
     assert torch.equal(ops.sgemm(torch.eye(n, device=gpu), b, variant=20), b)
