@@ -54,19 +54,26 @@ __device__ __forceinline__ float hi16(unsigned w) { return __uint_as_float(w & 0
 // Split of 8 elements (k order) into three bf16x8 planes, x == p0 + p1 + p2: per pair of elements 3
 // v_cvt_pk_bf16_f32, 2 unpacks and 2 residual subtractions for each of 2 levels (f32x2 arithmetic; the compiler
 // unpacks v_pk_add_f32 in the MFMA shadow). A tile: r[q] holds k = 4q .. 4q+3; words d = 2q, 2q+1 of each level come from r[q].
+// FAKE (lab only, wrong results): one conversion per pair and no residuals, to price the split's VALU work.
+template <bool FAKE = false>
 __device__ __forceinline__ void split_a4(f32x4 (&r)[2], Planes& o) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         f32x2 x0 = {r[q][0], r[q][1]}, x1 = {r[q][2], r[q][3]};
 #pragma unroll
         for (int l = 0; l < 3; ++l) {
+            if (FAKE && l > 0) {
+                o.p[l][2 * q] = o.p[0][2 * q], o.p[l][2 * q + 1] = o.p[0][2 * q + 1];
+                continue;
+            }
             const unsigned w0 = cvt2(x0[0], x0[1]), w1 = cvt2(x1[0], x1[1]);
             o.p[l][2 * q] = w0, o.p[l][2 * q + 1] = w1;
-            if (l < 2) x0 -= f32x2{lo16(w0), hi16(w0)}, x1 -= f32x2{lo16(w1), hi16(w1)};
+            if (!FAKE && l < 2) x0 -= f32x2{lo16(w0), hi16(w0)}, x1 -= f32x2{lo16(w1), hi16(w1)};
         }
     }
 }
 // B: word d (k rows 2d, 2d+1) of every level for all 4 N-tiles; r[e] holds k row e of the 4 N-tiles' columns.
+template <bool FAKE = false>
 __device__ __forceinline__ void split_b_word(const f32x4 (&r)[8], int d, Planes (&o)[4]) {
     f32x2 x[2][2];  // [row 2d / 2d+1][N-tile pair]
 #pragma unroll
@@ -76,9 +83,14 @@ __device__ __forceinline__ void split_b_word(const f32x4 (&r)[8], int d, Planes 
 #pragma unroll
     for (int l = 0; l < 3; ++l) {
         unsigned w[4];
+        if (FAKE && l > 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j].p[l][d] = o[j].p[0][d];
+            continue;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j].p[l][d] = w[j] = cvt2(x[0][j >> 1][j & 1], x[1][j >> 1][j & 1]);
-        if (l < 2) {
+        if (!FAKE && l < 2) {
 #pragma unroll
             for (int jp = 0; jp < 2; ++jp) {
                 x[0][jp] -= f32x2{lo16(w[2 * jp]), lo16(w[2 * jp + 1])};
@@ -175,19 +187,19 @@ __global__ __launch_bounds__(256, 1) void sgemm_x6_kernel(const float* __restric
             __builtin_amdgcn_sched_barrier(0);  // one scheduling region per M-tile: loads stay in issue order
             const Planes& cur = pa[i & 1];
             const int in = (i + 1) & 3;  // next A tile: i+1 of this step, or tile 0 of step s+1
-            split_a4(ra[in], pa[in & 1]);
+            split_a4<(VPM >= 10)>(ra[in], pa[in & 1]);
             load_a(ra[in], in, i < 3 ? s + 1 : s + 2);
-            split_b_word(rb[P ^ 1], i, pb[P ^ 1]);  // word i of every N-tile's planes for step s+1
+            split_b_word<(VPM >= 10)>(rb[P ^ 1], i, pb[P ^ 1]);  // word i of every N-tile's planes for step s+1
             if (i == 3) load_b(rb[P ^ 1], s + 3);
 #pragma unroll
             for (int p = 0; p < 6; ++p)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[i][j] = mfma(cur.p[kPA[p]], pb[P][j].p[kPB[p]], acc[i][j]);
-            if constexpr (VPM > 0) {
+            if constexpr (VPM % 10 > 0) {
 #pragma unroll
                 for (int m = 0; m < 24; ++m) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // 1 MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);  // VPM VALU
+                    __builtin_amdgcn_sched_group_barrier(0x002, VPM % 10, 0);  // VPM VALU
                 }
             }
         }
@@ -240,6 +252,7 @@ extern "C" int pcmx_sgemm_f32_x6_variant(const float* A, const float* B, float* 
             case 2: PCMX_X6(2); break;
             case 4: PCMX_X6(4); break;
             case 5: PCMX_X6(0); break;
+            case 13: PCMX_X6(13); break;  // lab: split VALU priced out (wrong results)
             default: PCMX_X6(3); break;
         }
 #undef PCMX_X6
