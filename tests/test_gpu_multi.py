@@ -37,6 +37,7 @@ def _check_line(out, n):
         assert out[k] > 0, k
     assert out["stencil_bit_exact"] and out["stencil_finite"]
     assert out["sgemm_max_rel_err_vs_fp64"] < 1e-5 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
+    assert out["sgemm_fp32_via_bf16x6_tflops"] > 0 and out["sgemm_fp32_via_bf16x6_max_rel_err_vs_fp64"] < 1e-5
     assert out["reduce_strong_rel_err_vs_fp64"] < 1e-5 and out["scan_strong_rel_err_vs_fp64"] < 1e-5
     assert not [k for k in out if k.endswith("_error")], out
 
