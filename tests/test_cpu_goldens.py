@@ -171,3 +171,16 @@ def test_reference_host_entry_points_t2():
     assert int(vol[300, 300, 50]) == 35  # the seed voxel sits in the value-35 box (ref raycast.cu:140-143)
     lib.pcmx_free(ctypes.cast(data, ctypes.c_void_p))
     lib.pcmx_free(ctypes.cast(region, ctypes.c_void_p))
+
+
+def test_sgemm_cli_host_backend():
+    """run_sgemm without a GPU: the host C GEMM backend, reference Time line + JSON line with its fp64 error."""
+    import json
+
+    from conftest import run_cli
+
+    out = run_cli("run_sgemm", 96, "--m", 40, "--steps", 1, "--warmup", 0, "--device", "cpu").stdout.splitlines()
+    assert out[0].startswith("Time : ")
+    line = json.loads(out[1])
+    assert (line["m"], line["n"], line["k"], line["device"]) == (40, 96, 96, "cpu")
+    assert line["max_rel_err_vs_fp64"] < 1e-5

@@ -40,6 +40,20 @@ def test_histogram_cli(gpu, tmp_path, method):
     assert np.array_equal(out, ref.numpy())
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6"])
+def test_sgemm_cli(gpu, precision):
+    """run_sgemm: the reference's Time line + one JSON line, odd shape padded by ops.sgemm, hipBLASLt comparison."""
+    import json
+
+    out = run_cli("run_sgemm", 1000, "--k", 700, "--precision", precision, "--steps", 2, "--warmup", 1,
+                  "--compare").stdout.splitlines()
+    assert out[0].startswith("Time : ") and out[0].endswith(" s")
+    line = json.loads(out[1])
+    assert line["precision"] == precision and line["kernel"] == f"variant {17 if precision == 'fp32' else 20}"
+    assert line["max_rel_err_vs_fp64"] < 1e-5 and line["hipblaslt_max_rel_err_vs_fp64"] < 1e-5
+    assert line["tflops"] > 0 and line["speedup_vs_hipblaslt"] > 0
+
+
 def test_vmul_cli_table(gpu):
     lines = run_cli("run_vmul").stdout.splitlines()
     i = lines.index("Host\tDevice")
