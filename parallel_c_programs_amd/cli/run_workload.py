@@ -5,12 +5,13 @@ whole-job throughput (sum over ranks), the max-over-ranks step time and the work
 from __future__ import annotations
 
 import argparse
-import json
 import sys
 
 from ..models import WORKLOADS, build_workload
 from ..parallel import finalize, init
 from ..utils.harness import timed
+from ..utils.metrics import emit_metric
+from ..utils.timing import print_time
 
 
 def _val(s: str):
@@ -22,16 +23,25 @@ def _val(s: str):
     return {"true": True, "false": False}.get(s.lower(), s)
 
 
-def run(name: str, argv=None, defaults: dict | None = None) -> dict | None:
-    ap = argparse.ArgumentParser(prog=f"run_{name}")
+def run(name: str, argv=None, defaults: dict | None = None, add_args=None, to_cfg=None, prog: str | None = None,
+        doc: str | None = None, time_line: bool = False) -> dict | None:
+    """Builds workload `name` from defaults <- to_cfg(parsed CLI args) <- --set key=value, times it like bench.py
+    (warm-up, then `steps` steps between barrier + device syncs, max over ranks) and prints one JSON line on rank 0
+    (preceded by the reference's "Time : %f s" per step when time_line)."""
+    ap = argparse.ArgumentParser(prog=prog or f"run_{name}", description=doc,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    if add_args:
+        add_args(ap)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--backend", default=None)
-    ap.add_argument("--device", default=None)
-    ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="workload config")
+    ap.add_argument("--backend", default=None, help="nccl (RCCL, default on a GPU) or gloo")
+    ap.add_argument("--device", default=None, help="cuda (default with a GPU) or cpu")
+    ap.add_argument("--no-check", action="store_true", help="skip the workload's numerics check")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="any workload config key")
     a = ap.parse_args(argv)
     cfg = dict(defaults or {})
+    if to_cfg:
+        cfg.update({k: v for k, v in to_cfg(a).items() if v is not None})
     cfg.update({k: _val(v) for k, v in (s.split("=", 1) for s in a.set)})
     ctx = init(a.backend, a.device)
     try:
@@ -43,7 +53,9 @@ def run(name: str, argv=None, defaults: dict | None = None) -> dict | None:
                "warmup": a.warmup, "config": w.cfg, **{k: (round(v, 4) if isinstance(v, float) else v)
                                                        for k, v in rep.items()}, **chk}
         if ctx.is_root:
-            print(json.dumps(out), flush=True)
+            if time_line:
+                print_time(rep["ms_per_step"] / 1e3)
+            emit_metric(**out)
         return out
     finally:
         finalize(ctx)

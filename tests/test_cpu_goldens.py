@@ -184,3 +184,26 @@ def test_sgemm_cli_host_backend():
     line = json.loads(out[1])
     assert (line["m"], line["n"], line["k"], line["device"]) == (40, 96, 96, "cpu")
     assert line["max_rel_err_vs_fp64"] < 1e-5
+
+
+@pytest.mark.parametrize("module,args,workloads", [
+    ("run_stencil", (128, "--fuse", 2), ["stencil"]),
+    ("run_reduce_scan", ("1e5", "--op", "both"), ["reduce", "scan"]),
+    ("run_reduce_scan", ("1e5", "--op", "scan"), ["scan"]),
+    ("run_spmv_dist", ("2e4", "2e5", "--chunks", 1), ["spmv"]),
+])
+def test_north_star_clis_on_host(module, args, workloads):
+    """The north-star CLIs' own arguments map onto the workloads (reference Time line + one JSON line per workload,
+    every numerics check passing) on the host path."""
+    import json
+
+    from conftest import run_cli
+
+    out = run_cli(module, *args, "--steps", 1, "--warmup", 0, "--device", "cpu").stdout.splitlines()
+    lines = [json.loads(s) for s in out if s.startswith("{")]
+    assert [ln["workload"] for ln in lines] == workloads
+    assert sum(s.startswith("Time : ") for s in out) == len(workloads)
+    for ln in lines:
+        errs = {k: v for k, v in ln.items() if "err" in k}
+        assert all(v < 1e-5 for v in errs.values()), ln
+        assert all(v for k, v in ln.items() if "bit_exact" in k), ln
