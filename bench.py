@@ -146,11 +146,16 @@ def main(argv=None):
             out["hipblaslt_torch_matmul_tflops"] = _r(world * g.work_per_step() * K / t_ref / 1e12, 3)
         if not args.no_x6 and dev.type == "cuda" and n % 256 == 0:
             # fp32 GEMM on the bf16 matrix cores (exact 3-way operand split, 6 piece products; sgemm_x6.hip): an
-            # fp32-accurate extra, timed identically with its own fp64 check; never the headline value
-            g.variant = 20
-            t_x6 = timed(ctx, g.step, K, Wm)
-            out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * g.work_per_step() * K / t_x6 / 1e12, 3)
-            out["sgemm_fp32_via_bf16x6_max_rel_err_vs_fp64"] = ctx.max_over_ranks(g.check()["max_rel_err_vs_fp64"])
+            # fp32-accurate extra, timed identically with its own fp64 check; never the headline value. A failure
+            # here costs only these fields (the headline above is already measured)
+            try:
+                g.variant = 20
+                t_x6 = timed(ctx, g.step, K, Wm)
+                out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * g.work_per_step() * K / t_x6 / 1e12, 3)
+                out["sgemm_fp32_via_bf16x6_max_rel_err_vs_fp64"] = ctx.max_over_ranks(
+                    g.check()["max_rel_err_vs_fp64"])
+            except Exception as e:  # noqa: BLE001 - reported in the JSON line
+                out["sgemm_fp32_via_bf16x6_error"] = f"{type(e).__name__}: {e}"[:300]
         del g
         free()
         log(f"sgemm {tflops:.1f} TFLOPS")
