@@ -7,6 +7,7 @@
 #include "pcmx_common.h"
 #include "pcmx_cpu.h"
 #include "pcmx_hip.h"
+#include <string.h>
 
 extern "C" int pcmx_device_count(void) {
     int n = 0;
@@ -51,10 +52,14 @@ static int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 extern "C" int pcmx_sgemm_host_arrays(const float* a, const float* b, float* c, int m, int n, int k) {
     if (pcmx_device_count() == 0) return (int)hipErrorNoDevice;
-    // the padding of the kernel pcmx_sgemm_f32 will pick: 256x256 tiles and K % 64 (direct-register variant 17)
-    // when the problem fills the chip with 256-tiles, else 128x128 tiles
-    const bool big = (long long)((m + 255) / 256) * ((n + 255) / 256) >= 192;
-    const int mp = round_up(m, big ? 256 : 128), np = round_up(n, big ? 256 : 128), kp = round_up(k, big ? 64 : 32);
+    // PCMX_SGEMM_PRECISION=bf16x6: the fp32-accurate GEMM on the bf16 matrix cores (sgemm_x6.hip, 256x256 tiles,
+    // K % 32); otherwise the padding of the kernel pcmx_sgemm_f32 will pick: 256x256 tiles and K % 64
+    // (direct-register variant 17) when the problem fills the chip with 256-tiles, else 128x128 tiles
+    const char* prec = getenv("PCMX_SGEMM_PRECISION");
+    const bool x6 = prec && strcmp(prec, "bf16x6") == 0;
+    const bool big = x6 || (long long)((m + 255) / 256) * ((n + 255) / 256) >= 192;
+    const int mp = round_up(m, big ? 256 : 128), np = round_up(n, big ? 256 : 128),
+              kp = round_up(k, big && !x6 ? 64 : 32);
     float *da = nullptr, *db = nullptr, *dc = nullptr;
     int rc = 0;
     if (hipMalloc(&da, sizeof(float) * (size_t)mp * kp) != hipSuccess || hipMalloc(&db, sizeof(float) * (size_t)kp * np) != hipSuccess ||
@@ -66,7 +71,8 @@ extern "C" int pcmx_sgemm_host_arrays(const float* a, const float* b, float* c, 
     PCMX_HIP_CHECK(hipMemset(db, 0, sizeof(float) * (size_t)kp * np));
     PCMX_HIP_CHECK(hipMemcpy2D(da, sizeof(float) * kp, a, sizeof(float) * k, sizeof(float) * k, m, hipMemcpyHostToDevice));
     PCMX_HIP_CHECK(hipMemcpy2D(db, sizeof(float) * np, b, sizeof(float) * n, sizeof(float) * n, k, hipMemcpyHostToDevice));
-    rc = pcmx_sgemm_f32(da, db, dc, mp, np, kp, kp, np, np, 1.0f, 0.0f, 0);
+    rc = x6 ? pcmx_sgemm_f32_x6(da, db, dc, mp, np, kp, kp, np, np, 1.0f, 0.0f, 0)
+            : pcmx_sgemm_f32(da, db, dc, mp, np, kp, kp, np, np, 1.0f, 0.0f, 0);
     if (rc == 0) {
         PCMX_HIP_CHECK(hipMemcpy2D(c, sizeof(float) * n, dc, sizeof(float) * np, sizeof(float) * n, m, hipMemcpyDeviceToHost));
     }

@@ -169,12 +169,20 @@ def test_matrix_multiply_dispatches_to_mfma_backend(gpu):
     a, b = lib.new_matrix(300, 200), lib.new_matrix(200, 260)
     ctypes.memmove(a.contents.data[0], a_np.ctypes.data, a_np.nbytes)
     ctypes.memmove(b.contents.data[0], b_np.ctypes.data, b_np.nbytes)
-    c = ctypes.POINTER(Mat)()
-    assert lib.matrix_multiply(a, b, ctypes.byref(c)) == 0
-    out = np.ctypeslib.as_array(c.contents.data[0], shape=(300 * 260,)).reshape(300, 260).copy()
     ref = a_np.astype(np.float64) @ b_np.astype(np.float64)
-    assert np.abs(out - ref).max() / np.abs(ref).max() < 1e-5
-    for m in (a, b, c):
+    import os
+
+    for prec in ("", "bf16x6"):  # the f32-MFMA kernel, then the fp32-accurate bf16 path (PCMX_SGEMM_PRECISION)
+        os.environ["PCMX_SGEMM_PRECISION"] = prec
+        try:
+            c = ctypes.POINTER(Mat)()
+            assert lib.matrix_multiply(a, b, ctypes.byref(c)) == 0
+        finally:
+            os.environ.pop("PCMX_SGEMM_PRECISION", None)
+        out = np.ctypeslib.as_array(c.contents.data[0], shape=(300 * 260,)).reshape(300, 260).copy()
+        assert np.abs(out - ref).max() / np.abs(ref).max() < 1e-5, prec
+        lib.free_matrix(c)
+    for m in (a, b):
         lib.free_matrix(m)
 
 
