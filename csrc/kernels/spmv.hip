@@ -18,8 +18,8 @@
 // slice (b % 8) + 8 * phase and all of a slice's gathers stay inside ONE L2. Each slice writes a COMPACT
 // partial y: one value per row the slice touches (36% of the S x n_rows pairs on the 1e8-nnz power-law graph;
 // the dense S x n_rows partials cost 640 MB of writes + 640 MB of combine reads per product). A combine pass
-// sums every row's partials (per-row slice mask + per-64-row-chunk base offsets, ranks from wave ballots), a
-// fix-up adds the later pieces of split long rows.
+// sums every row's partials (per-row slice mask + per-64-row-chunk base offsets, each lane's rank among the
+// lanes touching a slice from one byte-packed DPP wave scan), a fix-up adds the later pieces of split long rows.
 //
 // Banded (implicit column indices): one wave per row; the 5 bands are contiguous slices of x and of the
 // value array, so all loads are unit-stride and no column index is ever read.
@@ -373,6 +373,72 @@ __global__ __launch_bounds__(256) void spmv_combine_kernel(const float* __restri
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < S; ++k) acc += v[k];  // slice order; untouched slices add +0
+    if (r < n_rows) y[r] = acc;
+}
+
+// Production combine (same partials, same slice-order sums, so bit-identical to spmv_combine_kernel): the per-slice
+// ranks "lanes below me whose row slice k touches" come from ONE byte-packed wave scan instead of S ballots + S
+// popcounts. Slices 4j..4j+3 of a lane's mask become the bytes of word j (x * 0x00204081 spreads 4 bits to 4 bytes,
+// no carries), a 6-step DPP inclusive scan of the S/4 words sums them over the lanes (each byte <= 64, so bytes
+// never carry into each other), and inclusive - own is the exclusive rank. The pass is VALU-issue bound (~280 VALU
+// per 64 rows at S = 24 with ballots, profiles/r3_spmv/combine_scan_ab.txt); this form issues ~40% fewer.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ unsigned scan_step_u32(unsigned v) {
+    return v + (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
+}
+template <int S>
+__global__ __launch_bounds__(256) void spmv_combine_scan_kernel(const float* __restrict__ comp,
+                                                                const unsigned* __restrict__ mask,
+                                                                const int* __restrict__ base, SliceOut so,
+                                                                float* __restrict__ y, int n_rows) {
+    static_assert(S % 4 == 0 && S <= 32, "byte-packed slice counters");
+    constexpr int D = S / 4;
+    const int g = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);  // as above
+    const int c = __builtin_amdgcn_readfirstlane(g * 4 + (int)threadIdx.x / kWave);
+    const int lane = pcmx::lane_id();
+    const int r = c * kWave + lane;
+    if (c * kWave >= n_rows) return;
+    const unsigned m = r < n_rows ? __builtin_nontemporal_load(mask + r) : 0u;
+    const int* bc = base + (size_t)c * S;
+    unsigned own[D], inc[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        own[j] = (((m >> (4 * j)) & 0xfu) * 0x00204081u) & 0x01010101u;
+        inc[j] = own[j];
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        inc[j] = scan_step_u32<0x111, 0xf>(inc[j]);  // row_shr:1 .. row_shr:8 within rows of 16 lanes
+        inc[j] = scan_step_u32<0x112, 0xf>(inc[j]);
+        inc[j] = scan_step_u32<0x114, 0xf>(inc[j]);
+        inc[j] = scan_step_u32<0x118, 0xf>(inc[j]);
+        inc[j] = scan_step_u32<0x142, 0xa>(inc[j]);  // row_bcast:15 into rows 1 and 3
+        inc[j] = scan_step_u32<0x143, 0xc>(inc[j]);  // row_bcast:31 into rows 2 and 3
+    }
+    // the S wave-uniform partial bases (32-bit byte offsets: the host keeps the partials < 4 GiB), all in SGPRs
+    // BEFORE the predicated loads: left to itself the compiler sinks each scalar load into its slice's branch and
+    // waits on it there (S serial scalar round trips)
+    unsigned off[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) off[k] = (unsigned)(so.out0[k] + bc[k]) * 4u;
+#pragma unroll
+    for (int k = 0; k < S; ++k) asm volatile("" ::"s"(off[k]));
+    // exclusive ranks are < 64, so the byte offsets 4 * rank (< 256) still fit their bytes: one shift per word,
+    // then one bit-field extract per slice
+    unsigned ex4[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) ex4[j] = (inc[j] - own[j]) << 2;
+    const auto rc = rsrc(comp, 0xffffffffu);
+    float v[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        const unsigned boff = (ex4[k / 4] >> (8 * (k % 4))) & 0xffu;
+        v[k] = 0.f;
+        if ((own[k / 4] >> (8 * (k % 4))) & 0xffu) v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, boff, off[k], 0));
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < S; ++k) acc += v[k];
     if (r < n_rows) y[r] = acc;
 }
 
@@ -743,13 +809,22 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
     }
     if (mode & 16) return (int)hipGetLastError();
     const unsigned cb = (unsigned)((n_rows + 2047) / 2048) * 8;  // 4 waves of 64 rows per block, 8k blocks
+    // bit 6 (lab): the ballot-rank combine instead of the byte-packed scan (bit-identical results); the scan form
+    // addresses the partials with 32-bit byte offsets
+    if (so.out0[n_slices] >= (1ll << 30)) mode |= 64;
+#define PCMX_COMBINE(K)                                                                                            \
+    do {                                                                                                           \
+        if (mode & 64) spmv_combine_kernel<K><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows);      \
+        else spmv_combine_scan_kernel<K><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows);           \
+    } while (0)
     switch (n_slices) {
-        case 8: spmv_combine_kernel<8><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
-        case 16: spmv_combine_kernel<16><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
-        case 24: spmv_combine_kernel<24><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
-        case 32: spmv_combine_kernel<32><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows); break;
+        case 8: PCMX_COMBINE(8); break;
+        case 16: PCMX_COMBINE(16); break;
+        case 24: PCMX_COMBINE(24); break;
+        case 32: PCMX_COMBINE(32); break;
         default: return (int)hipErrorInvalidValue;
     }
+#undef PCMX_COMBINE
     if (n_fix > 0)
         spmv_fixup_kernel<<<(n_fix + 3) / 4, 256, 0, s>>>(extra, reinterpret_cast<const int2*>(fix), n_fix, y);
     return (int)hipGetLastError();

@@ -190,7 +190,7 @@ class SlicedCSR:
     def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None, mode: int = 0) -> torch.Tensor:
         """y = A x; `out` (contiguous f32, >= n_rows elements) receives y in place when given. mode bit 4: products
         only (compact partials, no combine), bit 5: combine + fix-up only (of the partials a bit-4 call wrote)."""
-        if self.cr is not None and (mode & 0xCF) == 0:  # production: packed index stream (bits 8+: resident blocks)
+        if self.cr is not None and (mode & 0x8F) == 0:  # production: packed index stream (bit 6: ballot combine, 8+: resident blocks)
             if getattr(self, "_meta_packed", None) is None:
                 self._meta_packed = torch.cat([self.meta, torch.tensor(self.colbase, dtype=torch.int64)]).contiguous()
                 self._no_lrow = torch.empty(0, dtype=torch.int16, device=self.cr.device)

@@ -402,6 +402,9 @@ def test_spmv_sliced_powerlaw_vs_fp64(gpu, slices, head):
     unpacked = ops.SlicedCSR(m.to(gpu), slices, head=head, pack=False)
     assert unpacked.cr is None
     assert torch.equal(out, unpacked.spmv(x.to(gpu)).cpu().double())
+    # byte-packed-scan combine (production) vs the ballot-rank combine (mode bit 6): same partials, same order
+    assert torch.equal(out, s.spmv(x.to(gpu), mode=64).cpu().double())
+    assert torch.equal(out, unpacked.spmv(x.to(gpu), mode=64).cpu().double())
 
 
 @pytest.mark.parametrize("item_nnz", [512, 1024])
