@@ -109,6 +109,7 @@ def main(argv=None):
     from parallel_c_programs_amd.models import workloads as W
     from parallel_c_programs_amd.parallel import finalize, init
     from parallel_c_programs_amd.utils.harness import timed
+    from parallel_c_programs_amd.utils.metrics import bench_line
 
     ctx = init(backend=args.backend, device=args.device)
     world, rank, dev = ctx.world, ctx.rank, ctx.device
@@ -268,29 +269,19 @@ def main(argv=None):
         guarded("allreduce", allreduce)
 
     if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": _r(tflops, 3),
-            "unit": "TFLOPS",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": Wm,
-            "ms_per_step": _r(ms_gemm),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (uniform random operands generated on device; power-law CSR generated per rank)",
-            "config": {
+        # BASELINE.json publishes no number ("published": {}), so vs_baseline stays null
+        line = bench_line(
+            metric=METRIC, value=_r(tflops, 3), unit="TFLOPS", n_gpus=world, steps=K, warmup=Wm,
+            ms_per_step=_r(ms_gemm), higher_is_better=True, scaling="weak", baseline=None, dtype="fp32",
+            data="synthetic (uniform random operands generated on device; power-law CSR generated per rank)",
+            config={
                 "model": f"SGEMM {n}x{n}x{n} fp32 (v_mfma_f32_32x32x2_f32) per GPU + global reduce/scan "
                          f"{rn:.0e} f32 + stencil {args.stencil_n}^2 bf16 + SpMV {args.spmv_nnz:.0e} nnz",
                 "global_batch": world,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
             },
-            "device": dev.type,
-            **out,
-        }
+            partial="sgemm" not in sections, device=dev.type, **out)
         print(json.dumps(line), flush=True)
     finalize(ctx)
 
