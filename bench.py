@@ -268,9 +268,10 @@ def main(argv=None):
     if ctx.distributed and dev.type == "cuda" and ctx.backend == "nccl":
         guarded("allreduce", allreduce)
 
+    rc = 0
     if rank == 0:
         # BASELINE.json publishes no number ("published": {}), so vs_baseline stays null
-        line = bench_line(
+        fields = dict(
             metric=METRIC, value=_r(tflops, 3), unit="TFLOPS", n_gpus=world, steps=K, warmup=Wm,
             ms_per_step=_r(ms_gemm), higher_is_better=True, scaling="weak", baseline=None, dtype="fp32",
             data="synthetic (uniform random operands generated on device; power-law CSR generated per rank)",
@@ -281,10 +282,17 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{world}",
             },
-            partial="sgemm" not in sections, device=dev.type, **out)
+            device=dev.type, **out)
+        try:
+            line = bench_line(partial="sgemm" not in sections, **fields)
+        except ValueError as e:  # still print what was measured (with the reason), then fail the run after finalize
+            line = {k: v for k, v in fields.items() if k != "baseline"}
+            line["vs_baseline"] = None
+            line["contract_error"], rc = str(e), 1
         print(json.dumps(line), flush=True)
-    finalize(ctx)
+    finalize(ctx)  # every rank reaches this, also when rank 0's line failed the contract
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
