@@ -51,3 +51,21 @@ def test_bench_small_cpu_prints_a_valid_line():
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     validate_bench_line(line)
     assert line["n_gpus"] == 1 and line["value"] > 0
+
+
+def test_bench_prints_line_with_contract_error(monkeypatch, capsys):
+    """A line that fails the contract is still printed (with the reason) and bench.main returns 1."""
+    import importlib
+
+    import parallel_c_programs_amd.utils.metrics as M
+
+    sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+
+    def broken(**kw):
+        raise ValueError("bench line violates the driver contract: test")
+
+    monkeypatch.setattr(M, "bench_line", broken)
+    rc = bench.main(["--small", "--device", "cpu", "--steps", "1", "--warmup", "0", "--sections", "reduce"])
+    line = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert rc == 1 and "test" in line["contract_error"] and line["vs_baseline"] is None and "reduce_weak_gbps" in line
