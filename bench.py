@@ -2,40 +2,52 @@
 """Headline benchmark: "TFLOPS SGEMM 8192^2 + GB/s reduce 1e9 f32, at 1/2/4/8 MI355X" (BASELINE.json), plus
 every other BASELINE.json north-star config measured at the same N in the same job.
 
-One process per GPU (torchrun / torch.distributed.run, RCCL over xGMI for N > 1). Sections, each with its
-own correctness check, all timed the same way (W untimed warm-up steps, then EXACTLY K timed steps bracketed
-by barrier + torch.cuda.synchronize() on both sides, max over ranks; utils/harness.py):
+One process per GPU over RCCL/xGMI. `bench.py --gpus N` with N > 1 and no launcher environment (no WORLD_SIZE)
+starts `python -m torch.distributed.run --nproc-per-node N bench.py ...` itself as a child process, before anything
+touches the GPU, and exits with its status (the reference's `mpirun -n P region pic1.bmp`,
+2-mpi-region-growing/Makefile:4); N larger than the visible GPU count is refused, and so is a launcher whose
+WORLD_SIZE differs from --gpus. Sections, each with its own correctness check, all timed the same way (W untimed
+warm-up steps, then EXACTLY K timed steps bracketed by barrier + torch.cuda.synchronize() on both sides, max over
+ranks; utils/harness.py), each also reporting its per-step hipEvent device time (min / median / max):
 
-  sgemm    (value) 8192^3 fp32 C = A @ B per GPU on the MFMA kernel, weak scaling; fp64 spot check; the
-           hipBLASLt torch.matmul of the same operands is timed alongside for reference, and so is the fp32 GEMM on
-           the bf16 matrix cores (exact 3-way operand split, 6 piece products: fp32 accuracy, its own fp64 check;
-           an extra field, never the headline value)
+  sgemm    (value) 8192^3 fp32 C = A @ B per GPU on the MFMA kernel, weak scaling; EVERY element of C checked
+           against an fp64 GEMM; the hipBLASLt torch.matmul of the same operands is timed alongside for reference,
+           and so is the fp32 GEMM on the bf16 matrix cores (exact 3-way operand split, 6 piece products: fp32
+           accuracy, its own full fp64 check; an extra field, never the headline value)
   reduce   global sum, local HBM reduce + one-scalar RCCL all-reduce: weak (1e9 f32 per GPU) and strong
            (1e9 f32 in total, 1e9/N per GPU); fp64 check
   scan     global inclusive prefix sum over the rank-ordered concatenation (reduce-then-scan): weak and
-           strong like reduce; fp64 check of EVERY output of every rank incl. its rank offset, after the stream's
-           look-back error word (scan_check)
+           strong like reduce; fp64 check of EVERY output of every rank incl. its rank offset, and the stream's
+           look-back error word
   stencil  16384^2 bf16 5-point stencil, strong scaling: row slabs, T fused updates per kernel (T by slab
            height: 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8) and one T-row halo exchange per neighbour overlapped with
            the interior update; bit-exact checks: the timed grid itself (all warm-up + timed updates) against a
            plain-PyTorch single-step oracle, and a small grid through the same distributed path
   spmv     power-law CSR, 1e8 nnz / 1e7 rows, strong scaling: nnz-balanced row blocks, XCD-sliced kernel,
            ghost exchange (only the x entries each rank's nonzeros reference, grouped per-peer send/recv) chunked
-           and overlapped with the product; fp64 check of every rank's rows
+           and overlapped with the product; fp64 check of every rank's rows and ghosts
   (N > 1)  256 MiB RCCL all-reduce bus bandwidth
-  vendor   every section carries the vendor library on the same data, timed identically: hipBLASLt
-           (torch.matmul), rocPRIM (torch.sum, torch.cumsum), hipSPARSE (torch sparse CSR x vector) and, at N = 1,
-           rocSPARSE's generic SpMV with its analysis done once (bin/spmv_vendor, a child process)
+  vendor   every section carries the vendor library on the same data: hipBLASLt (torch.matmul), rocPRIM
+           (torch.sum, torch.cumsum), hipSPARSE (torch sparse CSR x vector) timed like our kernels, and, at N = 1,
+           rocSPARSE's generic SpMV with its analysis done once (bin/spmv_vendor, a child process: W warm-ups, then
+           K back-to-back calls between two events, the mean; fp64 reference)
 
-rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra
-fields of the same line. A section after SGEMM that raises is reported as "<section>_error" in the line (its
-fields missing) instead of costing the line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
+Checks are ENFORCED: fp64-referenced errors must be <= 1e-5 (workloads.REL_ERR_LIMIT), bit-exact flags true. A
+failing check adds "<section>_check_failed" (the failing keys) to the line; a section that raises adds
+"<section>_error". Either way the line is still printed once by rank 0, every rank records the same outcome (a
+collective decision on a separate CPU process group at the end of each section: a failure local to one rank cannot
+pair with a data collective another rank waits in), and the run exits 1. `--inject-fault SECTION:RANK:KIND`
+(KIND perturb = corrupt that rank's timed output after timing, raise = raise in its check) is the test hook.
+
+rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra fields
+of the same line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 
 import torch
@@ -62,13 +74,16 @@ def parse(argv=None):
     ap.add_argument("--spmv-exchange", default="ghost", choices=("ghost", "allgather"),
                     help="N>1 vector exchange: only the referenced entries (ghost) or the whole y (allgather)")
     ap.add_argument("--sections", default=",".join(SECTIONS), help="comma list out of " + ",".join(SECTIONS))
-    ap.add_argument("--no-ref", action="store_true", help="skip the torch.matmul (hipBLASLt) reference timing")
+    ap.add_argument("--no-ref", action="store_true", help="skip the vendor-library timings")
     ap.add_argument("--no-x6", action="store_true", help="skip the fp32-via-bf16x6 SGEMM extra (variant 20)")
     ap.add_argument("--small", action="store_true", help="tiny sizes (CPU/gloo rehearsal)")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu")
     ap.add_argument("--backend", default=None, choices=("nccl", "gloo"),
                     help="process-group backend (default: nccl = RCCL on a GPU). gloo with --device cuda runs every "
-                         "rank's GPU kernels with host-staged messages: N ranks on ONE GPU (tests of the N>1 path)")
+                         "rank's GPU kernels with host-staged messages: N ranks may share ONE GPU (tests of the N>1 "
+                         "path)")
+    ap.add_argument("--inject-fault", default=None, metavar="SECTION:RANK:KIND",
+                    help="test hook: KIND perturb (corrupt that rank's timed output) or raise (raise in its check)")
     a = ap.parse_args(argv)
     if a.small:
         a.size, a.reduce_n, a.stencil_n, a.spmv_rows, a.spmv_nnz = 256, 1e5, 256, 2e4, 2e5
@@ -83,29 +98,152 @@ def _r(v, nd=4):
     return round(v, nd) if abs(v) >= 10 ** (3 - nd) else float(f"{v:.4g}")
 
 
-def rocsparse_bar(n_rows: int, nnz: int, reps: int) -> dict:
-    """rocSPARSE's generic SpMV (preprocess once, compute stage timed) on the same power-law matrix: bin/spmv_vendor,
-    a child process on /opt/rocm's rocSPARSE + HIP runtime (torch's sparse CSR path re-analyses the matrix per call).
-    Runs after our sections, this process idle on the GPU meanwhile."""
-    import subprocess
+# ------------------------------------------------------------------------------------------------ launcher
+def _wants_gpu(args) -> bool:
+    if args.device is not None:
+        return args.device.startswith("cuda")
+    return torch.cuda.device_count() > 0  # (counts devices without initialising HIP in this process)
 
+
+def launch(args, argv: list[str]) -> int:
+    """--gpus N > 1 without a launcher: one fresh `torch.distributed.run` child with N ranks (this process never
+    touches the GPU and never execs), its exit status returned. Each rank's stdout goes straight through; only rank 0
+    prints the JSON line."""
+    if _wants_gpu(args) and args.backend != "gloo":
+        visible = torch.cuda.device_count()
+        if args.gpus > visible:
+            print(f"[bench] error: --gpus {args.gpus} but only {visible} GPU(s) visible; one rank per GPU over RCCL "
+                  f"needs {args.gpus} (--backend gloo lets ranks share a GPU, for tests)", file=sys.stderr, flush=True)
+            return 2
+    from parallel_c_programs_amd.parallel.dist import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    print(f"[bench] launching {args.gpus} ranks: torch.distributed.run --nproc-per-node {args.gpus}", file=sys.stderr,
+          flush=True)
+    rc = subprocess.run(cmd, env=env).returncode
+    return rc if rc >= 0 else 128 - rc
+
+
+def rocsparse_bar(n_rows: int, nnz: int, reps: int, warmup: int) -> dict:
+    """rocSPARSE's generic SpMV (preprocess once; W warm-up calls, then K back-to-back compute calls between two
+    events, the mean; max error against an fp64 host product) on the same power-law matrix: bin/spmv_vendor, a
+    child process on /opt/rocm's rocSPARSE + HIP runtime (torch's sparse CSR path re-analyses the matrix per call).
+    Runs after our sections, this process idle on the GPU meanwhile."""
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bin", "spmv_vendor")
     if not os.path.exists(exe):
         return {"rocsparse_spmv_gflops": "not built (bin/spmv_vendor)"}
     try:
-        r = subprocess.run([exe, str(n_rows), str(nnz), str(reps)], capture_output=True, text=True, timeout=240)
+        r = subprocess.run([exe, str(n_rows), str(nnz), str(reps), str(warmup)], capture_output=True, text=True,
+                           timeout=240)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         res = json.loads(line)
         algs = {k[:-7]: v for k, v in res.items() if k.endswith("_gflops") and k != "best_gflops"}
         best = max(algs, key=algs.get)
         return {"rocsparse_spmv_gflops": res["best_gflops"], "rocsparse_spmv_alg": best,
-                "rocsparse_spmv_max_rel_err": res.get(f"{best}_max_rel_err")}
+                "rocsparse_spmv_max_rel_err_vs_fp64": res.get(f"{best}_max_rel_err")}
     except Exception as e:  # the line says why the bar is missing
         return {"rocsparse_spmv_gflops": f"failed: {type(e).__name__}: {e}"[:200]}
 
 
+# ------------------------------------------------------------------------------------------------ sections
+class Checks:
+    """One section's local check values: record(key, value, limit) with value <= limit to pass (errors), or a bool
+    that must be True (bit-exact flags); info(key, value, agg) for reported-only values (device step times)."""
+
+    def __init__(self):
+        self.items = {}  # key -> (value, agg, limit)
+
+    def error(self, key, value, limit):
+        self.items[key] = (float(value), "max", float(limit))
+
+    def flag(self, key, ok):
+        self.items[key] = (bool(ok), "all", None)
+
+    def info(self, key, value, agg="max"):
+        self.items[key] = (value, agg, None)
+
+
+class Runner:
+    """Runs bench sections; at the end of each one every rank joins ONE decision on a separate gloo group (each
+    rank's error and local check values), so all ranks record the same outcome and go on together."""
+
+    def __init__(self, ctx, out: dict, fault: str | None, log):
+        from parallel_c_programs_amd.parallel.dist import side_group
+
+        self.ctx, self.out, self.log = ctx, out, log
+        self.side = side_group(ctx)
+        self.failed = []  # sections that errored or failed a check
+        self.fault = None
+        if fault:
+            sec, rank, kind = fault.split(":")
+            if kind not in ("perturb", "raise"):
+                raise ValueError("--inject-fault SECTION:RANK:perturb|raise")
+            self.fault = (sec, int(rank), kind)
+
+    def injected(self, section: str, kind: str) -> bool:
+        return self.fault is not None and self.fault == (section, self.ctx.rank, kind)
+
+    def maybe_raise(self, section: str):
+        if self.injected(section, "raise"):
+            raise RuntimeError(f"injected fault in {section} on rank {self.ctx.rank}")
+
+    def run(self, name: str, fn) -> None:
+        from parallel_c_programs_amd.parallel.dist import gather_objects
+
+        chk, err = Checks(), None
+        try:
+            fn(chk)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            err = f"{type(e).__name__}: {e}"[:300]
+        if self.ctx.device.type == "cuda":
+            torch.cuda.empty_cache()  # (after the except block: no traceback pins the section's tensors)
+        states = gather_objects((err, chk.items), self.side)
+        errs = [(r, e) for r, (e, _) in enumerate(states) if e]
+        if errs:
+            r, e = errs[0]
+            self.out[f"{name}_error"] = e if r == 0 and len(errs) == 1 else f"rank {r}: {e}" + (
+                f" (+{len(errs) - 1} more ranks)" if len(errs) > 1 else "")
+        merged = {}
+        for _, items in states:
+            for k, (v, agg, limit) in items.items():
+                if k not in merged:
+                    merged[k] = (v, agg, limit)
+                    continue
+                pv = merged[k][0]
+                merged[k] = ((pv and v) if agg == "all" else max(pv, v) if agg == "max" else min(pv, v), agg, limit)
+        bad = []
+        for k, (v, agg, limit) in merged.items():
+            self.out[k] = _r(v, 4) if agg in ("max", "min") and limit is None else v
+            if (agg == "all" and not v) or (limit is not None and not v <= limit):
+                bad.append(k)
+        if bad:
+            self.out[f"{name}_check_failed"] = bad
+        if errs or bad:
+            self.failed.append(name)
+            self.log(f"{name} FAILED: " + (self.out.get(f"{name}_error", "") + " " + " ".join(bad)).strip())
+
+
+def device_times(chk: Checks, prefix: str, ms: list) -> None:
+    from parallel_c_programs_amd.utils.harness import step_stats
+
+    for k, v in step_stats(ms).items():
+        chk.info(f"{prefix}_device_ms_{k}", v, "max")
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch(args, argv)
+    if world_env is not None and int(world_env) != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks",
+              file=sys.stderr, flush=True)
+        return 2
+
     from parallel_c_programs_amd.models import workloads as W
     from parallel_c_programs_amd.parallel import finalize, init
     from parallel_c_programs_amd.utils.harness import timed
@@ -113,80 +251,83 @@ def main(argv=None):
 
     ctx = init(backend=args.backend, device=args.device)
     world, rank, dev = ctx.world, ctx.rank, ctx.device
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     if dev.type == "cuda":
         from parallel_c_programs_amd._native import ops as native_ops
 
         native_ops()  # the HIP extension must load: no silent fallback on a GPU box
+        if ctx.backend == "nccl" and world > torch.cuda.device_count():
+            raise SystemExit(f"[bench] {world} RCCL ranks but {torch.cuda.device_count()} GPU(s) visible")
     sections = [s for s in args.sections.split(",") if s]
     K, Wm = args.steps, args.warmup
+    LIM = W.REL_ERR_LIMIT
     out = {}
-
-    def free():
-        if dev.type == "cuda":
-            torch.cuda.empty_cache()
 
     def log(msg):
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
+    runner = Runner(ctx, out, args.inject_fault, log)
+
     # ---- SGEMM (headline value): weak scaling, 8192^3 per GPU
     n = args.size
-    tflops = ms_gemm = None
-    if "sgemm" in sections:
-        g = W.Sgemm(ctx, n=n)
-        t = timed(ctx, g.step, K, Wm)
-        rep = g.report(t, K)
-        tflops, ms_gemm = rep["value"], rep["ms_per_step"]
-        out["sgemm_tflops_per_gpu"] = _r(tflops / world, 3)
-        out["sgemm_max_rel_err_vs_fp64"] = ctx.max_over_ranks(g.check()["max_rel_err_vs_fp64"])
-        if not args.no_ref and dev.type == "cuda":
-            # the vendor library timed exactly like our kernel (same warm-up and step count)
-            t_ref = timed(ctx, lambda: torch.matmul(g.a, g.b, out=g.c), K, Wm)
-            out["hipblaslt_torch_matmul_tflops"] = _r(world * g.work_per_step() * K / t_ref / 1e12, 3)
-        if not args.no_x6 and dev.type == "cuda" and n % 256 == 0:
-            # fp32 GEMM on the bf16 matrix cores (exact 3-way operand split, 6 piece products; sgemm_x6.hip): an
-            # fp32-accurate extra, timed identically with its own fp64 check; never the headline value. A failure
-            # here costs only these fields (the headline above is already measured)
-            try:
-                g.variant = 20
-                t_x6 = timed(ctx, g.step, K, Wm)
-                out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * g.work_per_step() * K / t_x6 / 1e12, 3)
-                out["sgemm_fp32_via_bf16x6_max_rel_err_vs_fp64"] = ctx.max_over_ranks(
-                    g.check()["max_rel_err_vs_fp64"])
-            except Exception as e:  # noqa: BLE001 - reported in the JSON line
-                out["sgemm_fp32_via_bf16x6_error"] = f"{type(e).__name__}: {e}"[:300]
-        del g
-        free()
-        log(f"sgemm {tflops:.1f} TFLOPS")
+    head = {"tflops": None, "ms": None}
 
-    def guarded(name, fn):
-        """Runs one extra section; an exception (raised on every rank alike, e.g. a shape or check failure) is
-        recorded as "<name>_error" in the line instead of costing the whole line (the headline SGEMM value and the
-        other sections still report). A section that hangs is not caught: the driver's time limit ends the run."""
-        try:
-            fn()
-        except Exception as e:  # noqa: BLE001 - reported in the JSON line
-            out[f"{name}_error"] = f"{type(e).__name__}: {e}"[:300]
-            log(f"{name} FAILED: {out[name + '_error']}")
-        free()  # (after the except block: the traceback no longer pins the section's tensors)
+    def sgemm(chk):
+        g = W.Sgemm(ctx, n=n)
+        ms = []
+        t = timed(ctx, g.step, K, Wm, ms)
+        rep = g.report(t, K)
+        head["tflops"], head["ms"] = rep["value"], rep["ms_per_step"]
+        out["sgemm_tflops_per_gpu"] = _r(rep["value"] / world, 3)
+        device_times(chk, "sgemm", ms)
+        if not args.no_ref and dev.type == "cuda":
+            # the vendor library timed exactly like our kernel (same warm-up and step count), into its own buffer:
+            # g.c keeps the output of our timed steps for the check
+            cref = torch.empty_like(g.c)
+            t_ref = timed(ctx, lambda: torch.matmul(g.a, g.b, out=cref), K, Wm)
+            out["hipblaslt_torch_matmul_tflops"] = _r(world * g.work_per_step() * K / t_ref / 1e12, 3)
+            del cref
+        x6 = not args.no_x6 and dev.type == "cuda" and n % 256 == 0
+        if x6:
+            # fp32 GEMM on the bf16 matrix cores (exact 3-way operand split, 6 piece products; sgemm_x6.hip): an
+            # fp32-accurate extra with its own full fp64 check; never the headline value. Timed before the checks
+            # (the checks are local only; every collective of the section comes first)
+            gx = W.Sgemm.__new__(W.Sgemm)
+            gx.__dict__.update(g.__dict__)
+            gx.variant, gx.c = 20, torch.empty_like(g.c)
+            ms6 = []
+            t_x6 = timed(ctx, gx.step, K, Wm, ms6)
+            out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * gx.work_per_step() * K / t_x6 / 1e12, 3)
+            device_times(chk, "sgemm_fp32_via_bf16x6", ms6)
+        if runner.injected("sgemm", "perturb"):
+            g.c[n // 3, n // 5] += 1.0
+        runner.maybe_raise("sgemm")
+        chk.error("sgemm_max_rel_err_vs_fp64", g.check(reduce=False)["max_rel_err_vs_fp64"], LIM)
+        if x6:
+            chk.error("sgemm_fp32_via_bf16x6_max_rel_err_vs_fp64", gx.check(reduce=False)["max_rel_err_vs_fp64"], LIM)
+        log(f"sgemm {head['tflops']:.1f} TFLOPS")
+
+    if "sgemm" in sections:
+        runner.run("sgemm", sgemm)
 
     # ---- reduce / scan: weak (rn per GPU) and strong (rn in total); identical runs at N = 1
     rn = int(args.reduce_n)
 
-    def reduce_scan(name, cls):
+    def reduce_scan(name, cls, chk):
         for mode, per_rank in (("weak", rn), ("strong", -(-rn // world))):
             if mode == "strong" and world == 1:
-                for k in ("gbps", "ms_per_step", "rel_err_vs_fp64"):
+                for k in ("gbps", "ms_per_step"):
                     out[f"{name}_strong_{k}"] = out[f"{name}_weak_{k}"]
+                v, agg, lim = chk.items[f"{name}_weak_rel_err_vs_fp64"]
+                chk.error(f"{name}_strong_rel_err_vs_fp64", v, lim)
                 continue
             w = cls(ctx, n=per_rank)
-            t = timed(ctx, w.step, K, Wm)
+            ms = []
+            t = timed(ctx, w.step, K, Wm, ms)
             rep = w.report(t, K)
             out[f"{name}_{mode}_gbps"] = _r(rep["value"], 1)
             out[f"{name}_{mode}_ms_per_step"] = _r(rep["ms_per_step"])
-            out[f"{name}_{mode}_rel_err_vs_fp64"] = ctx.max_over_ranks(w.check()["rel_err_vs_fp64"])
+            device_times(chk, f"{name}_{mode}", ms)
             if mode == "weak" and not args.no_ref and dev.type == "cuda":
                 # the vendor library on the same per-GPU data, timed exactly like our kernel (rocPRIM behind both)
                 if name == "reduce":
@@ -197,45 +338,62 @@ def main(argv=None):
                     t_ref = timed(ctx, lambda: torch.cumsum(w.x, 0, out=ybuf), K, Wm)
                     out["torch_cumsum_gbps"] = _r(world * 8.0 * w.x.numel() * K / t_ref / 1e9, 1)
                     del ybuf
+            if runner.injected(name, "perturb") and mode == "weak":
+                if name == "reduce":
+                    w.total.mul_(1.001)
+                else:
+                    w.y[w.y.numel() // 3] += 1.0
+            c = w.check(reduce=False)
+            chk.error(f"{name}_{mode}_rel_err_vs_fp64", c["rel_err_vs_fp64"], LIM)
             if name == "scan":  # every timed output checked (not a prefix), rank offsets included
-                out["scan_full_max_rel_err_vs_fp64"] = max(out.get("scan_full_max_rel_err_vs_fp64", 0.0),
-                                                           out[f"scan_{mode}_rel_err_vs_fp64"])
+                chk.flag(f"scan_{mode}_lookback_ok", c["lookback_ok"])
+                prev = chk.items.get("scan_full_max_rel_err_vs_fp64", (0.0,))[0]
+                chk.error("scan_full_max_rel_err_vs_fp64", max(prev, c["rel_err_vs_fp64"]), LIM)
             del w
-            free()
+            if dev.type == "cuda":
+                torch.cuda.empty_cache()
+        runner.maybe_raise(name)  # (after the section's last collective)
         log(f"{name} weak {out[name + '_weak_gbps']} GB/s, strong {out[name + '_strong_gbps']} GB/s")
 
     for name, cls in (("reduce", W.Reduce), ("scan", W.Scan)):
         if name in sections:
-            guarded(name, lambda: reduce_scan(name, cls))
+            runner.run(name, lambda chk, name=name, cls=cls: reduce_scan(name, cls, chk))
 
     # ---- stencil 16384^2 bf16, strong scaling over row slabs with the overlapped fused halo exchange
-    def stencil():
+    def stencil(chk):
         s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse)
-        t = timed(ctx, s.step, K, Wm)
+        ms = []
+        t = timed(ctx, s.step, K, Wm, ms)
         rep = s.report(t, K)
-        chk = s.check()
         out.update({"stencil_glups": _r(rep["value"], 1), "stencil_ms_per_step": _r(rep["ms_per_step"]),
-                    "stencil_updates_per_step": s.slab.fuse,
-                    "stencil_timed_grid_bit_exact": chk["timed_grid_bit_exact"],
-                    "stencil_timed_grid_updates": chk["timed_grid_updates"],
-                    "stencil_bit_exact": chk["bit_exact_vs_single_step_oracle"], "stencil_finite": chk["finite"]})
+                    "stencil_updates_per_step": s.slab.fuse})
+        device_times(chk, "stencil", ms)
+        if runner.injected("stencil", "perturb"):
+            s.slab.interior()[s.slab.rows // 2, 7] += 1.0
+        c = s.check(reduce=False)  # (its small-grid distributed run first, then local-only work)
+        runner.maybe_raise("stencil")
+        out["stencil_timed_grid_updates"] = c["timed_grid_updates"]
+        chk.flag("stencil_timed_grid_bit_exact", c["timed_grid_bit_exact"])
+        chk.flag("stencil_bit_exact", c["bit_exact_vs_single_step_oracle"])
+        chk.flag("stencil_finite", c["finite"])
         del s
         log(f"stencil {out['stencil_glups']} GLUP/s")
 
     if "stencil" in sections:
-        guarded("stencil", stencil)
+        runner.run("stencil", stencil)
 
     # ---- SpMV 1e8-nnz power-law graph, strong scaling
-    def spmv():
+    def spmv(chk):
         vendor = not args.no_ref and dev.type == "cuda"
         sp = W.SpMV(ctx, n_rows=int(args.spmv_rows), nnz=int(args.spmv_nnz), chunks=args.spmv_chunks,
                     exchange=args.spmv_exchange, keep_plain=vendor)
-        t = timed(ctx, sp.step, K, Wm)
+        ms = []
+        t = timed(ctx, sp.step, K, Wm, ms)
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
-                    "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks, "spmv_slices": sp.d.slices,
-                    "spmv_exchange": sp.d.exchange if ctx.distributed else None,
-                    "spmv_max_rel_err_vs_fp64": sp.check()["max_rel_err_vs_fp64"]})
+                    "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks,
+                    "spmv_slices": sp.d.slices, "spmv_exchange": sp.d.exchange if ctx.distributed else None})
+        device_times(chk, "spmv", ms)
         if vendor:  # hipSPARSE (torch sparse CSR x dense vector) on each rank's own rows, the same matrix and x
             try:
                 A = sp.d.vendor_matrix()
@@ -247,17 +405,20 @@ def main(argv=None):
                 del A, yv
             except Exception as e:  # the line says so instead of dropping the bar
                 out["torch_sparse_csr_gflops"] = f"unsupported on this torch build: {type(e).__name__}: {e}"[:200]
+        if runner.injected("spmv", "perturb"):
+            sp.y[0] += 1.0
+        chk.error("spmv_max_rel_err_vs_fp64", sp.check(reduce=False)["max_rel_err_vs_fp64"], LIM)
+        runner.maybe_raise("spmv")
         del sp
-        free()
         log(f"spmv {out['spmv_gflops']} GFLOP/s")
         if vendor and world == 1:
-            out.update(rocsparse_bar(int(args.spmv_rows), int(args.spmv_nnz), K))
+            out.update(rocsparse_bar(int(args.spmv_rows), int(args.spmv_nnz), K, Wm))
 
     if "spmv" in sections:
-        guarded("spmv", spmv)
+        runner.run("spmv", spmv)
 
     # ---- RCCL all-reduce bus bandwidth over xGMI (N > 1)
-    def allreduce():
+    def allreduce(chk):
         import torch.distributed as dist
 
         v = torch.ones(64 << 20, device=dev)
@@ -266,14 +427,15 @@ def main(argv=None):
         out["allreduce_256MiB_busbw_gbps"] = _r(v.numel() * 4 * 2 * (world - 1) / world * kr / t_ar / 1e9, 1)
 
     if ctx.distributed and dev.type == "cuda" and ctx.backend == "nccl":
-        guarded("allreduce", allreduce)
+        runner.run("allreduce", allreduce)
 
-    rc = 0
+    rc = 1 if runner.failed else 0
     if rank == 0:
         # BASELINE.json publishes no number ("published": {}), so vs_baseline stays null
+        out["checks_passed"] = not runner.failed
         fields = dict(
-            metric=METRIC, value=_r(tflops, 3), unit="TFLOPS", n_gpus=world, steps=K, warmup=Wm,
-            ms_per_step=_r(ms_gemm), higher_is_better=True, scaling="weak", baseline=None, dtype="fp32",
+            metric=METRIC, value=_r(head["tflops"], 3), unit="TFLOPS", n_gpus=world, steps=K, warmup=Wm,
+            ms_per_step=_r(head["ms"]), higher_is_better=True, scaling="weak", baseline=None, dtype="fp32",
             data="synthetic (uniform random operands generated on device; power-law CSR generated per rank)",
             config={
                 "model": f"SGEMM {n}x{n}x{n} fp32 (v_mfma_f32_32x32x2_f32) per GPU + global reduce/scan "
@@ -284,7 +446,7 @@ def main(argv=None):
             },
             device=dev.type, **out)
         try:
-            line = bench_line(partial="sgemm" not in sections, **fields)
+            line = bench_line(partial="sgemm" not in sections or "sgemm" in runner.failed, **fields)
         except ValueError as e:  # still print what was measured (with the reason), then fail the run after finalize
             line = {k: v for k, v in fields.items() if k != "baseline"}
             line["vs_baseline"] = None

@@ -1,7 +1,9 @@
-/* bin/spmv_vendor [n_rows] [nnz] [reps] — the vendor-library bar of the north-star SpMV config: the same 1e8-nnz
- * power-law CSR matrix (libpcmx_cpu generator, bit-identical to the bench's) times x on the GPU through rocSPARSE's
- * generic SpMV, analysis/preprocess done ONCE, only the compute stage timed (HIP events, median of reps), for every
- * CSR algorithm rocSPARSE offers; the result is checked against the host OpenMP product. One JSON line.
+/* bin/spmv_vendor [n_rows] [nnz] [reps] [warmup] — the vendor-library bar of the north-star SpMV config: the same
+ * 1e8-nnz power-law CSR matrix (libpcmx_cpu generator, bit-identical to the bench's) times x on the GPU through
+ * rocSPARSE's generic SpMV, analysis/preprocess done ONCE, only the compute stage timed, for every CSR algorithm
+ * rocSPARSE offers. Timed like bench.py's own sections: `warmup` untimed calls, then `reps` back-to-back compute
+ * calls between two HIP events, the mean per call. The result is checked against an fp64 host product. One JSON
+ * line.
  * A standalone process linked against /opt/rocm's rocSPARSE + HIP (not torch's copies): bench.py runs it as a
  * child process after its own sections (torch's sparse CSR path re-analyses the matrix on every call, which is
  * why its own bar, torch_sparse_csr_gflops, reads ~6 GFLOP/s). */
@@ -36,11 +38,13 @@
 int main(int argc, char** argv) {
     const int n = argc > 1 ? (int)atof(argv[1]) : 10000000;
     const long long target = argc > 2 ? (long long)atof(argv[2]) : 100000000LL;
-    const int reps = argc > 3 ? atoi(argv[3]) : 10;
+    const int reps = std::max(1, argc > 3 ? atoi(argv[3]) : 10);
+    const int warmup = std::max(0, argc > 4 ? atoi(argv[4]) : 3);
     std::vector<long long> rp64(n + 1);
     const long long nnz = pcmx_powerlaw_row_counts(n, target, 2.5, 1, rp64.data());
     std::vector<int> col(nnz), rp(n + 1);
-    std::vector<float> val(nnz), x(n), y(n), yref(n);
+    std::vector<float> val(nnz), x(n), y(n);
+    std::vector<double> yref(n);
     pcmx_powerlaw_fill(n, n, rp64.data(), 1, col.data(), val.data());
     if (nnz >= (1LL << 31)) return 2;
     for (int i = 0; i <= n; ++i) rp[i] = (int)rp64[i];
@@ -49,7 +53,12 @@ int main(int argc, char** argv) {
         s = s * 1664525u + 1013904223u;
         v = (float)(s >> 8) * (1.f / 16777216.f);
     }
-    pcmx_spmv_csr_omp(n, rp.data(), col.data(), val.data(), x.data(), yref.data());
+
+    for (int i = 0; i < n; ++i) {  // fp64 reference
+        double acc = 0.0;
+        for (int j = rp[i]; j < rp[i + 1]; ++j) acc += (double)val[j] * (double)x[col[j]];
+        yref[i] = acc;
+    }
 
     int *drp, *dcol;
     float *dval, *dx, *dy;
@@ -98,24 +107,24 @@ int main(int argc, char** argv) {
         HCK(hipMalloc(&buf, bytes ? bytes : 16));
         RCK(rocsparse_spmv(h, rocsparse_operation_none, &one, A, vx, &zero, vy, rocsparse_datatype_f32_r, a.alg,
                            rocsparse_spmv_stage_preprocess, &bytes, buf));
-        std::vector<float> ts;
-        for (int r = 0; r < reps + 2; ++r) {
-            HCK(hipEventRecord(e0));
+        for (int r = 0; r < warmup; ++r)
             RCK(rocsparse_spmv(h, rocsparse_operation_none, &one, A, vx, &zero, vy, rocsparse_datatype_f32_r, a.alg,
                                rocsparse_spmv_stage_compute, &bytes, buf));
-            HCK(hipEventRecord(e1));
-            HCK(hipEventSynchronize(e1));
-            float ms = 0;
-            HCK(hipEventElapsedTime(&ms, e0, e1));
-            if (r >= 2) ts.push_back(ms);
-        }
-        std::sort(ts.begin(), ts.end());
-        const double ms = ts[ts.size() / 2];
+        HCK(hipDeviceSynchronize());
+        HCK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r)
+            RCK(rocsparse_spmv(h, rocsparse_operation_none, &one, A, vx, &zero, vy, rocsparse_datatype_f32_r, a.alg,
+                               rocsparse_spmv_stage_compute, &bytes, buf));
+        HCK(hipEventRecord(e1));
+        HCK(hipEventSynchronize(e1));
+        float total_ms = 0;
+        HCK(hipEventElapsedTime(&total_ms, e0, e1));
+        const double ms = total_ms / reps;
         HCK(hipMemcpy(y.data(), dy, sizeof(float) * n, hipMemcpyDeviceToHost));
         double err = 0.0, scale = 1e-30;
         for (int i = 0; i < n; ++i) {
-            err = std::max(err, (double)std::fabs(y[i] - yref[i]));
-            scale = std::max(scale, (double)std::fabs(yref[i]));
+            err = std::max(err, std::fabs((double)y[i] - yref[i]));
+            scale = std::max(scale, std::fabs(yref[i]));
         }
         const double gf = 2.0 * nnz / (ms * 1e-3) / 1e9;
         best = std::max(best, gf);

@@ -128,10 +128,12 @@ static int connect_retry(uint32_t ip_be, int port, double timeout_s) {
 
 static int tcp_push(pcmx_comm_t* c, int is_send, void* buf, size_t bytes, int peer) {
     tcp_impl_t* t = (tcp_impl_t*)c->impl;
-    if (peer < 0 || peer >= c->world) return -2;
+    if (peer < 0 || peer >= c->world) return PCMX_ERR_ARG;
     if (t->nops == t->cap) {
-        t->cap = t->cap ? 2 * t->cap : 16;
-        t->ops = (tcp_op_t*)realloc(t->ops, sizeof(tcp_op_t) * (size_t)t->cap);
+        const int cap = t->cap ? 2 * t->cap : 16;
+        tcp_op_t* ops = (tcp_op_t*)realloc(t->ops, sizeof(tcp_op_t) * (size_t)cap);
+        if (!ops) return PCMX_ERR_ALLOC;
+        t->ops = ops, t->cap = cap;
     }
     t->ops[t->nops++] = (tcp_op_t){is_send, (char*)buf, bytes, 0, peer};
     return 0;
@@ -151,7 +153,7 @@ static int tcp_progress(pcmx_comm_t* c) {
             tcp_op_t* r = &t->ops[j];
             if (r->is_send || r->peer != c->rank || r->done == r->bytes + 1) continue;
             if (r->bytes != s->bytes) {
-                rc = -3;
+                rc = PCMX_ERR_ARG; /* size mismatch of a send/recv-to-self pair */
                 break;
             }
             memcpy(r->buf, s->buf, s->bytes);
@@ -159,15 +161,20 @@ static int tcp_progress(pcmx_comm_t* c) {
             matched = 1;
             break;
         }
-        if (!matched && !rc) rc = -3; /* send to self without a recv from self */
+        if (!matched && !rc) rc = PCMX_ERR_ARG; /* send to self without a recv from self */
     }
     for (int i = 0; i < t->nops && !rc; ++i) /* recv from self without a send to self */
-        if (!t->ops[i].is_send && t->ops[i].peer == c->rank && t->ops[i].done != t->ops[i].bytes + 1) rc = -3;
+        if (!t->ops[i].is_send && t->ops[i].peer == c->rank && t->ops[i].done != t->ops[i].bytes + 1)
+            rc = PCMX_ERR_ARG;
     if (rc) {
         t->nops = 0;
         return rc;
     }
     struct pollfd* pf = (struct pollfd*)calloc((size_t)2 * W, sizeof(struct pollfd));
+    if (!pf) {
+        t->nops = 0;
+        return PCMX_ERR_ALLOC;
+    }
     double t_start = now_s(); /* deadline: 60 s without progress */
     const double t_limit = 60.0;
     for (;;) {
@@ -198,7 +205,7 @@ static int tcp_progress(pcmx_comm_t* c) {
         int k = left_ms > 0 ? poll(pf, (nfds_t)npf, left_ms) : 0;
         if (k < 0 && errno == EINTR) continue; /* a signal is not a transport failure: retry, same deadline */
         if (k <= 0) {
-            rc = k == 0 ? -4 : -5; /* timeout / error */
+            rc = k == 0 ? PCMX_ERR_TIMEOUT : PCMX_ERR_COMM; /* no progress for t_limit / poll() failed */
             break;
         }
         t_start = now_s();
@@ -214,8 +221,8 @@ static int tcp_progress(pcmx_comm_t* c) {
                 ssize_t n = dir ? send(pf[q].fd, o->buf + o->done, o->bytes - o->done, MSG_DONTWAIT | MSG_NOSIGNAL)
                                 : recv(pf[q].fd, o->buf + o->done, o->bytes - o->done, MSG_DONTWAIT);
                 if (n > 0) o->done += (size_t)n;
-                else if (n == 0 && !dir) rc = -6; /* peer closed */
-                else if (n < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) rc = -7;
+                else if (n == 0 && !dir) rc = PCMX_ERR_COMM; /* peer closed */
+                else if (n < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) rc = PCMX_ERR_COMM;
                 break;
             }
             if (rc) break;
@@ -233,7 +240,7 @@ static int tcp_group_start(pcmx_comm_t* c) {
 }
 static int tcp_group_end(pcmx_comm_t* c) {
     tcp_impl_t* t = (tcp_impl_t*)c->impl;
-    if (t->in_group <= 0) return -1;
+    if (t->in_group <= 0) return PCMX_ERR_ARG;
     if (--t->in_group == 0) return tcp_progress(c);
     return 0;
 }

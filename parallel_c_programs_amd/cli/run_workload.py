@@ -23,11 +23,16 @@ def _val(s: str):
     return {"true": True, "false": False}.get(s.lower(), s)
 
 
+class CheckFailed(SystemExit):
+    """The workload's numerics check failed: its JSON line is printed, then the process exits 1."""
+
+
 def run(name: str, argv=None, defaults: dict | None = None, add_args=None, to_cfg=None, prog: str | None = None,
         doc: str | None = None, time_line: bool = False) -> dict | None:
     """Builds workload `name` from defaults <- to_cfg(parsed CLI args) <- --set key=value, times it like bench.py
     (warm-up, then `steps` steps between barrier + device syncs, max over ranks) and prints one JSON line on rank 0
-    (preceded by the reference's "Time : %f s" per step when time_line)."""
+    (preceded by the reference's "Time : %f s" per step when time_line). A failed numerics check ("check_passed"
+    false in the line) exits the process with status 1 after the line is printed (CheckFailed)."""
     ap = argparse.ArgumentParser(prog=prog or f"run_{name}", description=doc,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     if add_args:
@@ -56,9 +61,11 @@ def run(name: str, argv=None, defaults: dict | None = None, add_args=None, to_cf
             if time_line:
                 print_time(rep["ms_per_step"] / 1e3)
             emit_metric(**out)
-        return out
     finally:
         finalize(ctx)
+    if not out.get("check_passed", True):
+        raise CheckFailed(1)
+    return out
 
 
 def main(argv=None) -> int:

@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 import socket
 from dataclasses import dataclass
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -161,8 +162,29 @@ def init(backend: str | None = None, device: str | None = None) -> Context:
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": dev} if backend == "nccl" else {}
+        # a collective that one rank never joins (it failed before reaching it) ends the job after this many
+        # seconds (RCCL watchdog / gloo timeout) instead of hanging it
+        kw["timeout"] = timedelta(seconds=int(os.environ.get("PCMX_PG_TIMEOUT_S", "600")))
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     return Context(rank, world, local, dev, backend if world > 1 else "none")
+
+
+def side_group(ctx: Context):
+    """A CPU (gloo) process group beside the data group, for collective DECISIONS (did any rank fail a section?):
+    its operations have their own sequence, so a decision can never pair with a data collective another rank is
+    still waiting in. None when not distributed."""
+    if not ctx.distributed:
+        return None
+    return dist.new_group(backend="gloo")
+
+
+def gather_objects(obj, group=None) -> list:
+    """Every rank's `obj` (picklable), in rank order, over `group` (a side_group; [obj] when not distributed)."""
+    if group is None:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj, group=group)
+    return out
 
 
 def finalize(ctx: Context | None = None) -> None:

@@ -311,10 +311,11 @@ class DistributedSpMV:
                 outs.append(y)
         return torch.cat(outs) if outs else torch.zeros(0, dtype=torch.float64, device=xp.device)
 
-    def layout_max_rel_err(self, y: torch.Tensor, xp: torch.Tensor) -> float:
+    def layout_max_rel_err(self, y: torch.Tensor, xp: torch.Tensor, reduce: bool = True) -> float:
         """Max relative error of EVERY entry of the layout vector y = A xp against fp64: own rows and the ghost
         entries the exchange delivered (each compared with its owner's fp64 row, gathered once), i.e. the
-        product and the exchange that the timed step performs. Same value on every rank."""
+        product and the exchange that the timed step performs. Same value on every rank (reduce=False: this
+        rank's entries only, no collective after the all-gather of the fp64 rows)."""
         ref = self.reference_local(xp)
         if self.ctx.distributed:
             buf = torch.zeros(self.block, dtype=torch.float64, device=ref.device)
@@ -328,5 +329,5 @@ class DistributedSpMV:
         got, want = y[m].double(), full[ids[m]]
         scale = full.abs().max().clamp_min(1e-30) if full.numel() else torch.ones((), dtype=torch.float64)
         err = ((got - want).abs().max() / scale).item() if want.numel() else 0.0
-        return self.ctx.max_over_ranks(err)
+        return self.ctx.max_over_ranks(err) if reduce else err
 

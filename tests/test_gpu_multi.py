@@ -14,10 +14,10 @@ from parallel_c_programs_amd.utils import bmp
 pytestmark = pytest.mark.gpu
 
 
-def _bench(nproc, *extra, timeout=240):
+def _bench(nproc, *extra, timeout=240, self_launch=False):
     from parallel_c_programs_amd.parallel import free_port
 
-    if nproc == 1:
+    if nproc == 1 or self_launch:  # (bench.py --gpus N > 1 starts torch.distributed.run itself)
         cmd = [sys.executable, str(ROOT / "bench.py")]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -32,10 +32,14 @@ def _bench(nproc, *extra, timeout=240):
 
 def _check_line(out, n):
     assert out["n_gpus"] == n and out["device"] == "cuda" and out["value"] > 0
+    assert out["checks_passed"] is True and not [k for k in out if k.endswith("_check_failed")], out
     for k in ("reduce_weak_gbps", "reduce_strong_gbps", "scan_weak_gbps", "scan_strong_gbps", "stencil_glups",
               "spmv_gflops"):
         assert out[k] > 0, k
-    assert out["stencil_bit_exact"] and out["stencil_finite"]
+    for k in ("sgemm", "reduce_weak", "scan_weak", "stencil", "spmv"):  # per-step hipEvent device time
+        assert 0 < out[f"{k}_device_ms_min"] <= out[f"{k}_device_ms_median"] <= out[f"{k}_device_ms_max"], k
+    assert out["stencil_bit_exact"] and out["stencil_finite"] and out["stencil_timed_grid_bit_exact"]
+    assert out["scan_full_max_rel_err_vs_fp64"] < 1e-5 and out["scan_weak_lookback_ok"]
     assert out["sgemm_max_rel_err_vs_fp64"] < 1e-5 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
     assert out["sgemm_fp32_via_bf16x6_tflops"] > 0 and out["sgemm_fp32_via_bf16x6_max_rel_err_vs_fp64"] < 1e-5
     assert out["reduce_strong_rel_err_vs_fp64"] < 1e-5 and out["scan_strong_rel_err_vs_fp64"] < 1e-5
@@ -48,6 +52,26 @@ def test_bench_small_one_gpu(gpu):
 
 def _ngpu():
     return torch.cuda.device_count()
+
+
+def test_bench_more_gpus_than_visible_is_refused(gpu):
+    """`bench.py --gpus N` with N > the visible GPUs (no launcher): a clear error and a non-zero exit, no line."""
+    n = _ngpu() + 1
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--small"], capture_output=True,
+                       text=True, timeout=120, env=cli_env())
+    assert r.returncode == 2 and f"--gpus {n} but only {n - 1} GPU(s) visible" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_wrong_result_fails_on_the_gpu(gpu):
+    """A perturbed timed SGEMM C (one element; the old 8-row sample would have missed it) fails the full fp64 check:
+    the line prints with sgemm_check_failed and the run exits 1."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--steps", "1", "--warmup", "0", "--size", "1024", "--no-ref",
+           "--sections", "sgemm", "--inject-fault", "sgemm:0:perturb"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=cli_env())
+    assert r.returncode == 1, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["sgemm_check_failed"] == ["sgemm_max_rel_err_vs_fp64"] and out["checks_passed"] is False
 
 
 @pytest.mark.parametrize("nproc", [2, 4, 8])
@@ -67,6 +91,20 @@ def test_bench_ranks_share_one_gpu_over_gloo(gpu, nproc):
 def test_bench_small_torchrun_all_gpus(gpu):
     n = min(_ngpu(), 8)
     _check_line(_bench(n, "--steps", "2", "--warmup", "1", "--small", "--no-ref"), n)
+
+
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 visible GPUs")
+def test_bench_self_launch_all_gpus_rccl(gpu):
+    """The driver's own command shape: `python bench.py --gpus N` (no launcher) runs N RCCL ranks."""
+    n = min(_ngpu(), 8)
+    _check_line(_bench(n, "--steps", "2", "--warmup", "1", "--small", "--no-ref", self_launch=True), n)
+
+
+def test_bench_self_launch_two_ranks_share_one_gpu(gpu):
+    """`bench.py --gpus 2 --backend gloo` without a launcher: two ranks (sharing the GPU over gloo) in one line."""
+    out = _bench(2, "--steps", "2", "--warmup", "1", "--no-ref", "--backend", "gloo", "--small", timeout=110,
+                 self_launch=True)
+    _check_line(out, 2)
 
 
 @pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 visible GPUs")

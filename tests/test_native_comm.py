@@ -152,3 +152,31 @@ def test_native_collectives_rccl(gpu):
     r = _launch(n, BIN / "collectives")
     assert r.returncode == 0, r.stderr
     assert f"collectives ok world={n}" in r.stdout
+
+
+def test_tcp_transport_error_codes_world1():
+    """TCP transport failures reach the caller as the shared PCMX_ERR_* codes (pcmx_errors.h): a peer out of range
+    and a send/recv-to-self size mismatch are argument errors (-1), not timeouts or allocation failures."""
+    import ctypes
+
+    from parallel_c_programs_amd._native import cpu_lib
+    from parallel_c_programs_amd.parallel import free_port
+
+    lib = cpu_lib()
+    comm = ctypes.c_void_p()
+    assert lib.pcmx_comm_init_tcp(0, 1, b"127.0.0.1", free_port(), ctypes.byref(comm)) == 0
+    try:
+        a, b = ctypes.create_string_buffer(16), ctypes.create_string_buffer(16)
+        assert lib.pcmx_comm_send(comm, a, ctypes.c_size_t(4), 3) == -1  # peer 3 of world 1
+        assert lib.pcmx_comm_group_start(comm) == 0
+        assert lib.pcmx_comm_send(comm, a, ctypes.c_size_t(8), 0) == 0
+        assert lib.pcmx_comm_recv(comm, b, ctypes.c_size_t(4), 0) == 0
+        assert lib.pcmx_comm_group_end(comm) == -1  # size mismatch of the self pair
+        assert lib.pcmx_comm_group_end(comm) == -1  # no group open
+        a.value = b"abcdefg"
+        assert lib.pcmx_comm_group_start(comm) == 0
+        assert lib.pcmx_comm_send(comm, a, ctypes.c_size_t(8), 0) == 0
+        assert lib.pcmx_comm_recv(comm, b, ctypes.c_size_t(8), 0) == 0
+        assert lib.pcmx_comm_group_end(comm) == 0 and b.value == b"abcdefg"
+    finally:
+        lib.pcmx_comm_destroy(comm)

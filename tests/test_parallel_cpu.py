@@ -347,9 +347,9 @@ def test_bench_rehearsal_gloo_world2():
     assert not [k for k in out if k.endswith("_error")]
 
 
-def test_bench_failed_section_is_reported_not_fatal():
+def test_bench_failed_section_is_reported_and_fails_the_run():
     """A section that raises (here: an unsupported stencil fuse depth) costs only its own fields: the line still
-    prints once, with "<section>_error", and the later sections still run."""
+    prints once, with "<section>_error", the later sections still run, and the run exits 1."""
     import json
     import subprocess
     import sys
@@ -359,12 +359,80 @@ def test_bench_failed_section_is_reported_not_fatal():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--small", "--device", "cpu", "--steps", "1",
                         "--warmup", "0", "--sections", "stencil,spmv", "--stencil-fuse", "99"],
                        capture_output=True, text=True, timeout=300, env=cli_env(OMP_NUM_THREADS="2"))
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 1, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["stencil_error"].startswith("ValueError") and "stencil_glups" not in out
     assert out["spmv_gflops"] > 0 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
+    assert out["checks_passed"] is False
+
+
+def _bench_cpu(*extra, timeout=600):
+    """bench.py on the CPU WITHOUT a launcher (--gpus N > 1 makes it start torch.distributed.run itself)."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT, cli_env
+
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--small", "--device", "cpu", *extra],
+                       capture_output=True, text=True, timeout=timeout, env=cli_env(OMP_NUM_THREADS="1"))
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[0]) if len(lines) == 1 else None), len(lines)
+
+
+def test_bench_gpus_2_launches_two_ranks_itself():
+    """`bench.py --gpus 2` with no WORLD_SIZE: one torch.distributed.run child with 2 ranks, ONE line, n_gpus 2."""
+    r, out, nlines = _bench_cpu("--gpus", "2", "--steps", "2", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert nlines == 1 and out["n_gpus"] == 2 and out["checks_passed"] is True
+    assert out["config"]["parallelism"] == "dp2" and out["reduce_strong_gbps"] > 0
+    for k in ("sgemm", "reduce_weak", "scan_weak", "stencil", "spmv"):
+        assert out[f"{k}_device_ms_median"] > 0, k
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    import subprocess
+    import sys
+
+    from conftest import ROOT, cli_env
+    from parallel_c_programs_amd.parallel import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "bench.py"), "--gpus", "3", "--small",
+           "--device", "cpu", "--steps", "1", "--warmup", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=cli_env(OMP_NUM_THREADS="1"))
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr and not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("fault,section,failed_key", [
+    ("sgemm:1:perturb", "sgemm", "sgemm_max_rel_err_vs_fp64"),
+    ("scan:0:perturb", "scan", "scan_weak_rel_err_vs_fp64"),
+    ("stencil:1:perturb", "stencil", "stencil_timed_grid_bit_exact"),
+    ("spmv:1:perturb", "spmv", "spmv_max_rel_err_vs_fp64"),
+])
+def test_bench_wrong_result_on_one_rank_fails_the_run(fault, section, failed_key):
+    """A wrong timed result on ONE rank (injected after timing): every rank records the failed check in the same
+    collective decision, the line still prints once with "<section>_check_failed", the later sections still run,
+    and the run exits 1 (ref 3-serial-optimization/spmv.c:179-191, 366: every output compared)."""
+    r, out, nlines = _bench_cpu("--gpus", "2", "--steps", "1", "--warmup", "0", "--inject-fault", fault)
+    assert r.returncode == 1, r.stderr[-3000:]
+    assert nlines == 1 and out["checks_passed"] is False
+    assert failed_key in out[f"{section}_check_failed"]
+    assert not [k for k in out if k.endswith("_check_failed") and k != f"{section}_check_failed"]
+    assert out["spmv_gflops"] > 0 and out["value"] > 0
+
+
+def test_bench_exception_on_one_rank_is_a_collective_decision():
+    """A section that raises on rank 1 only (after its collectives): both ranks record "<section>_error", the
+    following sections run on both ranks (no mismatched collectives, no hang) and pass, the run exits 1."""
+    r, out, nlines = _bench_cpu("--gpus", "2", "--steps", "1", "--warmup", "0", "--inject-fault", "reduce:1:raise")
+    assert r.returncode == 1, r.stderr[-3000:]
+    assert nlines == 1 and out["reduce_error"].startswith("rank 1: RuntimeError")
+    assert out["scan_strong_rel_err_vs_fp64"] < 1e-5 and out["stencil_bit_exact"] and out["spmv_gflops"] > 0
+    assert not [k for k in out if k.endswith("_check_failed")]
 
 
 # ------------------------------------------------------------------ launcher-level (torch.distributed.run)
@@ -436,3 +504,41 @@ def test_distributed_volume_zslabs_match_single_volume(world):
     assert digest == hashlib.md5(reg_ref.numpy().tobytes()).hexdigest()
     assert np.array_equal(img, img_ref.numpy())
     assert stats["host_reads"] <= stats["outer_steps"] // 2 + 1
+
+
+# ------------------------------------------------------------------ run_workload numerics checks (exit 1 on failure)
+
+@pytest.mark.parametrize("name,sets", [
+    ("region2d", []), ("region2d", ["side=700"]), ("histeq", ["side=512"]), ("region3d", []),
+    ("raycast", ["image_dim=32", "method=global"]),
+])
+def test_run_workload_checks_pass_on_cpu(name, sets):
+    """Every workload carries a real check: region2d = the golden out.bmp (T1) / the serial oracle, histeq = the
+    serial host oracle bit for bit (T3), region3d = the 2,197,899-voxel box (T2), raycast = the serial caster."""
+    import json
+
+    args = [name, "--steps", "1", "--warmup", "0", "--device", "cpu"]
+    for s_ in sets:
+        args += ["--set", s_]
+    r = run_cli("run_workload", *args, check=False, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["check_passed"] is True, out
+
+
+def test_run_workload_failed_check_exits_1(monkeypatch):
+    """A wrong result fails the check: the line is printed with check_passed false and the process exits 1."""
+    from parallel_c_programs_amd.cli import run_workload
+    from parallel_c_programs_amd.models import workloads as W
+
+    real = W.Histeq.step
+
+    def broken(self):
+        real(self)
+        self.out = self.out.clone()
+        self.out.view(-1)[5] ^= 1
+
+    monkeypatch.setattr(W.Histeq, "step", broken)
+    with pytest.raises(SystemExit) as e:
+        run_workload.run("histeq", ["--steps", "1", "--warmup", "0", "--device", "cpu", "--set", "side=64"])
+    assert e.value.code == 1
