@@ -68,6 +68,8 @@ def parse(argv=None):
     ap.add_argument("--stencil-n", type=int, default=16384)
     ap.add_argument("--stencil-fuse", type=int, default=0,
                     help="fused updates per kernel / halo depth (0: by slab height, 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8)")
+    ap.add_argument("--stencil-halo-mult", type=int, default=0,
+                    help="deep halo: m x fuse halo rows exchanged every m steps (0: 2 at N > 1, 1 at N = 1)")
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
     ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")
@@ -361,12 +363,12 @@ def main(argv=None):
 
     # ---- stencil 16384^2 bf16, strong scaling over row slabs with the overlapped fused halo exchange
     def stencil(chk):
-        s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse)
+        s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse, halo_mult=args.stencil_halo_mult)
         ms = []
         t = timed(ctx, s.step, K, Wm, ms)
         rep = s.report(t, K)
         out.update({"stencil_glups": _r(rep["value"], 1), "stencil_ms_per_step": _r(rep["ms_per_step"]),
-                    "stencil_updates_per_step": s.slab.fuse})
+                    "stencil_updates_per_step": s.slab.fuse, "stencil_halo_mult": s.slab.m})
         device_times(chk, "stencil", ms)
         if runner.injected("stencil", "perturb"):
             s.slab.interior()[s.slab.rows // 2, 7] += 1.0

@@ -485,12 +485,10 @@ __device__ __forceinline__ void band_limits(int n, int a, int b, int c, int d, i
 //    256-B wave loads, all ceil(nnz/64) <= NL of a row issued before use, two rows in flight per wave).
 //  * no per-row metadata: the rows' nonzero counts and band limits are computed in registers (a wave prefix
 //    scan of the R counts gives each row's offset from the block's first row); row_off is read ONCE per block.
-template <int R, int NL, int U = 2>
-__global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __restrict__ vals,
-                                                              const long long* __restrict__ row_off, int n, int a, int b,
-                                                              int c, int d, int e, const float* __restrict__ x,
-                                                              float* __restrict__ y) {
-    extern __shared__ float xw[];
+template <int R, int NL, int U>
+__device__ __forceinline__ void banded_rows_body(const float* __restrict__ vals, const long long* __restrict__ row_off,
+                                                 int n, int a, int b, int c, int d, int e, const float* __restrict__ x,
+                                                 float* __restrict__ y, float* xw) {
     static_assert(R <= kWave && R % 4 == 0, "rows per block");
     const int lane = pcmx::lane_id();
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
@@ -578,109 +576,134 @@ __global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __res
         }
     }
 }
-
-// Variant 2: the same row blocks and LDS windows, values read with 16-B loads: a row's values start at any 4-B
-// boundary, so lane l loads the aligned float4 l (+64m) of the span [start & ~3, start + nnz) and handles its 4
-// elements j = 4(l + 64m) + k - lead (lead = start & 3; elements outside the row are masked to 0). NL4 loads per
-// row (ceil((nnz + 3) / 256)), U rows of a wave in flight.
-template <int R, int NL4, int U>
-__global__ __launch_bounds__(256) void spmv_banded_lds4_kernel(const float* __restrict__ vals,
-                                                               const long long* __restrict__ row_off, int n, int a,
-                                                               int b, int c, int d, int e, const float* __restrict__ x,
-                                                               float* __restrict__ y) {
+template <int R, int NL, int U = 2>
+__global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __restrict__ vals,
+                                                              const long long* __restrict__ row_off, int n, int a, int b,
+                                                              int c, int d, int e, const float* __restrict__ x,
+                                                              float* __restrict__ y) {
     extern __shared__ float xw[];
-    static_assert(R <= kWave && R % 4 == 0 && (R / 4) % U == 0, "rows per block");
+    banded_rows_body<R, NL, U>(vals, row_off, n, a, b, c, d, e, x, y, xw);
+}
+
+// Variant 8 (block stream): a block of R rows reads its values — ONE contiguous CSR range — as one aligned 16-B
+// stream through a buffer descriptor over the whole value array (a float4 past the end reads 0; nothing is read
+// outside the array), instead of row by row with 4-B loads. Wave w takes the w-th quarter of the block's float4s,
+// all NV loads issued before the x windows are staged, so each lane keeps NV x 16 B in flight.
+// Valid for blocks of UNCLIPPED rows (every band inside [0, n)): all such rows have the same length L and the
+// same band layout, so element e of the block (from its first value) is row rr = floor(e / L), position
+// j = e - rr L, and its x window slot is j + rr + lut[j] (lut[j] = window base of j's band minus the band's
+// first position: the windows shift by one column per row). Blocks holding a clipped row (the first / last
+// ~(a/2 + b + c + d + e) rows) run the row-per-wave body of variant 1 instead.
+// Row sums: the 256 elements of one wave iteration span at most two rows (L >= 256, checked by the launcher);
+// lanes add their products to acc_cur (the wave's current row) or acc_next, and when the current row has ended
+// the wave reduces acc_cur into the block's row sums in LDS (ds_add_f32: a row split between two waves gets two
+// commutative adds, so the result is the same whichever lands first).
+template <int R, int NV>
+__device__ __forceinline__ void banded_stream_body(const float* __restrict__ vals, long long boff,
+                                                   int L, int r0, const int (&cum)[5], const float* __restrict__ x,
+                                                   const int (&wlo)[5], const int (&wbase)[5], int total,
+                                                   float* __restrict__ y, float* xw, int* lut, float* ysum) {
     const int lane = pcmx::lane_id();
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
-    const int r0 = (int)blockIdx.x * R, nr = min(R, n - r0);
-    int wlo[5], wbase[5], total = 0;
-    {
-        int lo0[5], hi0[5], lo1[5], hi1[5];
-        band_limits(n, a, b, c, d, e, r0, lo0, hi0);
-        band_limits(n, a, b, c, d, e, r0 + nr - 1, lo1, hi1);
+    const long long a0 = boff & ~3LL;
+    const int lead = (int)(boff - a0);
+    const int nf4 = (lead + R * L + 3) >> 2;         // float4s of the block's aligned span
+    const int q = (nf4 + 3) >> 2;                    // per wave
+    const int f0 = wave * q, f1 = min(nf4, f0 + q);  // this wave's float4s [f0, f1)
+    // descriptor over exactly the block's aligned span (vals is 16-B aligned, a0 a multiple of 4 floats; the span's
+    // last float4 ends at most 3 values past the block, inside the array: clipped rows always follow)
+    const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vals + a0), (short)0, nf4 * 16, 0x00020000);
+    pcmx::f32x4 v[NV];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            wlo[k] = lo0[k], wbase[k] = total;
-            total += max(0, hi1[k] - lo0[k]);
-        }
+    for (int m = 0; m < NV; ++m) {
+        const int f = f0 + lane + 64 * m;
+        const unsigned off = f < f1 ? (unsigned)f * 16u : 0x80000000u;  // past this wave's quarter: reads 0
+        v[m] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, off, 0, 2));
     }
     for (int i = (int)threadIdx.x; i < total; i += 256) {
         const int k = (i >= wbase[1]) + (i >= wbase[2]) + (i >= wbase[3]) + (i >= wbase[4]);
-        const int src = wlo[0] + i - wbase[0] + (k >= 1 ? (wlo[1] - wbase[1]) - (wlo[0] - wbase[0]) : 0) +
-                        (k >= 2 ? (wlo[2] - wbase[2]) - (wlo[1] - wbase[1]) : 0) +
-                        (k >= 3 ? (wlo[3] - wbase[3]) - (wlo[2] - wbase[2]) : 0) +
-                        (k >= 4 ? (wlo[4] - wbase[4]) - (wlo[3] - wbase[3]) : 0);
-        xw[i] = x[src];
-    }
-    int my = 0;
-    if (lane < nr) {
-        int lo[5], hi[5];
-        band_limits(n, a, b, c, d, e, r0 + lane, lo, hi);
+        int wl = wlo[0], wb = wbase[0];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) my += hi[k] - lo[k];
+        for (int p = 1; p < 5; ++p)
+            if (k == p) wl = wlo[p], wb = wbase[p];
+        xw[i] = x[wl + i - wb];
     }
-    int incl = my;
+    for (int i = (int)threadIdx.x; i < L; i += 256) {  // lut[j] = window base - first position of j's band
+        const int k = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]) + (i >= cum[4]);
+        int v = wbase[0] - cum[0];
 #pragma unroll
-    for (int off = 1; off < R; off <<= 1) {
-        const int o = __shfl_up(incl, off, kWave);
-        if (lane >= off) incl += o;
+        for (int p = 1; p < 5; ++p)
+            if (k == p) v = wbase[p] - cum[p];
+        lut[i] = v;
     }
-    const long long boff = row_off[r0];
+    if (threadIdx.x < R) ysum[threadIdx.x] = 0.f;
     __syncthreads();
-
-    for (int rr = wave; rr < nr; rr += 4 * U) {
-        pcmx::f32x4 v[U][NL4];
-        int off[U][5], cum[U][4], nnz[U], lead[U];
+    if (f0 < f1) {
+        const float invL = 1.0f / (float)L;
+        // element index of lane 0's first element in iteration m: 4 (f0 + 64 m) - lead
+        int cur = (4 * f0 - lead) < 0 ? 0 : (4 * f0 - lead) / L;  // wave-uniform current row
+        float acc = 0.f, accn = 0.f;
+        const int elast = min(4 * f1 - lead, R * L) - 1;  // last element of this wave
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int row = rr + 4 * u;
-            nnz[u] = 0;
-            if (row >= nr) continue;
-            const int row_nnz = __builtin_amdgcn_readlane(my, row);
-            const long long start = boff + (long long)__builtin_amdgcn_readlane(incl - my, row);
-            const long long a0 = start & ~3LL;
-            lead[u] = (int)(start - a0);
-            const int span = lead[u] + row_nnz;
-            const pcmx::f32x4* vr = reinterpret_cast<const pcmx::f32x4*>(vals + a0);
+        for (int m = 0; m < NV; ++m) {
+            const int ebase = 4 * (f0 + 64 * m) - lead;  // wave-uniform
+            if (ebase > elast) break;
 #pragma unroll
-            for (int m = 0; m < NL4; ++m) {
-                const int q = lane + 64 * m;
-                v[u][m] = (256 * m < span && 4 * q < span) ? vr[q] : pcmx::f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int kk = 0; kk < 4; ++kk) {
+                const int e = ebase + 4 * lane + kk;
+                const bool in = e >= 0 && e <= elast;
+                const int ec = in ? e : (cur * L);
+                // rr = floor(e / L): (e + 0.5) / L is at least 0.5 / L away from an integer, far above the f32 error
+                const int rr = (int)__builtin_fmaf((float)ec, invL, 0.5f * invL);
+                const int j = ec - rr * L;
+                const float p = (in ? v[m][kk] : 0.f) * xw[j + rr + lut[j]];
+                if (rr == cur) acc += p;
+                else accn += p;
             }
-            int lo[5], hi[5];
-            band_limits(n, a, b, c, d, e, r0 + row, lo, hi);
-            int cs = 0;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                off[u][k] = wbase[k] + lo[k] - wlo[k] - cs;
-                cs += hi[k] - lo[k];
-                if (k < 4) cum[u][k] = cs;
+            // the current row ended inside this iteration (its last element is at or below the iteration's last)
+            const int eend = min(ebase + 255, elast);
+            if ((cur + 1) * L - 1 <= eend) {
+                const float s = pcmx::wave_reduce<float, 0>(acc);
+                if (lane == 0) atomicAdd(&ysum[cur], s);
+                acc = accn, accn = 0.f, ++cur;
             }
-            nnz[u] = row_nnz;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (nnz[u] == 0) continue;
-            float acc = 0.f;
-#pragma unroll
-            for (int m = 0; m < NL4; ++m) {
-                if (256 * m >= lead[u] + nnz[u]) break;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int jr = 4 * (lane + 64 * m) + k - lead[u];
-                    const bool in = jr >= 0 && jr < nnz[u];
-                    const int j = min(max(jr, 0), nnz[u] - 1);
-                    const int o = off[u][0] + (j >= cum[u][0] ? off[u][1] - off[u][0] : 0) +
-                                  (j >= cum[u][1] ? off[u][2] - off[u][1] : 0) +
-                                  (j >= cum[u][2] ? off[u][3] - off[u][2] : 0) +
-                                  (j >= cum[u][3] ? off[u][4] - off[u][3] : 0);
-                    acc = fmaf(in ? v[u][m][k] : 0.f, xw[j + o], acc);
-                }
-            }
-            acc = pcmx::wave_reduce<float, 0>(acc);
-            if (lane == 0) y[r0 + rr + 4 * u] = acc;
+        if (cur < R) {  // the wave's range ends inside row cur (its other part belongs to the next wave)
+            const float s = pcmx::wave_reduce<float, 0>(acc);
+            if (lane == 0) atomicAdd(&ysum[cur], s);
         }
     }
+    __syncthreads();
+    if (threadIdx.x < R) y[r0 + threadIdx.x] = ysum[threadIdx.x];
+}
+
+// Variant 8 launch: blocks of unclipped rows stream (banded_stream_body); the others take the row-per-wave body.
+template <int R, int NV, int NL>
+__global__ __launch_bounds__(256) void spmv_banded_stream_kernel(const float* __restrict__ vals,
+                                                                 const long long* __restrict__ row_off, int n, int a,
+                                                                 int b, int c, int d, int e, int rlo, int rhi, int L,
+                                                                 const float* __restrict__ x, float* __restrict__ y) {
+    extern __shared__ float xw[];
+    const int r0 = (int)blockIdx.x * R;
+    if (r0 < rlo || r0 + R > rhi) {  // a clipped row in the block: the variant-1 body (dynamic LDS sized for it)
+        banded_rows_body<R, NL, 2>(vals, row_off, n, a, b, c, d, e, x, y, xw);
+        return;
+    }
+    int wlo[5], wbase[5], cum[5], total = 0, cs = 0;
+    {
+        int lo0[5], hi0[5], lo1[5], hi1[5];
+        band_limits(n, a, b, c, d, e, r0, lo0, hi0);
+        band_limits(n, a, b, c, d, e, r0 + R - 1, lo1, hi1);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            wlo[k] = lo0[k], wbase[k] = total, cum[k] = cs;
+            total += max(0, hi1[k] - lo0[k]);
+            cs += hi0[k] - lo0[k];
+        }
+    }
+    int* lut = reinterpret_cast<int*>(xw + total);
+    float* ysum = reinterpret_cast<float*>(lut + L);
+    banded_stream_body<R, NV>(vals, row_off[r0], L, r0, cum, x, wlo, wbase, total, y, xw, lut, ysum);
 }
 
 // fallback for rows longer than 16 x 64 nonzeros: one wave per row, strided band loops
@@ -831,13 +854,16 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
 }
 
 extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_off, int n, int a, int b, int c, int d,
+                                        int e, const float* x, float* y, int variant, hipStream_t s);
+extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_off, int n, int a, int b, int c, int d,
                                         int e, const float* x, float* y, int variant, hipStream_t s) {
     if (n <= 0) return 0;
     if (a < 1 || b < 0 || c < 0 || d < 0 || e < 0) return PCMX_ERR_ARG;
     const long long maxrow = 2LL * (a / 2) + 1 + 2LL * c + 2LL * e;  // nonzeros of an unclipped row
     const int nl = (int)((maxrow + 63) / 64);
     // variant 1 (default) R = 16 rows per block, 2 rows per wave in flight; 4: R 32 / U 2; 5: R 16 / U 4;
-    // 6: R 32 / U 4; 7: R 64 / U 2 (scripts/spmv_banded_lab.py); 2 / 3: 16-B value loads
+    // 6: R 32 / U 4; 7: R 64 / U 2 (scripts/spmv_banded_lab.py); 8: block stream (16-B loads over each block's
+    // contiguous value range, spmv_banded_stream_kernel)
     const int R = variant == 4 || variant == 6 ? 32 : variant == 7 ? 64 : 16;
     const size_t lds = (size_t)(maxrow + 5 * (R - 1)) * sizeof(float);
     if (variant == 0 || nl > 16 || lds > 64 * 1024) {
@@ -845,18 +871,30 @@ extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_
         return (int)hipGetLastError();
     }
     const int grid = (n + R - 1) / R;
-    const int nl4 = (int)((maxrow + 3 + 255) / 256);
-    if (variant == 2 || variant == 3) {
-        if (nl4 > 4) return PCMX_ERR_ARG;
-        const bool u4 = variant == 3;
-#define PCMX_BANDED4(NL4)                                                                                              \
-    (u4 ? (spmv_banded_lds4_kernel<16, NL4, 4><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y), 0)      \
-        : (spmv_banded_lds4_kernel<16, NL4, 2><<<grid, 256, lds, s>>>(vals, row_off, n, a, b, c, d, e, x, y), 0))
-        if (nl4 <= 1) PCMX_BANDED4(1);
-        else if (nl4 <= 2) PCMX_BANDED4(2);
-        else if (nl4 <= 3) PCMX_BANDED4(3);
-        else PCMX_BANDED4(4);
-#undef PCMX_BANDED4
+    if (variant == 8) {
+        // rows [rlo, rhi) are unclipped (every band inside [0, n)) and all hold L nonzeros; a block of RS rows
+        // streams when all its rows are unclipped, and its wave quarters need NV float4 loads per lane
+        constexpr int RS = 16;
+        const long long ah = a / 2, r9 = ah + b + c + d + e;
+        const long long L = 2 * ah + 1 + 2LL * c + 2LL * e;
+        const long long rlo = r9, rhi = (long long)n - r9;
+        const long long q = ((L * RS + 3 + 3) / 4 + 3) / 4;  // float4s per wave quarter (lead <= 3)
+        const long long nv = (q + 63) / 64;
+        // the wave-iteration rule needs rows of >= 256 nonzeros, the float4 stream a 16-B aligned vals; otherwise
+        // (or when the LDS windows do not fit) the variant-1 kernel runs
+        const size_t lds8 = (size_t)(maxrow + 5 * (RS - 1) + L + RS) * sizeof(float);
+        const bool ok = L >= 256 && nv <= 12 && rhi - rlo >= RS && !((uintptr_t)vals & 15) && lds8 <= 64 * 1024;
+        if (!ok) return pcmx_spmv_banded_variant(vals, row_off, n, a, b, c, d, e, x, y, 1, s);
+        const int g8 = (n + RS - 1) / RS;
+#define PCMX_STREAM(NV)                                                                                               \
+    spmv_banded_stream_kernel<RS, NV, 16><<<g8, 256, lds8, s>>>(vals, row_off, n, a, b, c, d, e, (int)rlo, (int)rhi, \
+                                                                 (int)L, x, y)
+        if (nv <= 4) PCMX_STREAM(4);
+        else if (nv <= 6) PCMX_STREAM(6);
+        else if (nv <= 8) PCMX_STREAM(8);
+        else if (nv <= 10) PCMX_STREAM(10);
+        else PCMX_STREAM(12);
+#undef PCMX_STREAM
         return (int)hipGetLastError();
     }
 #define PCMX_BANDED(RR, UU)                                                                                            \

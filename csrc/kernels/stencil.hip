@@ -433,6 +433,8 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
     W pre[kAhead];
 #pragma unroll
     for (int j = 0; j < kAhead; ++j) pre[j] = fetch(min(i0 + j, i1 - 1));
+    // (a branch-free main loop — the per-level trapezoid / store tests peeled into the first 2T rows — measured no
+    // faster at any shape and spilled at 8 columns per lane: profiles/r4_stencil/peel_rpw128_rejected.txt)
     for (int ib = i0; ib < i1; ib += kAhead) {
 #pragma unroll
         for (int j = 0; j < kAhead; ++j) {
@@ -525,26 +527,33 @@ int strips_for(int cols, int cpl, int steps) {
 }
 // lab override of the launch shape (0 = production rule): columns per lane, rows per wave
 int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0;
-// the halo rule of one row range: rows within `steps` of a non-global slab edge read `steps` halo rows
+// the halo rule of one row range: a row r reads rows r - steps .. r + steps, which must lie in the slab on a side
+// with a neighbour (at a GLOBAL edge the clamped reads only feed Dirichlet rows)
 bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row0, long long global_rows) {
     const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
-    return halo >= steps || r0 >= r1 || !((r0 < steps && !top_global) || (r1 > rows - steps && !bot_global));
+    return r0 >= r1 || ((top_global || r0 - steps >= -halo) && (bot_global || r1 + steps <= rows + halo));
 }
 }  // namespace
 
 // T fused updates over local rows [r0a, r1a) and [r0b, r1b) (either may be empty) of a slab with `halo` rows
-// above and below (T = 2, 3, 4, 6, 8), in one launch.
+// above and below (T = 2, 3, 4, 6, 8), in one launch. On a side with a neighbour a span may reach into the halo
+// region (local rows -(halo - T) .. rows + halo - T): the deep-halo schedule of the distributed stencil computes
+// those rows redundantly so the next step needs no exchange (parallel/stencil.py); at a global edge spans are
+// clamped to [0, rows).
 extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, int cols, int ld, int halo, int steps,
                                           int r0a, int r1a, int r0b, int r1b, long long global_row0,
                                           long long global_rows, float k, hipStream_t s) {
     if (rows <= 0 || cols <= 0 || ld < cols || (ld & 7) || (cols & 7) || halo < 1 || steps < 1 ||
         (((uintptr_t)u | (uintptr_t)out) & 15))
         return -1;
-    r0a = max(r0a, 0), r1a = min(r1a, rows), r0b = max(r0b, 0), r1b = min(r1b, rows);
-    if (r0a >= r1a) r0a = r1a = 0;
-    if (r0b >= r1b) r0b = r1b = 0;
-    if (r1a == 0 && r1b == 0) return 0;
-    if (r1a > r0b && r1b > r0a) return -1;  // overlapping spans would race (two waves storing one row)
+    const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
+    const int lo_lim = top_global ? 0 : -max(0, halo - steps), hi_lim = bot_global ? rows : rows + max(0, halo - steps);
+    r0a = max(r0a, lo_lim), r1a = min(r1a, hi_lim), r0b = max(r0b, lo_lim), r1b = min(r1b, hi_lim);
+    const bool ea = r0a >= r1a, eb = r0b >= r1b;
+    if (ea) r0a = r1a = 0;
+    if (eb) r0b = r1b = 0;
+    if (ea && eb) return 0;
+    if (!ea && !eb && r1a > r0b && r1b > r0a) return -1;  // overlapping spans would race (two waves storing one row)
     if (!halo_ok(rows, halo, steps, r0a, r1a, global_row0, global_rows) ||
         !halo_ok(rows, halo, steps, r0b, r1b, global_row0, global_rows))
         return -1;

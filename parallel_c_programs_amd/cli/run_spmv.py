@@ -2,8 +2,10 @@
 
 Host path (default): prints "Time : %f s" for the naive CSR product and for the banded SIMD product, then
 the compare() report — the reference's exact output. --gpu additionally times the gfx950 CSR-adaptive and
-banded kernels on the same matrix (HIP events) and prints each in the reference's format ("Time : %f s" and the
-compare() report against the host naive product)."""
+banded kernels on the same matrix (HIP events) and prints each in the reference's format ("Time : %f s", the median
+of back-to-back calls, and the compare() report against the host naive product), plus its cold-cache time (median
+of 5 calls each after a 1 GiB read: the 248 MB value stream of the reference config otherwise stays in the 256 MiB
+Infinity Cache between calls)."""
 from __future__ import annotations
 
 import argparse
@@ -42,16 +44,29 @@ def main(argv=None) -> int:
              m.nnz * 8 + (m.n_rows + 1) * 8 + m.n_rows * 8),
             ("GPU banded, implicit columns, LDS-staged x windows", lambda: ops.spmv_banded(g.val, g.row_ptr, *dims, xg),
              m.nnz * 4 + m.n_rows * 8))
+    scrub = torch.empty(256 << 20, device="cuda").uniform_()  # 1 GiB, READ between cold calls (evicts the MALL)
     for name, fn, bytes_ in runs:
         y = fn()
         ms = device_time_ms(fn)
+        cold = []
+        for _ in range(5):
+            scrub.sum()
+            torch.cuda.synchronize()
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            fn()
+            s1.record()
+            s1.synchronize()
+            cold.append(s0.elapsed_time(s1))
+        cold_ms = sorted(cold)[2]
         print(f"\n{name}:", flush=True)
         c_call("print_time_seconds", None, [ctypes.c_double], ms * 1e-3)
         yc = y.cpu().contiguous()
         c_call("compare", None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int], y_ref.data_ptr(), yc.data_ptr(),
                a.dim)
         print(f"({bytes_ / ms / 1e6:.1f} GB/s of compulsory traffic, {2 * m.nnz / ms / 1e6:.1f} GFLOP/s, "
-              f"max |err| {(yc - y_ref).abs().max().item():.3g})", flush=True)
+              f"max |err| {(yc - y_ref).abs().max().item():.3g}; cold cache (after a 1 GiB read): "
+              f"{cold_ms * 1e3:.1f} us = {bytes_ / cold_ms / 1e6:.1f} GB/s)", flush=True)
     return 0
 
 

@@ -167,13 +167,15 @@ class Stencil(Workload):
     fuse=T (default 0: auto_fuse of the slab height): T time steps per kernel (temporal blocking, bit-identical to single steps) and a T-row
     halo exchange every T steps; one step() then advances T time steps and counts T updates per cell."""
 
-    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, fuse=0, **_):
-        from ..parallel.stencil import StencilSlab, auto_fuse
+    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, fuse=0, halo_mult=0, **_):
+        from ..parallel.stencil import StencilSlab, auto_fuse, auto_halo_mult
 
         rows = n * (ctx.world if per_rank else 1)
         fuse = int(fuse) or auto_fuse(rows // ctx.world)
-        super().__init__(ctx, {"n": n, "rows": rows, "graph_steps": graph_steps, "fuse": fuse}, "stencil", "GLUP/s")
-        self.slab = StencilSlab(ctx, rows, n, fuse=fuse)
+        halo_mult = int(halo_mult) or auto_halo_mult(rows // ctx.world, fuse, ctx.world)
+        super().__init__(ctx, {"n": n, "rows": rows, "graph_steps": graph_steps, "fuse": fuse,
+                               "halo_mult": halo_mult}, "stencil", "GLUP/s")
+        self.slab = StencilSlab(ctx, rows, n, fuse=fuse, halo_mult=halo_mult)
         self.overlap = overlap
         self.graph_steps = graph_steps  # >0: one step() = graph_steps updates replayed from a HIP graph
         self.cells_local = self.slab.rows * n
@@ -206,8 +208,8 @@ class Stencil(Workload):
 
         sl = self.slab
         f = sl.fuse
-        n, cols, steps = max(64, 2 * f * self.ctx.world + 8), 200, 4 * f
-        small = StencilSlab(self.ctx, n, cols, fuse=f)
+        n, cols, steps = max(64, 2 * f * sl.m * self.ctx.world + 8), 200, 4 * f
+        small = StencilSlab(self.ctx, n, cols, fuse=f, halo_mult=sl.m)
         small.run(steps, self.overlap)
         full = small.gather()
         ok = 1.0

@@ -8,7 +8,7 @@ from .halo import HaloExchanger2D
 from .region2d import gather_tiles, grow_distributed, scatter_tiles
 from .ring import token_ring
 from .spmv import DistributedSpMV, nnz_balanced_cuts
-from .stencil import StencilSlab, auto_fuse, reference_run
+from .stencil import StencilSlab, auto_fuse, auto_halo_mult, reference_run
 from .topology import CartTopology, dims_create, prime_factors, split
 from .volume3d import DistributedVolume, VolumeSlab, emulate_slabs
 
@@ -17,6 +17,6 @@ __all__ = [
     "CartTopology", "dims_create", "prime_factors", "split",
     "HaloExchanger2D", "global_reduce", "global_scan", "allreduce_buckets", "scatter_rows", "gather_rows",
     "grow_distributed", "scatter_tiles", "gather_tiles", "token_ring",
-    "DistributedSpMV", "nnz_balanced_cuts", "StencilSlab", "auto_fuse", "reference_run",
+    "DistributedSpMV", "nnz_balanced_cuts", "StencilSlab", "auto_fuse", "auto_halo_mult", "reference_run",
     "DistributedVolume", "VolumeSlab", "emulate_slabs",
 ]

@@ -16,6 +16,8 @@ N=8 but up to 17% slower at N=2/4 (cross-stream waits), so it stays on the compu
 Temporal blocking (fuse=T in 2, 3, 4, 6, 8): the slab keeps T halo rows per side, one grouped exchange moves
 T rows per neighbour every T updates (1/T of the messages — the halos are latency-bound on xGMI), and one
 fused kernel performs the T updates with a single HBM read + write per cell. Bit-identical to fuse=1.
+Deep halo (halo_mult m): mT halo rows exchanged every m steps, the rows next to a neighbour computed redundantly in
+between (StencilSlab docstring): one exchange and one edge launch per m steps.
 """
 from __future__ import annotations
 
@@ -36,14 +38,34 @@ def auto_fuse(slab_rows: int) -> int:
     return 8 if slab_rows >= 6144 else 6
 
 
-class StencilSlab:
-    """One rank's (rows + 2, cols) bf16 slab and its double buffer."""
+def auto_halo_mult(slab_rows: int, fuse: int, world: int) -> int:
+    """Halo depth in units of `fuse` rows (the deep-halo schedule, see StencilSlab): 2 for a distributed slab (one
+    exchange + one edge launch per 2 fused launches), 1 on one rank (no halo)."""
+    return 2 if world > 1 and fuse > 1 and slab_rows >= 4 * 2 * fuse else 1
 
-    def __init__(self, ctx: Context, n: int, cols: int | None = None, k: float = DEFAULT_K, fuse: int = 1):
+
+class StencilSlab:
+    """One rank's (rows + 2 halo, cols) bf16 slab and its double buffer.
+
+    Deep halo (halo_mult m >= 2, fuse T > 1): the slab keeps H = mT halo rows per side and exchanges H rows every
+    m steps (every mT updates). The exchange step computes T updates over its own rows AND the (m-1)T halo rows
+    next to each neighbour (their T-step cone reaches H rows out: exactly the received halo); the next step then
+    already holds T valid halo rows and updates rows -(m-2)T .. rows + (m-2)T with ONE launch and no exchange, and so
+    on down to 0 extra rows at the m-th step. Per m steps: one exchange of mT rows, one interior launch + one edge
+    launch (the two halo-dependent bands, mT rows each) and m-1 full launches — instead of m exchanges and 2m
+    launches; the redundant rows cost (m-1)mT / rows of extra work (0.6% at m = 2, T = 6, 2048 rows). Bit-identical
+    to single steps: every computed row follows the same arithmetic from the same inputs."""
+
+    def __init__(self, ctx: Context, n: int, cols: int | None = None, k: float = DEFAULT_K, fuse: int = 1,
+                 halo_mult: int = 1):
         self.ctx, self.n, self.cols, self.k = ctx, n, (n if cols is None else cols), k
         if fuse != 1 and fuse not in FUSED_STEPS:
             raise ValueError(f"fuse: 1 or one of {FUSED_STEPS} updates per kernel")
-        self.fuse, self.halo = fuse, fuse  # T fused updates read T rows beyond the slab
+        if halo_mult < 1 or (halo_mult > 1 and fuse == 1):
+            raise ValueError("halo_mult: >= 1, and > 1 only with fused steps")
+        self.fuse = fuse
+        self.m = halo_mult if ctx.distributed else 1
+        self.halo = fuse * self.m  # T fused updates read T rows beyond the slab; m steps read mT
         self.row0, row1 = split(n, ctx.world, ctx.rank)
         self.rows = row1 - self.row0
         if self.rows < 2 * self.halo:
@@ -51,6 +73,7 @@ class StencilSlab:
         self.u = init_grid(self.rows, self.cols, self.row0, n, device=ctx.device, halo=self.halo)
         self.v = self.u.clone()
         self.steps_done = 0
+        self.phase = 0  # step index within the current deep-halo period (0: the exchange step)
         self.north = ctx.rank - 1 if ctx.rank > 0 else -1
         self.south = ctx.rank + 1 if ctx.rank < ctx.world - 1 else -1
 
@@ -65,6 +88,12 @@ class StencilSlab:
             pairs.append((self.south, u[rows:rows + h], u[rows + h:rows + 2 * h]))
         return self.ctx.neighbour_exchange(pairs, async_op=True)
 
+    def _extent(self, phase: int) -> tuple[int, int]:
+        """Local rows the step at `phase` updates: its own rows plus (m-1-phase)T halo rows on each side with a
+        neighbour."""
+        e = (self.m - 1 - phase) * self.fuse
+        return (-e if self.north >= 0 else 0), self.rows + (e if self.south >= 0 else 0)
+
     def _update(self, u, v, row_range=None):
         """`fuse` updates u -> v over local rows row_range (default all)."""
         if self.fuse > 1:
@@ -72,32 +101,39 @@ class StencilSlab:
         else:
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=row_range)
 
-    def _update_edges(self, u, v):
-        """The two rank-edge bands (rows within `halo` of either end), after the halo rows arrived: one launch."""
-        d, rows = self.halo, self.rows
+    def _update_edges(self, u, v, lo: int, hi: int):
+        """The two halo-dependent bands [lo, T) and [rows - T, hi) after the halo rows arrived: one launch."""
+        T, rows = self.fuse, self.rows
         if self.fuse > 1:
-            stencil5_fused_spans_(u, v, ((0, d), (rows - d, rows)), self.row0, self.n, self.k, halo=d, steps=self.fuse)
+            stencil5_fused_spans_(u, v, ((lo, T), (rows - T, hi)), self.row0, self.n, self.k, halo=self.halo,
+                                  steps=self.fuse)
         else:
-            stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(0, d))
-            stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(rows - d, rows))
+            stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(0, T))
+            stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(rows - T, rows))
 
     def step(self, overlap: bool = True) -> None:
-        """Advances `fuse` time steps (one halo exchange, one kernel launch per row range)."""
-        ctx, rows, d = self.ctx, self.rows, self.halo  # rows within d of a rank edge read the halo
+        """Advances `fuse` time steps: at phase 0 one halo exchange overlapped with the interior launch, then the
+        edge launch; at later phases of a deep halo, one launch and no exchange."""
+        ctx, rows, T = self.ctx, self.rows, self.fuse  # rows within T of a rank edge read the halo
         if not ctx.distributed:
             self._update(self.u, self.v)
-        elif overlap and rows > 2 * d:
-            reqs = self._post_exchange()
-            self._update(self.u, self.v, (d, rows - d))
-            for r in reqs:
-                r.wait()
-            self._update_edges(self.u, self.v)
+        elif self.phase == 0:
+            lo, hi = self._extent(0)
+            if overlap and rows > 2 * T:
+                reqs = self._post_exchange()
+                self._update(self.u, self.v, (T, rows - T))
+                for r in reqs:
+                    r.wait()
+                self._update_edges(self.u, self.v, lo, hi)
+            else:
+                for r in self._post_exchange():
+                    r.wait()
+                self._update(self.u, self.v, (lo, hi))
         else:
-            for r in self._post_exchange():
-                r.wait()
-            self._update(self.u, self.v)
+            self._update(self.u, self.v, self._extent(self.phase))
         self.u, self.v = self.v, self.u
-        self.steps_done += self.fuse
+        self.steps_done += T
+        self.phase = (self.phase + 1) % self.m
 
     # ---- checkpoint / resume (SURVEY §5.4): each rank writes its own slab; tensors only (weights_only load)
     def checkpoint(self, prefix: str) -> str:
@@ -115,6 +151,7 @@ class StencilSlab:
         self.interior().copy_(st["u"].to(self.u.device))  # halos are refreshed by the next exchange
         self.v.copy_(self.u)
         self.k, self.steps_done = st["k"], st["steps_done"]
+        self.phase = 0  # the next step exchanges (the restored halo rows are stale)
 
     def run(self, steps: int, overlap: bool = True, graph: bool = False) -> torch.Tensor:
         """`steps` updates (a multiple of `fuse`). graph=True (single GPU rank): a HIP graph of two launches

@@ -5,7 +5,9 @@ exchange, for the launch shapes a step can take:
   full      one launch over all rows (no overlap split)
   split3    interior launch + one launch per edge band (round-2 step)
   split2    interior launch + both edge bands in ONE two-span launch
-  split2c   split2 with the edge launch on a side stream, concurrent with the interior kernel (current step)
+  split2c   split2 with the edge launch on a side stream, concurrent with the interior kernel
+  deep2     the deep-halo schedule (StencilSlab halo_mult=2): per 2 steps an interior launch + one edge launch over
+            the two 2T-row halo-dependent bands, then ONE launch over the own rows; the time is per step (pair / 2)
 
 Every variant is checked bit for bit against `full`. Prints ms per step and GLUP/s per GPU; with the 1-GPU
 full-grid time this bounds the strong-scaling efficiency of the compute part (docs/ARCHITECTURE.md, stencil).
@@ -68,18 +70,37 @@ def main():
                     ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), row0, N, halo=T, steps=T)
                 main.wait_stream(side)
 
+            # deep halo (m = 2): a slab with 2T halo rows; step 1 covers local rows [-T, rows + T) (interior launch +
+            # edge spans), step 2 the own rows; checked against the same two steps as single full launches
+            u2 = (torch.rand(rows + 4 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
+            v2, w2, ref2 = u2.clone(), u2.clone(), u2.clone()
+
+            def deep2():
+                ops.stencil5_fused_step_(u2, v2, row0, N, halo=2 * T, steps=T, row_range=(T, rows - T))
+                ops.stencil5_fused_spans_(u2, v2, ((-T, T), (rows - T, rows + T)), row0, N, halo=2 * T, steps=T)
+                ops.stencil5_fused_step_(v2, w2, row0, N, halo=2 * T, steps=T, row_range=(0, rows))
+
+            ops.stencil5_fused_step_(u2, ref2, row0, N, halo=2 * T, steps=T, row_range=(-T, rows + T))
+            ref3 = ref2.clone()
+            ops.stencil5_fused_step_(ref2, ref3, row0, N, halo=2 * T, steps=T, row_range=(0, rows))
+
             full()
             res = {}
-            for name, fn in (("full", full), ("split3", split3), ("split2", split2), ("split2c", split2c)):
+            for name, fn in (("full", full), ("split3", split3), ("split2", split2), ("split2c", split2c),
+                             ("deep2", deep2)):
                 out.zero_()
                 fn()
                 torch.cuda.synchronize()
+                if name == "deep2":
+                    same = torch.equal(w2[2 * T:-2 * T], ref3[2 * T:-2 * T])
+                    res[name] = (timed(fn) / 2, same)
+                    continue
                 same = name == "full" or torch.equal(out[T:-T], ref[T:-T])
                 res[name] = (timed(fn), same)
             line = " ".join(f"{k} {ms:.4f} ms {rows * N * T / ms / 1e6:7.0f} GLUP/s{'' if ok else ' MISMATCH'}"
                             for k, (ms, ok) in res.items())
             print(f"fuse={T} N={world} rows={rows:5d}  {line}", flush=True)
-            del u, ref, out
+            del u, ref, out, u2, v2, w2, ref2, ref3
             torch.cuda.empty_cache()
 
 

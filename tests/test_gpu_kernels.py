@@ -313,22 +313,35 @@ def test_stencil_fused_spans_match_full(gpu, steps, spans):
 
 
 @pytest.mark.parametrize("dims", [(20000, 41, 20, 10, 20, 5), (333, 41, 20, 10, 20, 5), (50, 9, 3, 5, 2, 3),
-                                  (4000, 1301, 10, 200, 10, 50)])
+                                  (4000, 1301, 10, 200, 10, 50), (20000, 401, 200, 100, 200, 10),
+                                  (3001, 301, 10, 50, 10, 3), (1500, 401, 200, 100, 200, 10)])
 def test_spmv_banded_variants_vs_host(gpu, dims):
     """Every banded kernel variant (0: wave per row; 1/4-7: LDS-staged windows, 4-B loads, block rows x rows in
-    flight; 2/3: 16-B loads) against the host product: interior rows, rows clipped at both matrix edges (n smaller
-    than the band reach), a row block past the last row, and rows longer than 16 x 64 nonzeros (1301 + 400 + 100:
-    the dispatcher falls back to the wave-per-row kernel for the 4-B-load variants)."""
+    flight; 8: block stream, 16-B loads over each row block's contiguous values) against the host product: interior
+    rows, rows clipped at both matrix edges (n smaller than the band reach: variant 8 then runs the variant-1 body in
+    every block), a row block past the last row, rows longer than 16 x 64 nonzeros (1301 + 400 + 100: the dispatcher
+    falls back to the wave-per-row kernel), and rows shorter than 256 nonzeros (variant 8 falls back to 1)."""
     n = dims[0]
     m = ops.banded_csr(*dims)
     x = ops.create_vector(n)
     ref = ops.spmv(m, x)
     vals, ro, xg = m.val.to(gpu), m.row_ptr.to(gpu), x.to(gpu)
-    for v in (0, 1, 2, 3, 4, 5, 6, 7):
-        if v in (2, 3) and dims[1] + 2 * dims[3] + 2 * dims[5] > 1021:
-            continue  # 16-B variants take rows of up to 4 x 256 - 3 nonzeros
+    for v in (0, 1, 4, 5, 6, 7, 8):
         out = ops.spmv_banded(vals, ro, *dims, xg, variant=v).cpu()
         assert (out - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item()), (v, dims)
+
+
+def test_spmv_banded_stream_unaligned_values_fall_back(gpu):
+    """Variant 8 on a value array that is not 16-B aligned (a view one float in): the variant-1 kernel runs, same
+    result; nothing is read outside the array."""
+    dims = (6000, 401, 200, 100, 200, 10)
+    m = ops.banded_csr(*dims)
+    x = ops.create_vector(dims[0])
+    ref = ops.spmv(m, x)
+    buf = torch.zeros(m.val.numel() + 1, device=gpu)
+    buf[1:] = m.val.to(gpu)
+    out = ops.spmv_banded(buf[1:], m.row_ptr.to(gpu), *dims, x.to(gpu), variant=8).cpu()
+    assert (out - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item())
 
 
 def test_scan_check_per_stream(gpu):

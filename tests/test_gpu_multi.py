@@ -181,13 +181,14 @@ def test_volume3d_ranks_share_one_gpu_over_gloo(gpu, tmp_path, nproc):
     assert out["region_voxels"] == 2197899 and out["image_sum"] == 127183
 
 
-@pytest.mark.parametrize("world,fuse", [(2, 6), (8, 6), (8, 4), (4, 8)])
-def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse):
+@pytest.mark.parametrize("world,fuse,m", [(2, 6, 1), (8, 6, 1), (8, 4, 1), (4, 8, 1), (8, 6, 2), (4, 8, 2), (8, 4, 3)])
+def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse, m):
     """Every rank of a `world`-rank row-slab stencil on one GPU: halos copied slab to slab (what the grouped RCCL
     send/recv moves), then StencilSlab.step's overlapped path itself (interior rows, then both boundary bands in
     one two-span launch) — bit-identical to the single-domain oracle. At
     world 8 a slab of a 2048-row grid is a short range, so this runs the v2 kernel's 24-rows-per-wave launch with
-    interior and edge waves."""
+    interior and edge waves. m > 1: the deep-halo schedule (edge spans reaching into the halo, extended full launches
+    at the later phases)."""
     from parallel_c_programs_amd.parallel.dist import Context
     from parallel_c_programs_amd.parallel.stencil import StencilSlab, reference_run
 
@@ -196,12 +197,15 @@ def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse):
         def distributed(self):
             return True
 
-    n, cols, steps = 2048, 1000, 2 * fuse
-    slabs = [StencilSlab(Emulated(rank=r, world=world, device=gpu), n, cols, fuse=fuse) for r in range(world)]
+    n, cols, steps = 2048, 1000, 2 * m * fuse + fuse  # (m > 1: two deep-halo periods and one exchange step)
+    slabs = [StencilSlab(Emulated(rank=r, world=world, device=gpu), n, cols, fuse=fuse, halo_mult=m)
+             for r in range(world)]
     for s in slabs:
         s._post_exchange = lambda: []
     for _ in range(steps // fuse):
-        for r, s in enumerate(slabs):  # halo exchange: T rows from each neighbour
+        for r, s in enumerate(slabs):  # halo exchange at the period's first step: m * T rows from each neighbour
+            if s.phase:
+                continue
             h = s.halo
             if r > 0:
                 s.u[0:h].copy_(slabs[r - 1].u[slabs[r - 1].rows:slabs[r - 1].rows + h])

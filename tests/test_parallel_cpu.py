@@ -193,8 +193,8 @@ def test_distributed_region_equals_serial(world):
     assert stats["outer_steps"] >= 2  # the region crosses tile borders
 
 
-def _stencil(ctx, q, n, cols, steps, overlap, fuse=1):
-    slab = StencilSlab(ctx, n, cols, fuse=fuse)
+def _stencil(ctx, q, n, cols, steps, overlap, fuse=1, halo_mult=1):
+    slab = StencilSlab(ctx, n, cols, fuse=fuse, halo_mult=halo_mult)
     slab.run(steps, overlap)
     full = slab.gather()
     if ctx.is_root:
@@ -215,6 +215,17 @@ def test_distributed_stencil_fused_steps_bit_exact(world, overlap, fuse):
     """Temporal blocking: `fuse`-row halos, one exchange per `fuse` updates, same bits as single steps."""
     n, cols, steps = 64, 48, 12
     res = _collect(world, _stencil, n, cols, steps, overlap, fuse)
+    ref = reference_run(n, steps, cols)
+    assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("world,overlap,fuse,m,steps", [(2, True, 2, 2, 12), (3, True, 2, 3, 10), (4, True, 4, 2, 16),
+                                                        (3, False, 3, 2, 9), (2, True, 4, 3, 12)])
+def test_distributed_stencil_deep_halo_bit_exact(world, overlap, fuse, m, steps):
+    """Deep halo: m*fuse halo rows exchanged every m steps, the rows next to a neighbour recomputed in between (one
+    exchange + one edge launch per m steps) — same bits as single steps, also when the run stops mid-period."""
+    n, cols = 72, 40
+    res = _collect(world, _stencil, n, cols, steps, overlap, fuse, m)
     ref = reference_run(n, steps, cols)
     assert torch.equal(torch.from_numpy(res[0]), ref.view(torch.int16))
 
