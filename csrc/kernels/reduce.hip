@@ -2,18 +2,21 @@
 // kernel and the device-side MIN flag of the distributed region growing (ref 2-mpi-region-growing/
 // region.c:435-440, MPI_Allreduce MIN) before it goes to RCCL.
 //
-// Pass 1: grid capped at 256 CUs x 8 blocks, each thread keeps UNROLL independent float4 loads in flight
+// Pass 1: grid capped at 256 CUs x 64 blocks, each thread keeps UNROLL independent float4 loads in flight
 // (non-temporal: the data is streamed once), reduces in registers, then wave64 butterfly + LDS across the
-// 4 waves. Pass 2: one block folds the <= 2048 partials in f64 (sum) in a fixed order, so the result is
-// bitwise reproducible run to run (no float atomics, cdna_hip_programming.md G12).
+// 4 waves. Pass 2: one block folds the <= 16384 partials in f64 (sum) in a fixed order, so the result is
+// bitwise reproducible run to run (no float atomics, cdna_hip_programming.md G12). Grid cap (round 4,
+// scripts/stream_bw_lab.hip, profiles/r4_bench/stream_bw_lab.txt): a 1e9-f32 read stream runs 6.70 TB/s with 2048
+// blocks of 4 float4 per lane and 7.14 TB/s with 16384 (more blocks retire and refill the CUs' queues between
+// each other's HBM round trips).
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 
 namespace {
 using pcmx::kWave;
 constexpr int kThreads = 256;
-constexpr int kUnroll = 8;  // float4 loads in flight per lane: 8 x 16 B x 256 threads = 32 KiB per block
-constexpr int kMaxBlocks = 2048;
+constexpr int kUnroll = 4;  // float4 loads in flight per lane: 4 x 16 B x 256 threads = 16 KiB per block
+constexpr int kMaxBlocks = 16384;
 
 template <class T>
 struct Vec4;
@@ -109,10 +112,24 @@ template <class T, int OP>
 __global__ __launch_bounds__(kThreads) void reduce_pass2(const T* __restrict__ partials, int np, T* __restrict__ out) {
     using W = typename std::conditional<std::is_same<T, float>::value, double, long long>::type;
     __shared__ W lds[kThreads / kWave];
-    W acc = OP == 0 ? W(0) : W(identity<T, OP>());
-    for (int i = threadIdx.x; i < np; i += kThreads) acc = comb<W, OP>(acc, (W)partials[i]);
-    acc = block_reduce<W, OP>(acc, lds);
-    if (threadIdx.x == 0) out[0] = (T)acc;
+    // 8 independent partial loads per thread in flight (up to 16384 partials: one pass of 8 x 256 strided loads per
+    // 2048, instead of a dependent load-add chain per 256); fixed assignment and fold order, so still bitwise
+    // reproducible
+    constexpr int kU = 8;
+    W acc[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) acc[u] = OP == 0 ? W(0) : W(identity<T, OP>());
+    for (int i0 = threadIdx.x; i0 < np; i0 += kThreads * kU) {
+        T v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[u] = i0 + u * kThreads < np ? partials[i0 + u * kThreads] : identity<T, OP>();
+#pragma unroll
+        for (int u = 0; u < kU; ++u) acc[u] = comb<W, OP>(acc[u], (W)v[u]);
+    }
+#pragma unroll
+    for (int u = 1; u < kU; ++u) acc[0] = comb<W, OP>(acc[0], acc[u]);
+    const W r = block_reduce<W, OP>(acc[0], lds);
+    if (threadIdx.x == 0) out[0] = (T)r;
 }
 
 inline int pass1_blocks(long long n) {

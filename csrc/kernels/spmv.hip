@@ -208,9 +208,10 @@ __device__ __forceinline__ void seg_scan_wave(float& v, int& f) {
 // stripe carries its partial sum into the next stripe). No LDS, no barriers. Otherwise: LDS scatter (ds_add_f32
 // into the item's rows, then one store per row) — measured LDS-issue bound (34% of wave cycles in
 // SQ_WAIT_INST_LDS, profiles/r2_spmv).
-template <int kMode, int kPL>
+template <int kMode, int kPL, bool kTS = false>
 __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, const Item& cur, const StreamRegs<kPL>& q,
                                             Item& nitem, StreamRegs<kPL>& nq) {
+    constexpr int kStAux = kTS ? 0 : 2;  // partial stores: temporal (kTS: may stay in L2 / MALL for the combine) or nt
     constexpr bool kPacked = (kMode & 8) != 0;
     const int lane = k.lane;
     float g[kPL];
@@ -238,7 +239,7 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
             for (int j = 0; j < kPL; ++j) acc += q.v[j] * g[j];
             acc = pcmx::wave_reduce<float, 0>(acc);
             const auto r1 = rsrc(nrows == 1 ? k.yp + cur.row0 : k.extra + it, 4u);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc), r1, lane == 0 ? 0u : 0x80000000u, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc), r1, lane == 0 ? 0u : 0x80000000u, 0, kStAux);
         } else {
             const auto ry = rsrc(k.yp + cur.row0, (unsigned)nrows * 4);
             float carry = 0.f;
@@ -259,7 +260,7 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
                 const bool tail = valid && r != rn;
                 // predicated: only a row's last lane issues its store (an out-of-range offset on the other lanes
                 // still cost them address slots: 0.706 -> 0.693 ms per product, profiles/r2_spmv/store_ab.txt)
-                if (tail) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, (unsigned)r * 4u, 0, 2);
+                if (tail) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, (unsigned)r * 4u, 0, kStAux);
                 const int r63 = __builtin_amdgcn_readlane(r, 63);
                 carry = r63 == rnext0 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)) : 0.f;
                 rprev = r63;
@@ -307,7 +308,7 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
     return more;
 }
 
-template <int kMode, int kPL>
+template <int kMode, int kPL, bool kTS = false>
 __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     const unsigned short* __restrict__ lrow, const int* __restrict__ col, const float* __restrict__ val,
     const float* __restrict__ x, int n_cols, float* __restrict__ ypart, float* __restrict__ extra,
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     Item ia = items[it], ib;
     StreamRegs<kPL> qa, qb;
     load_item_stream<kPL, (kMode & 8) != 0>(k.col, k.val, k.lrow, ia, qa, k.lane);
-    while (sliced_step<kMode, kPL>(k, it, ia, qa, ib, qb) && sliced_step<kMode, kPL>(k, it, ib, qb, ia, qa)) {
+    while (sliced_step<kMode, kPL, kTS>(k, it, ia, qa, ib, qb) && sliced_step<kMode, kPL, kTS>(k, it, ib, qb, ia, qa)) {
     }
 }
 
@@ -488,11 +489,11 @@ __device__ __forceinline__ void band_limits(int n, int a, int b, int c, int d, i
 template <int R, int NL, int U>
 __device__ __forceinline__ void banded_rows_body(const float* __restrict__ vals, const long long* __restrict__ row_off,
                                                  int n, int a, int b, int c, int d, int e, const float* __restrict__ x,
-                                                 float* __restrict__ y, float* xw) {
+                                                 float* __restrict__ y, float* xw, int r0) {
     static_assert(R <= kWave && R % 4 == 0, "rows per block");
     const int lane = pcmx::lane_id();
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
-    const int r0 = (int)blockIdx.x * R, nr = min(R, n - r0);
+    const int nr = min(R, n - r0);
     int wlo[5], wbase[5], total = 0;
     {
         int lo0[5], hi0[5], lo1[5], hi1[5];
@@ -582,36 +583,76 @@ __global__ __launch_bounds__(256) void spmv_banded_lds_kernel(const float* __res
                                                               int c, int d, int e, const float* __restrict__ x,
                                                               float* __restrict__ y) {
     extern __shared__ float xw[];
-    banded_rows_body<R, NL, U>(vals, row_off, n, a, b, c, d, e, x, y, xw);
+    banded_rows_body<R, NL, U>(vals, row_off, n, a, b, c, d, e, x, y, xw, (int)blockIdx.x * R);
 }
 
 // Variant 8 (block stream): a block of R rows reads its values — ONE contiguous CSR range — as one aligned 16-B
-// stream through a buffer descriptor over the whole value array (a float4 past the end reads 0; nothing is read
-// outside the array), instead of row by row with 4-B loads. Wave w takes the w-th quarter of the block's float4s,
-// all NV loads issued before the x windows are staged, so each lane keeps NV x 16 B in flight.
-// Valid for blocks of UNCLIPPED rows (every band inside [0, n)): all such rows have the same length L and the
-// same band layout, so element e of the block (from its first value) is row rr = floor(e / L), position
-// j = e - rr L, and its x window slot is j + rr + lut[j] (lut[j] = window base of j's band minus the band's
-// first position: the windows shift by one column per row). Blocks holding a clipped row (the first / last
-// ~(a/2 + b + c + d + e) rows) run the row-per-wave body of variant 1 instead.
-// Row sums: the 256 elements of one wave iteration span at most two rows (L >= 256, checked by the launcher);
-// lanes add their products to acc_cur (the wave's current row) or acc_next, and when the current row has ended
-// the wave reduces acc_cur into the block's row sums in LDS (ds_add_f32: a row split between two waves gets two
-// commutative adds, so the result is the same whichever lands first).
-template <int R, int NV>
-__device__ __forceinline__ void banded_stream_body(const float* __restrict__ vals, long long boff,
-                                                   int L, int r0, const int (&cum)[5], const float* __restrict__ x,
-                                                   const int (&wlo)[5], const int (&wbase)[5], int total,
-                                                   float* __restrict__ y, float* xw, int* lut, float* ysum) {
+// stream through a buffer descriptor over exactly that range's float4s, instead of row by row with 4-B loads.
+// Valid for blocks of UNCLIPPED rows (every band inside [0, n)): all such rows hold L nonzeros in the same band
+// layout, and band k's window of a block starting at row r0 begins at column r0 + delta[k], so every block's five
+// concatenated x windows have the same layout. Element e of a block (from its first value) is row rr = floor(e / L),
+// position j = e - rr L, and its x slot is s(e) = e - rr (L - 1) + lut(j), lut(j) = window base of j's band minus the
+// band's first position. Per float4 (elements e0 .. e0 + 3) ONE 16-B LDS read of lut4[j0] gives the four slot
+// offsets (lut4[j][kk] = kk + lut(j + kk), or, past the row end, kk - (L - 1) + lut(j + kk - L): the next row), so
+// the slots cost one add each and no per-element band search.
+// Row sums: one wave iteration's 256 elements span at most two rows (L >= 256, checked by the launcher); lanes add
+// their products to acc (the wave's current row `cur`) or accn, and when row cur has ended the wave sums acc on the
+// DPP path into lane 63, which adds it to the block's row sums in LDS (ds_add_f32: a row split between two waves
+// gets two commutative adds, the same result whichever lands first).
+struct BandGeo {
+    int L, W, n;     // row length, window floats per block (L + 5 (R - 1)), rows
+    int delta[5];    // window k of a block starting at row r0 begins at column r0 + delta[k]
+    int wbase[6];    // window k occupies LDS [wbase[k], wbase[k + 1])
+    int cum[5];      // first position of band k in a row
+};
+
+__device__ __forceinline__ int band_lut(const BandGeo& g, int j) {  // window base - first position of j's band
+    const int k = (j >= g.cum[1]) + (j >= g.cum[2]) + (j >= g.cum[3]) + (j >= g.cum[4]);
+    int v = g.wbase[0] - g.cum[0];
+#pragma unroll
+    for (int p = 1; p < 5; ++p)
+        if (k == p) v = g.wbase[p] - g.cum[p];
+    return v;
+}
+
+template <int R, int NV, int XW>
+__device__ __forceinline__ void banded_stream_block(const float* __restrict__ vals, long long off0, const BandGeo& g,
+                                                    int rb_begin, int sb_idx, const float* __restrict__ x,
+                                                    float* __restrict__ y, float* sm) {
+    const int L = g.L;
+    // four copies of the x windows, copy q shifted by q (xq[q][i] = window[i + q]), each 16-B aligned: the four x
+    // values of a float4 whose slots s .. s + 3 are consecutive are ONE aligned ds_read_b128 from copy s & 3
+    // (conflict-free across the wave) instead of four ds_read_b32 at a 16-B lane stride (4-way bank conflicts)
+    const int wq = 256 * XW;                                       // floats per copy (>= W + 3, checked by the launcher)
+    float* xq = sm;                                                // [4][wq]
+    float* ysum = sm + 4 * wq;                                     // [R]
+    pcmx::i32x4* lut4 = reinterpret_cast<pcmx::i32x4*>(sm + 4 * wq + ((R + 3) & ~3));  // [L + 3], 16-B aligned
     const int lane = pcmx::lane_id();
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+    const int r0 = (rb_begin + sb_idx) * R;
+    // first value of the block: unclipped rows all hold L values, so no row_off load sits before the stream loads
+    const long long boff = off0 + (long long)sb_idx * R * L;
     const long long a0 = boff & ~3LL;
     const int lead = (int)(boff - a0);
-    const int nf4 = (lead + R * L + 3) >> 2;         // float4s of the block's aligned span
-    const int q = (nf4 + 3) >> 2;                    // per wave
-    const int f0 = wave * q, f1 = min(nf4, f0 + q);  // this wave's float4s [f0, f1)
-    // descriptor over exactly the block's aligned span (vals is 16-B aligned, a0 a multiple of 4 floats; the span's
-    // last float4 ends at most 3 values past the block, inside the array: clipped rows always follow)
+    const int nf4 = (lead + R * L + 3) >> 2;           // float4s of the block's aligned span
+    const int qw = (nf4 + 3) >> 2;                     // per wave
+    const int f0 = wave * qw, f1 = min(nf4, f0 + qw);  // this wave's float4s [f0, f1)
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, g.n * 4, 0x00020000);
+    float xv[XW];  // the x windows, loaded BEFORE the value stream: the LDS writes below wait for them with vmcnt, which counts in
+                   // issue order, so they do not wait for the 40 KB of values behind them
+#pragma unroll
+    for (int t = 0; t < XW; ++t) {
+        const int i = (int)threadIdx.x + 256 * t;
+        const int k = (i >= g.wbase[1]) + (i >= g.wbase[2]) + (i >= g.wbase[3]) + (i >= g.wbase[4]);
+        int dl = g.delta[0] - g.wbase[0];
+#pragma unroll
+        for (int p = 1; p < 5; ++p)
+            if (k == p) dl = g.delta[p] - g.wbase[p];
+        const unsigned off = i < g.W ? (unsigned)(r0 + dl + i) * 4u : 0x80000000u;  // (past the windows: reads 0)
+        xv[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, 0));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // (keep every window load ahead of the value stream in issue order)
+    // the span's last float4 ends at most 3 values past the block, inside the array: clipped rows always follow
     const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vals + a0), (short)0, nf4 * 16, 0x00020000);
     pcmx::f32x4 v[NV];
 #pragma unroll
@@ -620,90 +661,112 @@ __device__ __forceinline__ void banded_stream_body(const float* __restrict__ val
         const unsigned off = f < f1 ? (unsigned)f * 16u : 0x80000000u;  // past this wave's quarter: reads 0
         v[m] = __builtin_bit_cast(pcmx::f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, off, 0, 2));
     }
-    for (int i = (int)threadIdx.x; i < total; i += 256) {
-        const int k = (i >= wbase[1]) + (i >= wbase[2]) + (i >= wbase[3]) + (i >= wbase[4]);
-        int wl = wlo[0], wb = wbase[0];
+    // (unconditional writes: slots past W land in the copy's padding, i - cq < 0 in the previous copy's padding, so
+    // no branch keeps a window load from issuing ahead of the value stream)
 #pragma unroll
-        for (int p = 1; p < 5; ++p)
-            if (k == p) wl = wlo[p], wb = wbase[p];
-        xw[i] = x[wl + i - wb];
+    for (int t = 0; t < XW; ++t) {
+        const int i = (int)threadIdx.x + 256 * t;
+#pragma unroll
+        for (int cq = 0; cq < 4; ++cq) xq[max(cq * wq + i - cq, 0)] = xv[t];
     }
-    for (int i = (int)threadIdx.x; i < L; i += 256) {  // lut[j] = window base - first position of j's band
-        const int k = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]) + (i >= cum[4]);
-        int v = wbase[0] - cum[0];
+    // lut4[j + 3] for j in [-3, L): the block's first float4 starts up to 3 values before its first element (j < 0,
+    // row 0): those (zeroed) values read slot 0
+    // stored phase-major (entry jj = j + 3 at (jj & 3) * ql + (jj >> 2)): the lanes of one row read positions 4 apart,
+    // i.e. consecutive entries of one phase table (16-B lane stride, no bank conflicts)
+    const int ql = (L + 3 + 3) >> 2;
+    for (int j = (int)threadIdx.x - 3; j < L; j += 256) {
+        pcmx::i32x4 t;
 #pragma unroll
-        for (int p = 1; p < 5; ++p)
-            if (k == p) v = wbase[p] - cum[p];
-        lut[i] = v;
+        for (int kk = 0; kk < 4; ++kk)
+            t[kk] = j + kk < 0 ? -j : j + kk < L ? kk + band_lut(g, j + kk) : kk - (L - 1) + band_lut(g, j + kk - L);
+        const int jj = j + 3;
+        lut4[(jj & 3) * ql + (jj >> 2)] = t;
     }
     if (threadIdx.x < R) ysum[threadIdx.x] = 0.f;
+    // the block's first / last value: elements before / past them in the first / last float4 are other rows' values
+    if (f0 < f1) {
+        if (f0 == 0 && lane == 0) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                if (kk < lead) v[0][kk] = 0.f;
+        }
+        const int last = nf4 - 1 - f0;  // this wave's index of the block's last float4 (if it holds it)
+        if (f1 == nf4 && (last & 63) == lane) {
+            const int tail = 4 * nf4 - lead - R * L;  // values past the block in its last float4 (0..3)
+#pragma unroll
+            for (int m = 0; m < NV; ++m)
+                if (m == (last >> 6)) {
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+                        if (kk >= 4 - tail) v[m][kk] = 0.f;
+                }
+        }
+    }
     __syncthreads();
     if (f0 < f1) {
         const float invL = 1.0f / (float)L;
-        // element index of lane 0's first element in iteration m: 4 (f0 + 64 m) - lead
-        int cur = (4 * f0 - lead) < 0 ? 0 : (4 * f0 - lead) / L;  // wave-uniform current row
+        int cur = max(0, 4 * f0 - lead) / L;  // wave-uniform current row
         float acc = 0.f, accn = 0.f;
         const int elast = min(4 * f1 - lead, R * L) - 1;  // last element of this wave
 #pragma unroll
         for (int m = 0; m < NV; ++m) {
             const int ebase = 4 * (f0 + 64 * m) - lead;  // wave-uniform
             if (ebase > elast) break;
+            const int e0 = ebase + 4 * lane;  // >= -3 (the block's first float4: its lead values are zeroed)
+            // rr0 = floor(e0 / L): (e0 + 0.5) / L is at least 0.5 / L away from an integer, far above the f32 error
+            // (e0 in [-3, 0): the product is in (-1, 0) and truncates to row 0)
+            const int rr0 = (int)__builtin_fmaf((float)e0, invL, 0.5f * invL);
+            const int j0 = e0 - rr0 * L;
+            const pcmx::i32x4 lo = lut4[((j0 + 3) & 3) * ql + ((j0 + 3) >> 2)];
+            const int sb = e0 - rr0 * (L - 1);
+            const int split = L - j0;  // elements kk >= split belong to row rr0 + 1
+            const int s0 = sb + lo[0];
+            pcmx::f32x4 xs = *reinterpret_cast<const pcmx::f32x4*>(xq + (s0 & 3) * wq + (s0 & ~3));
+            if (lo[3] - lo[0] != 3) {  // a band or row boundary inside the float4 (a few lanes per iteration)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) xs[kk] = xq[sb + lo[kk]];
+            }
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const int e = ebase + 4 * lane + kk;
-                const bool in = e >= 0 && e <= elast;
-                const int ec = in ? e : (cur * L);
-                // rr = floor(e / L): (e + 0.5) / L is at least 0.5 / L away from an integer, far above the f32 error
-                const int rr = (int)__builtin_fmaf((float)ec, invL, 0.5f * invL);
-                const int j = ec - rr * L;
-                const float p = (in ? v[m][kk] : 0.f) * xw[j + rr + lut[j]];
-                if (rr == cur) acc += p;
-                else accn += p;
+                const float p = v[m][kk] * xs[kk];
+                const bool same = (kk < split ? rr0 : rr0 + 1) == cur;
+                acc += same ? p : 0.f;
+                accn += same ? 0.f : p;
             }
             // the current row ended inside this iteration (its last element is at or below the iteration's last)
             const int eend = min(ebase + 255, elast);
             if ((cur + 1) * L - 1 <= eend) {
-                const float s = pcmx::wave_reduce<float, 0>(acc);
-                if (lane == 0) atomicAdd(&ysum[cur], s);
+                const float s = pcmx::wave_sum_to_lane63(acc);
+                if (lane == 63) atomicAdd(&ysum[cur], s);
                 acc = accn, accn = 0.f, ++cur;
             }
         }
         if (cur < R) {  // the wave's range ends inside row cur (its other part belongs to the next wave)
-            const float s = pcmx::wave_reduce<float, 0>(acc);
-            if (lane == 0) atomicAdd(&ysum[cur], s);
+            const float s = pcmx::wave_sum_to_lane63(acc);
+            if (lane == 63) atomicAdd(&ysum[cur], s);
         }
     }
     __syncthreads();
     if (threadIdx.x < R) y[r0 + threadIdx.x] = ysum[threadIdx.x];
 }
 
-// Variant 8 launch: blocks of unclipped rows stream (banded_stream_body); the others take the row-per-wave body.
-template <int R, int NV, int NL>
+// Variant 8 launch: ONE grid; its first nclip blocks take the clipped first / last row blocks (row blocks [0, nfront)
+// and [back0, ...)) with variant 1's row body, the rest stream. Dispatched first, the few clipped blocks (whose cost
+// is latency: ~10 us as a launch of their own) overlap the streaming blocks instead of adding to them.
+template <int R, int NV, int XW>
 __global__ __launch_bounds__(256) void spmv_banded_stream_kernel(const float* __restrict__ vals,
                                                                  const long long* __restrict__ row_off, int n, int a,
-                                                                 int b, int c, int d, int e, int rlo, int rhi, int L,
+                                                                 int b, int c, int d, int e, int nfront, int back0,
+                                                                 int nclip, long long off0, BandGeo g, int rb_begin,
                                                                  const float* __restrict__ x, float* __restrict__ y) {
-    extern __shared__ float xw[];
-    const int r0 = (int)blockIdx.x * R;
-    if (r0 < rlo || r0 + R > rhi) {  // a clipped row in the block: the variant-1 body (dynamic LDS sized for it)
-        banded_rows_body<R, NL, 2>(vals, row_off, n, a, b, c, d, e, x, y, xw);
+    extern __shared__ float sm[];
+    const int bid = (int)blockIdx.x;
+    if (bid < nclip) {
+        const int rb = bid < nfront ? bid : back0 + (bid - nfront);
+        banded_rows_body<R, 16, 1>(vals, row_off, n, a, b, c, d, e, x, y, sm, rb * R);
         return;
     }
-    int wlo[5], wbase[5], cum[5], total = 0, cs = 0;
-    {
-        int lo0[5], hi0[5], lo1[5], hi1[5];
-        band_limits(n, a, b, c, d, e, r0, lo0, hi0);
-        band_limits(n, a, b, c, d, e, r0 + R - 1, lo1, hi1);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            wlo[k] = lo0[k], wbase[k] = total, cum[k] = cs;
-            total += max(0, hi1[k] - lo0[k]);
-            cs += hi0[k] - lo0[k];
-        }
-    }
-    int* lut = reinterpret_cast<int*>(xw + total);
-    float* ysum = reinterpret_cast<float*>(lut + L);
-    banded_stream_body<R, NV>(vals, row_off[r0], L, r0, cum, x, wlo, wbase, total, y, xw, lut, ysum);
+    banded_stream_block<R, NV, XW>(vals, off0, g, rb_begin, bid - nclip, x, y, sm);
 }
 
 // fallback for rows longer than 16 x 64 nonzeros: one wave per row, strided band loops
@@ -774,6 +837,19 @@ extern "C" int pcmx_spmv_csr(const long long* row_ptr, const int* col, const flo
     return (int)hipGetLastError();
 }
 
+namespace {
+// temporal partial stores in the sliced product (default since round 4: the ~340 MB of compact partials are re-read
+// by the combine right after the product, and non-temporal stores evicted them early: 0.633-0.652 -> 0.628 ms per
+// step at 1e8 nnz, bit-identical; scripts/spmv_store_lab.py, profiles/r4_spmv/store_temporal_partials.txt).
+// pcmx_spmv_lab_set(0, 0) restores the nt stores.
+int g_spmv_ts = 1;
+}
+extern "C" int pcmx_spmv_lab_set(int key, int val) {
+    if (key != 0 || val < 0 || val > 1) return -1;
+    g_spmv_ts = val;
+    return 0;
+}
+
 extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x,
                                 float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
                                 const long long* slice_nz0, const long long* slice_item0, const long long* slice_out0,
@@ -812,12 +888,15 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
 #define PCMX_SLICED(M, PL) spmv_sliced_kernel<M, PL><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp)
         // slice_colbase != NULL: col holds the packed words (production layout when every slice is < 2^21 columns)
         if (slice_colbase) {
+            // lab knob (pcmx_spmv_lab_set(0, 1)): temporal partial stores
+#define PCMX_SLICED_TS(M, PL) spmv_sliced_kernel<M, PL, true><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp)
             if ((mode & 7) == 2)
-                PCMX_SLICED(12, 8);
+                (g_spmv_ts ? PCMX_SLICED_TS(12, 8) : PCMX_SLICED(12, 8));
             else if ((mode & 7) == 0)
-                PCMX_SLICED(12, 16);
+                (g_spmv_ts ? PCMX_SLICED_TS(12, 16) : PCMX_SLICED(12, 16));
             else
                 return (int)hipErrorInvalidValue;  // the lab modes read the unpacked layout
+#undef PCMX_SLICED_TS
         } else switch (mode & 7) {
             case 0: PCMX_SLICED(4, 16); break;
             case 1: PCMX_SLICED(5, 16); break;
@@ -853,6 +932,68 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
     return (int)hipGetLastError();
 }
 
+namespace {
+// host twin of band_limits (the launcher derives variant 8's window geometry from one unclipped row)
+void band_limits_host(int n, int a, int b, int c, int d, int e, int row, int (&lo)[5], int (&hi)[5]) {
+    const int ah = a / 2;
+    const int r5 = ah, r6 = ah + b, r7 = ah + b + c, r8 = ah + b + c + d, r9 = ah + b + c + d + e;
+    lo[0] = std::max(0, row - r9), hi[0] = std::max(0, row - r8);
+    lo[1] = std::max(0, row - r7), hi[1] = std::max(0, row - r6);
+    lo[2] = std::max(0, row - r5), hi[2] = std::min(row + r5 + 1, n);
+    lo[3] = std::min(n, row + r6 + 1), hi[3] = std::min(n, row + r7 + 1);
+    lo[4] = std::min(n, row + r8 + 1), hi[4] = std::min(n, row + r9 + 1);
+    for (int k = 0; k < 5; ++k) hi[k] = std::max(hi[k], lo[k]);
+}
+}  // namespace
+
+namespace {
+constexpr int kStreamNotApplicable = -1000;
+// Variant 8/9 launch (block stream over the unclipped rows, the clipped row blocks folded into the same grid);
+// kStreamNotApplicable when the band geometry or the value alignment rules it out.
+template <int RS, int NV, int XW>
+int launch_banded_stream(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
+                         const float* x, float* y, hipStream_t s) {
+    // rows [rlo, rhi) are unclipped (every band inside [0, n)) and all hold L nonzeros
+    const int ah = a / 2, r9 = ah + b + c + d + e;
+    const int L = 2 * ah + 1 + 2 * c + 2 * e;
+    const long long maxrow = L;
+    const int rlo = r9, rhi = n - r9;
+    const int rb_lo = (rlo + RS - 1) / RS, rb_hi = rhi >= 0 ? rhi / RS : 0, nrb = (n + RS - 1) / RS;
+    const long long q = ((long long)L * RS + 6) / 16;  // float4s per wave quarter (lead <= 3)
+    const int W = L + 5 * (RS - 1);
+    const size_t lds_rows = (size_t)(maxrow + 5 * (RS - 1)) * sizeof(float);  // the clipped blocks' row body
+    const size_t lds8 = (size_t)(4 * 256 * XW + ((RS + 3) & ~3) + 16 * ((L + 6) / 4)) * sizeof(float);
+    // the wave-iteration rule needs rows of >= 256 nonzeros, the float4 stream a 16-B aligned vals; the register
+    // sets hold NV float4s per lane and XW window floats per thread; the clipped body NL = 16 chunks of 64
+    const bool ok = L >= 256 && L <= 16 * 64 && q <= 64 * NV && W + 3 <= XW * 256 && rb_hi > rb_lo &&
+                    !((uintptr_t)vals & 15) && lds_rows <= 64 * 1024 && lds8 <= 64 * 1024;
+    if (!ok) return kStreamNotApplicable;
+    BandGeo g{};
+    g.L = L, g.W = W, g.n = n;
+    {
+        int lo[5], hi[5], wb = 0, cs = 0;
+        band_limits_host(n, a, b, c, d, e, rlo, lo, hi);
+        for (int k = 0; k < 5; ++k) {
+            g.delta[k] = lo[k] - rlo, g.wbase[k] = wb, g.cum[k] = cs;
+            wb += hi[k] - lo[k] + RS - 1;
+            cs += hi[k] - lo[k];
+        }
+        g.wbase[5] = wb;
+    }
+    const int nfront = rb_lo, back0 = rb_hi, nback = nrb - rb_hi;
+    // first value of row rb_lo * RS: the nonzeros of the clipped rows before it (host sum of row lengths)
+    long long off0 = 0;
+    for (int r = 0; r < rb_lo * RS; ++r) {
+        int lo[5], hi[5];
+        band_limits_host(n, a, b, c, d, e, r, lo, hi);
+        for (int k = 0; k < 5; ++k) off0 += hi[k] - lo[k];
+    }
+    spmv_banded_stream_kernel<RS, NV, XW><<<nfront + nback + rb_hi - rb_lo, 256, std::max(lds_rows, lds8), s>>>(
+        vals, row_off, n, a, b, c, d, e, nfront, back0, nfront + nback, off0, g, rb_lo, x, y);
+    return (int)hipGetLastError();
+}
+}  // namespace
+
 extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_off, int n, int a, int b, int c, int d,
                                         int e, const float* x, float* y, int variant, hipStream_t s);
 extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_off, int n, int a, int b, int c, int d,
@@ -871,31 +1012,13 @@ extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_
         return (int)hipGetLastError();
     }
     const int grid = (n + R - 1) / R;
-    if (variant == 8) {
-        // rows [rlo, rhi) are unclipped (every band inside [0, n)) and all hold L nonzeros; a block of RS rows
-        // streams when all its rows are unclipped, and its wave quarters need NV float4 loads per lane
-        constexpr int RS = 16;
-        const long long ah = a / 2, r9 = ah + b + c + d + e;
-        const long long L = 2 * ah + 1 + 2LL * c + 2LL * e;
-        const long long rlo = r9, rhi = (long long)n - r9;
-        const long long q = ((L * RS + 3 + 3) / 4 + 3) / 4;  // float4s per wave quarter (lead <= 3)
-        const long long nv = (q + 63) / 64;
-        // the wave-iteration rule needs rows of >= 256 nonzeros, the float4 stream a 16-B aligned vals; otherwise
-        // (or when the LDS windows do not fit) the variant-1 kernel runs
-        const size_t lds8 = (size_t)(maxrow + 5 * (RS - 1) + L + RS) * sizeof(float);
-        const bool ok = L >= 256 && nv <= 12 && rhi - rlo >= RS && !((uintptr_t)vals & 15) && lds8 <= 64 * 1024;
-        if (!ok) return pcmx_spmv_banded_variant(vals, row_off, n, a, b, c, d, e, x, y, 1, s);
-        const int g8 = (n + RS - 1) / RS;
-#define PCMX_STREAM(NV)                                                                                               \
-    spmv_banded_stream_kernel<RS, NV, 16><<<g8, 256, lds8, s>>>(vals, row_off, n, a, b, c, d, e, (int)rlo, (int)rhi, \
-                                                                 (int)L, x, y)
-        if (nv <= 4) PCMX_STREAM(4);
-        else if (nv <= 6) PCMX_STREAM(6);
-        else if (nv <= 8) PCMX_STREAM(8);
-        else if (nv <= 10) PCMX_STREAM(10);
-        else PCMX_STREAM(12);
-#undef PCMX_STREAM
-        return (int)hipGetLastError();
+    if (variant == 8 || variant == 9) {
+        // 8: 16-row blocks (production), 9: 32-row blocks (lab: the per-block setup — x windows, slot table,
+        // barrier — amortised over twice the values, at 2x the value registers)
+        const int rc = variant == 8 ? launch_banded_stream<16, 10, 3>(vals, row_off, n, a, b, c, d, e, x, y, s)
+                                    : launch_banded_stream<32, 20, 4>(vals, row_off, n, a, b, c, d, e, x, y, s);
+        if (rc == kStreamNotApplicable) return pcmx_spmv_banded_variant(vals, row_off, n, a, b, c, d, e, x, y, 1, s);
+        return rc;
     }
 #define PCMX_BANDED(RR, UU)                                                                                            \
     do {                                                                                                               \

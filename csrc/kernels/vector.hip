@@ -3,7 +3,9 @@
 //
 // MI355X design: 16-B (f32x4) accesses per lane so one wave instruction moves 1 KiB, 4 independent
 // f32x4 per lane per iteration to keep enough bytes in flight, non-temporal hints on streamed-once
-// data, grid capped at 256 CUs x 8 blocks with a grid-stride loop (cdna_hip_programming.md G11/G13).
+// data, grid capped at 256 CUs x 64 blocks with a grid-stride loop (cdna_hip_programming.md G11/G13; the write side
+// of an HBM stream tops out near 5.5 TB/s on MI355X: vadd 1e9 2.18 ms = 5.5 TB/s, fill 5.6, against 7.1 for a
+// read-only stream, profiles/r4_bench/stream_bw_lab.txt).
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 

@@ -50,6 +50,23 @@ __device__ __forceinline__ T wave_reduce(T v) {
     return v;
 }
 
+// Sum over the 64 lanes on the DPP path (no LDS round trip): quad swaps and row rotations leave every lane of a
+// 16-lane row holding its row sum, then row_bcast:15 / row_bcast:31 fold the rows upward. The total is in lane 63
+// (other lanes hold partial sums).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, kRowMask, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum_to_lane63(float v) {
+    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x124, 0xf>(v);  // row_ror:4
+    v = dpp_add<0x128, 0xf>(v);  // row_ror:8
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return v;
+}
+
 // Whole-wave lane shifts on the DPP path (GFX9 wave_shr:1 / wave_shl:1): a VALU modifier, no LDS round trip
 // like __shfl_up/__shfl_down (ds_bpermute). wave_from_prev: lane l gets lane l-1's value; wave_from_next: lane
 // l gets lane l+1's value. The end lane (0 / 63) receives 0.
@@ -79,6 +96,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
-inline int grid_cap_streaming() { return 256 * 8; }  // 256 CUs x 8 blocks: cap, then grid-stride
+// Streaming grid cap (256 CUs x 64 blocks, then grid-stride): at 1e9 f32 a 16384-block grid streams 5.5 TB/s for
+// vadd / copy / fill against 4.8-5.1 with 2048 (scripts/stream_bw_lab.hip, profiles/r4_bench/stream_bw_lab.txt)
+inline int grid_cap_streaming() { return 256 * 64; }
 
 }  // namespace pcmx

@@ -19,7 +19,7 @@ y_ref = ops.spmv(m, x)
 vals, ro, xg = m.val.cuda(), m.row_ptr.cuda(), x.cuda()
 scrub = torch.rand(256 << 20, device="cuda")  # 1 GiB, READ between cold calls (no dirty lines)
 bytes_ = m.nnz * 4 + dims[0] * 8
-for v in [int(a) for a in sys.argv[7].split(',')] if len(sys.argv) > 7 else (1, 8):
+for v in [int(a) for a in sys.argv[7].split(",")] if len(sys.argv) > 7 else (1, 8):  # variants, e.g. "1,8"
     fn = lambda: ops.spmv_banded(vals, ro, *dims, xg, variant=v)  # noqa: E731
     y = fn().cpu()
     ms = device_time_ms(fn, reps=20)
