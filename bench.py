@@ -394,7 +394,8 @@ def main(argv=None):
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
                     "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks,
-                    "spmv_slices": sp.d.slices, "spmv_exchange": sp.d.exchange if ctx.distributed else None})
+                    "spmv_slices": sp.d.slices, "spmv_exchange": sp.d.exchange if ctx.distributed else None,
+                    "spmv_colsplit": sp.d.colsplit})
         device_times(chk, "spmv", ms)
         if vendor:  # hipSPARSE (torch sparse CSR x dense vector) on each rank's own rows, the same matrix and x
             try:

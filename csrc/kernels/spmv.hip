@@ -312,11 +312,11 @@ template <int kMode, int kPL, bool kTS = false>
 __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     const unsigned short* __restrict__ lrow, const int* __restrict__ col, const float* __restrict__ val,
     const float* __restrict__ x, int n_cols, float* __restrict__ ypart, float* __restrict__ extra,
-    const Item* __restrict__ items, SliceMeta meta, int blocks_per_slice) {
+    const Item* __restrict__ items, SliceMeta meta, int blocks_per_slice, int phase_lo) {
     __shared__ float yl[kWavesPerBlock][kItemRows + 1];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int b = blockIdx.x;
-    const int phase = b / (8 * blocks_per_slice);
+    const int phase = phase_lo + b / (8 * blocks_per_slice);
     const int s = phase * 8 + (b & 7);
     SlicedCtx k;
     k.i1 = meta.item0[s + 1];
@@ -857,7 +857,11 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
                                 int n_fix, int mode, const int* slice_colbase, hipStream_t s) {
     if (n_rows <= 0) return 0;
     if (n_slices <= 0 || n_slices % 8 || n_slices > kMaxSlices) return (int)hipErrorInvalidValue;
-    const int persist_blocks = (mode >> 8) ? (mode >> 8) : kPersistBlocks;
+    const int persist_blocks = (mode >> 8) & 0xff ? (mode >> 8) & 0xff : kPersistBlocks;
+    // bits 16-20 / 21-25: the product launch covers phases [ph_lo, ph_lo + ph_n) (8 slices, one per XCD, per phase;
+    // ph_n = 0: all): a column-split caller multiplies the slices of the columns it already holds first
+    const int ph_all = n_slices / 8, ph_lo = (mode >> 16) & 31, ph_n = (mode >> 21) & 31 ? (mode >> 21) & 31 : ph_all - ph_lo;
+    if (ph_lo + ph_n > ph_all || ph_n <= 0) return (int)hipErrorInvalidValue;
     SliceMeta meta{};
     SliceOut so{};
     long long most = 0;
@@ -866,7 +870,8 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         meta.item0[k] = slice_item0[k];
         meta.out0[k] = so.out0[k] = slice_out0[k];
         if (slice_item0[k + 1] < slice_item0[k]) return (int)hipErrorInvalidValue;
-        most = slice_item0[k + 1] - slice_item0[k] > most ? slice_item0[k + 1] - slice_item0[k] : most;
+        if (k >= 8 * ph_lo && k < 8 * (ph_lo + ph_n))
+            most = slice_item0[k + 1] - slice_item0[k] > most ? slice_item0[k + 1] - slice_item0[k] : most;
     }
     meta.item0[n_slices] = slice_item0[n_slices];
     for (int k = 0; k < n_slices; ++k) meta.colbase[k] = slice_colbase ? slice_colbase[k] : 0;
@@ -881,15 +886,15 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         const long long need = (most + kWavesPerBlock - 1) / kWavesPerBlock;
         const long long per = (long long)(cus / 8) * persist_blocks;  // resident blocks per XCD
         const int bp = (int)(need < per ? need : per);
-        const unsigned nb = (unsigned)(bp * n_slices);
+        const unsigned nb = (unsigned)(bp * 8 * ph_n);
         const Item* it = reinterpret_cast<const Item*>(items);
         const dim3 blk(kWavesPerBlock * kWave);
         // bit 0: skip the x gathers (lab), bit 1: items of 512 nonzeros (8 per lane), bit 2: LDS row sums (lab)
-#define PCMX_SLICED(M, PL) spmv_sliced_kernel<M, PL><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp)
+#define PCMX_SLICED(M, PL) spmv_sliced_kernel<M, PL><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp, ph_lo)
         // slice_colbase != NULL: col holds the packed words (production layout when every slice is < 2^21 columns)
         if (slice_colbase) {
             // lab knob (pcmx_spmv_lab_set(0, 1)): temporal partial stores
-#define PCMX_SLICED_TS(M, PL) spmv_sliced_kernel<M, PL, true><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp)
+#define PCMX_SLICED_TS(M, PL) spmv_sliced_kernel<M, PL, true><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp, ph_lo)
             if ((mode & 7) == 2)
                 (g_spmv_ts ? PCMX_SLICED_TS(12, 8) : PCMX_SLICED(12, 8));
             else if ((mode & 7) == 0)

@@ -238,23 +238,25 @@ class SpMV(Workload):
     layout with exchange="allgather"). Strong scaling: one fixed matrix."""
 
     def __init__(self, ctx, n_rows=10_000_000, nnz=100_000_000, alpha=2.5, slices=-1, head=0.0625,
-                 balance=0.0, chunks=0, exchange="ghost", keep_plain=False, **_):
+                 balance=0.0, chunks=0, exchange="ghost", keep_plain=False, colsplit=None, **_):
         from ..parallel.spmv import DistributedSpMV
 
         slices = int(slices) if ctx.device.type == "cuda" else 0
         self.d = DistributedSpMV.powerlaw(ctx, n_rows, nnz, alpha, slices=slices, head=float(head),
                                           balance=float(balance), chunks=int(chunks) or None, exchange=exchange,
-                                          keep_plain=keep_plain)
+                                          keep_plain=keep_plain, colsplit=colsplit)
         slices = self.d.slices
         super().__init__(ctx, {"n_rows": n_rows, "nnz": nnz, "slices": slices, "head": head,
-                               "chunks": self.d.chunks}, "spmv", "GFLOP/s")
+                               "chunks": self.d.chunks, "colsplit": self.d.colsplit}, "spmv", "GFLOP/s")
         x = ops.rand_uniform_(torch.empty(n_rows, device=ctx.device), 5, 0.0, 1.0)
         self.xp = self.d.to_padded(x)
         del x
         self.y = None
 
     def step(self):
-        self.y = self.d.step_padded(self.xp)
+        # the column-split pipeline: each step's last exchange overlaps the next step's first products (the next step
+        # waits for it before the products that read those columns); check() finishes it
+        self.y = self.d.step_padded(self.xp, defer_exchange=True)
 
     def check(self, reduce: bool = True):
         """Every entry of the timed step's output layout (own rows AND the ghost entries the exchange wrote) against

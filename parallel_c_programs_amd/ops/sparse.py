@@ -71,7 +71,7 @@ class SlicedCSR:
     """
 
     def __init__(self, m: CSR, n_slices: int = 16, head: float = 0.0625, balance: float = 0.0, item_nnz: int = 1024,
-                 pack: bool = True):
+                 pack: bool = True, col_split: int = 0):
         from .. import _C  # noqa: F401  (pybind module carries the planner)
 
         if n_slices % 8 or not 8 <= n_slices <= 32:
@@ -87,14 +87,26 @@ class SlicedCSR:
         hist = torch.bincount(col, minlength=m.n_cols).double()
         H = int(torch.searchsorted(hist.cumsum(0), torch.tensor([head * nnz], device=dev, dtype=torch.float64))) \
             if head > 0 else 0
-        self.head_cols = H
+        if col_split:  # column split: slices 0 .. S/2-1 cover columns [0, col_split), the others [col_split, n_cols)
+            if S % 16 or not 0 < col_split < m.n_cols:
+                raise ValueError("col_split needs 16 or 32 slices and 0 < col_split < n_cols")
+            H = min(H, col_split)
+        self.head_cols, self.col_split = H, int(col_split)
         # slice bounds over the tail: equal quantiles of a per-column cost = nnz in the column + balance * mean
         # nnz per column (balance 0: equal nnz per slice, the measured best)
         w = hist + balance * nnz / max(1, m.n_cols)
         w[:H] = 0
         cum = w.cumsum(0)
-        tgt = torch.arange(1, S, device=dev, dtype=torch.float64) * (float(cum[-1]) / S)
-        bounds = torch.searchsorted(cum, tgt, right=True).to(torch.int32)
+        if col_split:
+            S2, B = S // 2, int(col_split)
+            t0, tot = float(cum[B - 1]), float(cum[-1])
+            g = torch.arange(1, S2, device=dev, dtype=torch.float64)
+            b0 = torch.searchsorted(cum, g * (t0 / S2), right=True).clamp(max=B)
+            b1 = torch.searchsorted(cum, t0 + g * ((tot - t0) / S2), right=True).clamp(min=B)
+            bounds = torch.cat([b0, torch.tensor([B], device=dev), b1]).to(torch.int32)
+        else:
+            tgt = torch.arange(1, S, device=dev, dtype=torch.float64) * (float(cum[-1]) / S)
+            bounds = torch.searchsorted(cum, tgt, right=True).to(torch.int32)
         self.bounds = bounds.cpu()
         sid = torch.bucketize(col, bounds, right=True)  # slice of every nonzero (int64)
         deg = (m.row_ptr[1:] - m.row_ptr[:-1]).to(dev)
@@ -187,9 +199,17 @@ class SlicedCSR:
         """Compact partials per product (touched (row, slice) pairs)."""
         return int(self.meta[-1])
 
-    def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None, mode: int = 0) -> torch.Tensor:
+    def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None, mode: int = 0,
+             phases: tuple[int, int] | None = None) -> torch.Tensor:
         """y = A x; `out` (contiguous f32, >= n_rows elements) receives y in place when given. mode bit 4: products
-        only (compact partials, no combine), bit 5: combine + fix-up only (of the partials a bit-4 call wrote)."""
+        only (compact partials, no combine), bit 5: combine + fix-up only (of the partials a bit-4 call wrote).
+        phases=(lo, n): the products of slices [8 lo, 8 (lo + n)) only (one slice per XCD per phase) — with col_split,
+        phases (0, S/16) multiply the columns below the split and (S/16, S/16) the others."""
+        if phases is not None:
+            lo, n = phases
+            if not (0 <= lo and 0 < n and lo + n <= self.n_slices // 8):
+                raise ValueError(f"phases {phases} outside the {self.n_slices // 8} phases")
+            mode |= (lo << 16) | (n << 21)
         if self.cr is not None and (mode & 0x8F) == 0:  # production: packed index stream (bit 6: ballot combine, 8+: resident blocks)
             if getattr(self, "_meta_packed", None) is None:
                 self._meta_packed = torch.cat([self.meta, torch.tensor(self.colbase, dtype=torch.int64)]).contiguous()

@@ -20,6 +20,10 @@ CSR benchmark of ref 3-serial-optimization/spmv.c:170-177, 331-367).
     ONE contiguous all_gather_into_tensor region written straight into the next x.
   * overlap (both): chunk c's exchange is issued async (RCCL's own stream waits only for chunk c's kernel)
     while chunk c+1 is multiplied, so only the last chunk's exchange is exposed (docs/ARCHITECTURE.md, SpMV).
+  * column split (ghost layout, 2 chunks, N > 1; round 4): every product is also cut at the first layout column of
+    chunk 1, and a step multiplies the chunk-0 columns of both row chunks first, waits for the previous step's
+    chunk-1 exchange only then, and leaves its own chunk-1 exchange in flight for the next step: in steady state no
+    exchange is exposed, at the cost of 4 product launches per step instead of 2 (_step_colsplit).
 """
 from __future__ import annotations
 
@@ -61,10 +65,58 @@ def auto_slices(n_cols: int) -> int:
     return int(min(32, max(8, 8 * round(n_cols / 400_000 / 8))))
 
 
+class ColSplitCSR:
+    """A row block split at layout column B into the CSR of its columns < B and of the rest (the column-split schedule
+    on the plain CSR path: CPU / gloo tests and GPUs without slices): product_phase(x, 0) multiplies the first,
+    product_phase(x, 1, dst) adds the second (same fp32 sum on every path: (A0 x) + (A1 x))."""
+
+    def __init__(self, m: CSR, B: int):
+        self.n_rows, self.nnz = m.n_rows, m.nnz
+        self.parts = []
+        rows = torch.repeat_interleave(torch.arange(m.n_rows, device=m.col.device), m.row_ptr[1:] - m.row_ptr[:-1])
+        for keep in (m.col < B, m.col >= B):
+            cnt = torch.bincount(rows[keep], minlength=m.n_rows)
+            rp = torch.zeros(m.n_rows + 1, dtype=torch.int64, device=m.col.device)
+            rp[1:] = cnt.cumsum(0)
+            part = CSR(rp, m.col[keep].contiguous(), m.val[keep].contiguous(), m.n_cols)
+            self.parts.append(part.plan() if part.val.is_cuda else part)
+        self.tmp = {}
+
+    def product_phase(self, x: torch.Tensor, phase: int, key=0, dst: torch.Tensor | None = None) -> None:
+        if phase == 0:
+            self.tmp[key] = spmv(self.parts[0], x)
+        else:
+            dst.copy_(self.tmp.pop(key) + spmv(self.parts[1], x))
+
+    def product(self, x: torch.Tensor) -> torch.Tensor:
+        return spmv(self.parts[0], x) + spmv(self.parts[1], x)
+
+    def reference(self, x: torch.Tensor) -> torch.Tensor:
+        y = torch.zeros(self.n_rows, dtype=torch.float64, device=x.device)
+        for p in self.parts:
+            rows = torch.repeat_interleave(torch.arange(p.n_rows, device=x.device), (p.row_ptr[1:] - p.row_ptr[:-1]).to(x.device))
+            y.index_add_(0, rows, p.val.double().to(x.device) * x.double()[p.col.long().to(x.device)])
+        return y
+
+
+def _sliced_product_phase(self: SlicedCSR, x: torch.Tensor, phase: int, key=0, dst: torch.Tensor | None = None) -> None:
+    """Column-split product of a SlicedCSR: phase 0 = the products of the slices below the split (partials only),
+    phase 1 = the products of the others, then the combine + fix-up into dst."""
+    half = self.n_slices // 16
+    if phase == 0:
+        self.spmv(x, mode=16, phases=(0, half))
+    else:
+        self.spmv(x, mode=16, phases=(half, half))
+        self.spmv(x, dst, mode=32)
+
+
+SlicedCSR.product_phase = _sliced_product_phase
+
+
 class DistributedSpMV:
     def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
                  head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 0,
-                 exchange: str = "ghost", keep_plain: bool = False):
+                 exchange: str = "ghost", keep_plain: bool = False, colsplit: bool | None = None):
         W, dev = ctx.world, ctx.device
         if exchange not in ("ghost", "allgather"):
             raise ValueError("exchange: 'ghost' or 'allgather'")
@@ -96,15 +148,30 @@ class DistributedSpMV:
         self.plain = m if keep_plain else None
         if slices < 0:
             slices = auto_slices(self.n_pad)
+        # column split (2 chunks, ghost layout, N > 1): every product is cut at B = the first layout column of chunk
+        # 1, so the next step multiplies the chunk-0 columns (their exchange overlapped this step's chunk-1 product)
+        # while the chunk-1 exchange is still in flight, and only then the chunk-1 columns (see step_padded)
+        B = self.ghost0[1] if self.exchange == "ghost" and C == 2 else 0
+        if colsplit is None:
+            colsplit = ctx.distributed and 0 < B < self.n_pad
+        self.colsplit = bool(colsplit) and 0 < B < self.n_pad
+        self.col_split = B if self.colsplit else 0
+        if self.colsplit and slices:
+            slices = max(16, 16 * round(slices / 16))  # 8-slice phases on each side of the split
         self.slices = slices
         self.sliced = bool(slices) and dev.type == "cuda"
-        self.parts = []  # (first local row, last local row + 1, CSR or SlicedCSR)
+        self.parts = []  # (first local row, last local row + 1, CSR, SlicedCSR or ColSplitCSR)
         for c in range(C):
             a, b = min(c * self.L, self.rows), min((c + 1) * self.L, self.rows)
             part = m.row_block(a, b)
-            if dev.type == "cuda":
-                part = SlicedCSR(part, slices, head, balance, item_nnz) if self.sliced else part.plan()
+            if self.sliced:
+                part = SlicedCSR(part, slices, head, balance, item_nnz, col_split=self.col_split)
+            elif self.colsplit:
+                part = ColSplitCSR(part, self.col_split)
+            elif dev.type == "cuda":
+                part = part.plan()
             self.parts.append((a, b, part))
+        self._pending = [[], []]  # column split: the exchange works of the previous step's chunks 0 and 1
         del col
         if not keep_plain:
             del m
@@ -180,11 +247,12 @@ class DistributedSpMV:
     def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
                  slices: int = 0, head: float = 0.0625, balance: float = 0.0,
                  chunks: int | None = None, item_nnz: int = 0, exchange: str = "ghost",
-                 keep_plain: bool = False) -> "DistributedSpMV":
+                 keep_plain: bool = False, colsplit: bool | None = None) -> "DistributedSpMV":
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)
-        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz, exchange, keep_plain)
+        return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz, exchange, keep_plain,
+                               colsplit)
 
     def vendor_matrix(self) -> torch.Tensor:
         """This rank's rows as a torch sparse CSR tensor (layout columns): `torch.mv(A, xp)` runs hipSPARSE."""
@@ -249,6 +317,8 @@ class DistributedSpMV:
     def _mul(self, part, xp: torch.Tensor, dst: torch.Tensor) -> None:
         if self.sliced:
             part.spmv(xp, dst)
+        elif isinstance(part, ColSplitCSR):
+            dst.copy_(part.product(xp))
         else:
             dst.copy_(spmv(part, xp))
 
@@ -270,10 +340,50 @@ class DistributedSpMV:
             outs.append(out[s0:s0 + (0 if q == r else self.recv_counts[c][q])])
         return self.ctx.exchange(outs, ins, async_op=True)
 
-    def step_padded(self, xp: torch.Tensor) -> torch.Tensor:
+    def _wait(self, k: int) -> None:
+        for w in self._pending[k]:
+            w.wait()
+        self._pending[k] = []
+
+    def finish(self) -> None:
+        """Waits for the exchanges a column-split step left in flight (the next step waits for them itself; call this
+        before reading the layout vector a step returned)."""
+        self._wait(0)
+        self._wait(1)
+
+    def _step_colsplit(self, xp: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Column-split schedule (2 chunks): products over the chunk-0 columns of xp (their exchange was posted
+        mid-way through the previous step) for both row chunks, then — once the previous step's chunk-1 exchange has
+        landed — the chunk-1 columns, the combine of row chunk c and the post of its exchange. Nothing waits at the
+        end of the step: the chunk-1 exchange overlaps the next step's chunk-0-column products, so in steady state
+        no exchange is exposed (4 product launches per step instead of 2)."""
+        W, r = self.ctx.world, self.ctx.rank
+        self._wait(0)
+        for c, (a, b, part) in enumerate(self.parts):
+            if b > a:
+                part.product_phase(xp, 0, c)
+        self._wait(1)
+        pending = [[], []]
+        for c, (a, b, part) in enumerate(self.parts):
+            s0 = self.seg[c * W + r]
+            if b > a:
+                part.product_phase(xp, 1, c, out[s0:s0 + (b - a)])
+            pending[c] = self._post_chunk(out, c)
+        self._pending = pending
+        return out
+
+    def step_padded(self, xp: torch.Tensor, defer_exchange: bool = False) -> torch.Tensor:
         """xp (this rank's layout) -> A xp in the same layout (own rows + every ghost the next product reads).
-        The result lives in one of two internal buffers; the buffer that is not `xp` is overwritten."""
+        The result lives in one of two internal buffers; the buffer that is not `xp` is overwritten.
+        defer_exchange (column split): return with the last chunk's exchange still in flight — the next step waits
+        for it before the products that read those columns (an iterating caller: the steady-state pipeline); call
+        finish() before reading the result yourself."""
         out = self.bufs[0] if xp.data_ptr() != self.bufs[0].data_ptr() else self.bufs[1]
+        if self.colsplit and self.ctx.distributed:
+            self._step_colsplit(xp, out)
+            if not defer_exchange:
+                self.finish()
+            return out
         W, L, works = self.ctx.world, self.L, []
         for c, (a, b, part) in enumerate(self.parts):
             if self.exchange == "allgather":
@@ -295,13 +405,17 @@ class DistributedSpMV:
 
     def step(self, x: torch.Tensor) -> torch.Tensor:
         """x (full, natural order, replicated) -> A x (full, natural order, replicated)."""
-        return self.from_padded(self.step_padded(self.to_padded(x)))
+        y = self.step_padded(self.to_padded(x))
+        self.finish()
+        return self.from_padded(y)
 
     def reference_local(self, xp: torch.Tensor) -> torch.Tensor:
         """fp64 product of this rank's rows with xp (its layout), in local row order."""
         outs = []
         for a, b, part in self.parts:
-            if isinstance(part, SlicedCSR):
+            if isinstance(part, ColSplitCSR):
+                outs.append(part.reference(xp))
+            elif isinstance(part, SlicedCSR):
                 outs.append(part.reference(xp))
             else:
                 rows = torch.repeat_interleave(torch.arange(part.n_rows, device=xp.device),
@@ -316,6 +430,7 @@ class DistributedSpMV:
         entries the exchange delivered (each compared with its owner's fp64 row, gathered once), i.e. the
         product and the exchange that the timed step performs. Same value on every rank (reduce=False: this
         rank's entries only, no collective after the all-gather of the fp64 rows)."""
+        self.finish()
         ref = self.reference_local(xp)
         if self.ctx.distributed:
             buf = torch.zeros(self.block, dtype=torch.float64, device=ref.device)

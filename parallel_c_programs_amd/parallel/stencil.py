@@ -39,9 +39,12 @@ def auto_fuse(slab_rows: int) -> int:
 
 
 def auto_halo_mult(slab_rows: int, fuse: int, world: int) -> int:
-    """Halo depth in units of `fuse` rows (the deep-halo schedule, see StencilSlab): 2 for a distributed slab (one
-    exchange + one edge launch per 2 fused launches), 1 on one rank (no halo)."""
-    return 2 if world > 1 and fuse > 1 and slab_rows >= 4 * 2 * fuse else 1
+    """Halo depth in units of `fuse` rows (the deep-halo schedule, see StencilSlab): 2 on short distributed slabs, 1
+    otherwise. Measured per step of one interior rank (scripts/stencil_rank_lab.py, profiles/r4_stencil/
+    rank_lab_deep_halo.txt, T = 6): 2048 rows (N = 8) interior + edge launch 0.0603 ms -> deep halo 0.0550 ms (the
+    single full launch: 0.0539); 4096 rows (N = 4) 0.0926 -> 0.0980 and 8192 rows 0.163 -> 0.175 (taller slabs lose:
+    their two-launch step hides the edge launch better than the extended launches cost)."""
+    return 2 if world > 1 and fuse > 1 and 8 * fuse <= slab_rows <= 3072 else 1
 
 
 class StencilSlab:

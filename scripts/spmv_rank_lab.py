@@ -4,8 +4,8 @@ N = 2 / 4 / 8 on one GPU (ranks emulated one at a time, no exchange), for both v
   ghost      compact local vector: own rows + only the x entries the rank's nonzeros reference
   allgather  padded replicated vector (every row of y on every rank)
 
-Prints the product time (4 pipeline chunks, as the bench runs N > 1), the layout length and the exchange
-volume per step: bytes this rank receives (ghost: its ghosts; allgather: every other rank's rows).
+Prints the product time (the chunk / column-split schedules the bench can run at N > 1), the layout length and the
+exchange volume per step: bytes this rank receives (ghost: its ghosts; allgather: every other rank's rows).
 Run: python scripts/spmv_rank_lab.py [world ...]
 """
 import os
@@ -37,16 +37,23 @@ def main():
     n, nnz = 10_000_000, 100_000_000
     for W in worlds:
         for r in sorted({0, W - 1}):
-            for ex, C, item, S in (("ghost", 2, 512, 24), ("ghost", 2, 512, 16), ("ghost", 1, 512, 24),
-                                   ("ghost", 2, 1024, 24), ("allgather", 2, 512, 24), ("ghost", 2, 512, 32)):
-                if r and (ex, C, item, S) != ("ghost", 2, 512, 24):
-                    continue
+            for ex, C, item, S, cs in (("ghost", 2, 512, 16, True), ("ghost", 2, 512, 16, False),
+                                       ("ghost", 1, 512, 16, False), ("ghost", 2, 512, 24, False),
+                                       ("ghost", 2, 512, 32, True)):
                 d = DistributedSpMV.powerlaw(Context(rank=r, world=W, device=dev), n, nnz, slices=S, chunks=C,
-                                             exchange=ex, item_nnz=item)
+                                             exchange=ex, item_nnz=item, colsplit=cs)
                 xp = torch.rand(d.n_pad, device=dev)
                 dsts = [torch.empty(max(1, b - a), device=dev) for a, b, _ in d.parts]
 
                 def products():
+                    if d.colsplit:  # the column-split schedule: chunk-0 columns of both row chunks, then the rest
+                        for c, ((a, b, part), dst) in enumerate(zip(d.parts, dsts)):
+                            if b > a:
+                                part.product_phase(xp, 0, c)
+                        for c, ((a, b, part), dst) in enumerate(zip(d.parts, dsts)):
+                            if b > a:
+                                part.product_phase(xp, 1, c, dst[:b - a])
+                        return
                     for (a, b, part), dst in zip(d.parts, dsts):
                         if b > a:
                             d._mul(part, xp, dst[:b - a])
@@ -56,7 +63,7 @@ def main():
                 ref = d.reference_local(xp)
                 err = ((got - ref).abs().max() / ref.abs().max()).item()
                 recv = d.n_ghost if ex == "ghost" else d.n - d.rows
-                print(f"N={W} rank {r} {ex:9s} slices {S} chunks {C} item {item:4d} nnz {d.local_nnz} layout {d.n_pad:9d} product {ms:.4f} ms "
+                print(f"N={W} rank {r} {ex:9s} colsplit {int(d.colsplit)} slices {d.slices} chunks {C} item {item:4d} nnz {d.local_nnz} layout {d.n_pad:9d} product {ms:.4f} ms "
                       f"({2 * d.local_nnz / ms / 1e6:.1f} GFLOP/s) recv/step {recv * 4 / 1e6:.1f} MB err {err:.1e}",
                       flush=True)
                 del d, xp, dsts, got, ref

@@ -83,7 +83,7 @@ def test_bench_ranks_share_one_gpu_over_gloo(gpu, nproc):
     out = _bench(nproc, "--steps", "2", "--warmup", "1", "--no-ref", "--backend", "gloo", "--size", "2048",
                  "--reduce-n", "5e7", "--stencil-n", "2048", "--spmv-rows", "5e5", "--spmv-nnz", "5e6", timeout=110)
     _check_line(out, nproc)
-    assert out["spmv_exchange"] == "ghost" and out["spmv_chunks"] == 2 and out["spmv_slices"] >= 8
+    assert out["spmv_exchange"] == "ghost" and out["spmv_chunks"] == 2 and out["spmv_slices"] >= 16 and out["spmv_colsplit"]
     assert out["stencil_updates_per_step"] == 6  # auto_fuse of 1024 / 512 / 256-row slabs
 
 
@@ -216,6 +216,32 @@ def test_stencil_slabs_emulated_on_one_gpu(gpu, world, fuse, m):
     got = torch.cat([s.interior() for s in slabs]).cpu()
     ref = reference_run(n, steps, cols, device=gpu).cpu()
     assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_spmv_colsplit_phases_emulated_on_one_gpu(gpu, world):
+    """The column-split product of one rank (SlicedCSR cut at the first layout column of chunk 1): the products of the
+    slices below the split, then of the others, then the combine — bit-identical to the one-call product of the same
+    matrix (same partials, same slice-order combine) and within 1e-5 of fp64."""
+    from parallel_c_programs_amd.parallel.dist import Context
+    from parallel_c_programs_amd.parallel.spmv import DistributedSpMV
+
+    for r in sorted({0, world - 1}):
+        d = DistributedSpMV.powerlaw(Context(rank=r, world=world, device=gpu), 300_000, 3_000_000, slices=16, chunks=2,
+                                     colsplit=True)
+        assert d.colsplit and d.slices == 16 and 0 < d.col_split < d.n_pad
+        xp = torch.rand(d.n_pad, device=gpu)
+        for c, (a, b, part) in enumerate(d.parts):
+            if b <= a:
+                continue
+            assert part.col_split == d.col_split and int(part.bounds[7]) == d.col_split
+            full = part.spmv(xp)
+            dst = torch.full_like(full, float("nan"))
+            part.product_phase(xp, 0, c)
+            part.product_phase(xp, 1, c, dst)
+            assert torch.equal(dst, full), (r, c)
+            ref = part.reference(xp)
+            assert ((dst.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
 @pytest.mark.parametrize("exchange", ["ghost", "allgather"])
