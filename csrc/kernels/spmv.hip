@@ -26,6 +26,10 @@
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 
+#include <map>
+#include <mutex>
+#include <vector>
+
 namespace {
 using pcmx::kWave;
 constexpr int kItemNnz = 1024;
@@ -606,19 +610,14 @@ struct BandGeo {
     int cum[5];      // first position of band k in a row
 };
 
-__device__ __forceinline__ int band_lut(const BandGeo& g, int j) {  // window base - first position of j's band
-    const int k = (j >= g.cum[1]) + (j >= g.cum[2]) + (j >= g.cum[3]) + (j >= g.cum[4]);
-    int v = g.wbase[0] - g.cum[0];
-#pragma unroll
-    for (int p = 1; p < 5; ++p)
-        if (k == p) v = g.wbase[p] - g.cum[p];
-    return v;
-}
-
+// The slot table lut4 is the same for every block of a geometry: the launcher builds it once on the host (cached in
+// device memory per geometry, banded_lut_table) and each block copies it into LDS with kLutPer 16-B loads per thread
+// issued with the window loads (building it per block cost ~1/3 of the kernel's VALU work: profiles/r4_spmv).
+constexpr int kLutPer = 4;  // table entries per thread: 4 * ql <= 1024, checked by the launcher
 template <int R, int NV, int XW>
 __device__ __forceinline__ void banded_stream_block(const float* __restrict__ vals, long long off0, const BandGeo& g,
-                                                    int rb_begin, int sb_idx, const float* __restrict__ x,
-                                                    float* __restrict__ y, float* sm) {
+                                                    const pcmx::i32x4* __restrict__ lut_g, int rb_begin, int sb_idx,
+                                                    const float* __restrict__ x, float* __restrict__ y, float* sm) {
     const int L = g.L;
     // four copies of the x windows, copy q shifted by q (xq[q][i] = window[i + q]), each 16-B aligned: the four x
     // values of a float4 whose slots s .. s + 3 are consecutive are ONE aligned ds_read_b128 from copy s & 3
@@ -651,7 +650,14 @@ __device__ __forceinline__ void banded_stream_block(const float* __restrict__ va
         const unsigned off = i < g.W ? (unsigned)(r0 + dl + i) * 4u : 0x80000000u;  // (past the windows: reads 0)
         xv[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, 0));
     }
-    __builtin_amdgcn_sched_barrier(0);  // (keep every window load ahead of the value stream in issue order)
+    const int ql = (L + 3 + 3) >> 2, nlut = 4 * ql;
+    const auto rl = __builtin_amdgcn_make_buffer_rsrc(const_cast<pcmx::i32x4*>(lut_g), (short)0, nlut * 16, 0x00020000);
+    pcmx::i32x4 lv[kLutPer];
+#pragma unroll
+    for (int t = 0; t < kLutPer; ++t)
+        lv[t] = __builtin_bit_cast(pcmx::i32x4,
+                                   __builtin_amdgcn_raw_buffer_load_b128(rl, ((int)threadIdx.x + 256 * t) * 16, 0, 0));
+    __builtin_amdgcn_sched_barrier(0);  // (keep every window / table load ahead of the value stream in issue order)
     // the span's last float4 ends at most 3 values past the block, inside the array: clipped rows always follow
     const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vals + a0), (short)0, nf4 * 16, 0x00020000);
     pcmx::f32x4 v[NV];
@@ -669,19 +675,9 @@ __device__ __forceinline__ void banded_stream_block(const float* __restrict__ va
 #pragma unroll
         for (int cq = 0; cq < 4; ++cq) xq[max(cq * wq + i - cq, 0)] = xv[t];
     }
-    // lut4[j + 3] for j in [-3, L): the block's first float4 starts up to 3 values before its first element (j < 0,
-    // row 0): those (zeroed) values read slot 0
-    // stored phase-major (entry jj = j + 3 at (jj & 3) * ql + (jj >> 2)): the lanes of one row read positions 4 apart,
-    // i.e. consecutive entries of one phase table (16-B lane stride, no bank conflicts)
-    const int ql = (L + 3 + 3) >> 2;
-    for (int j = (int)threadIdx.x - 3; j < L; j += 256) {
-        pcmx::i32x4 t;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-            t[kk] = j + kk < 0 ? -j : j + kk < L ? kk + band_lut(g, j + kk) : kk - (L - 1) + band_lut(g, j + kk - L);
-        const int jj = j + 3;
-        lut4[(jj & 3) * ql + (jj >> 2)] = t;
-    }
+    for (int t = 0; t < kLutPer; ++t)
+        if ((int)threadIdx.x + 256 * t < nlut) lut4[threadIdx.x + 256 * t] = lv[t];
     if (threadIdx.x < R) ysum[threadIdx.x] = 0.f;
     // the block's first / last value: elements before / past them in the first / last float4 are other rows' values
     if (f0 < f1) {
@@ -713,6 +709,24 @@ __device__ __forceinline__ void banded_stream_block(const float* __restrict__ va
             const int ebase = 4 * (f0 + 64 * m) - lead;  // wave-uniform
             if (ebase > elast) break;
             const int e0 = ebase + 4 * lane;  // >= -3 (the block's first float4: its lead values are zeroed)
+            const int eend = min(ebase + 255, elast);
+            if ((cur + 1) * L - 1 > eend) {
+                // fast path (wave-uniform, ~60% of the iterations at L = 620): every element of the iteration is in row
+                // cur, so no per-lane row and no per-element row select
+                // (lanes past the wave's last element hold zero values; the clamp keeps their slot reads in the table)
+                const int j0 = min(e0 - cur * L, L - 1);
+                const pcmx::i32x4 lo = lut4[((j0 + 3) & 3) * ql + ((j0 + 3) >> 2)];
+                const int sb = e0 - cur * (L - 1);
+                const int s0 = sb + lo[0];
+                pcmx::f32x4 xs = *reinterpret_cast<const pcmx::f32x4*>(xq + (s0 & 3) * wq + (s0 & ~3));
+                if (lo[3] - lo[0] != 3) {  // a band boundary inside the float4
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) xs[kk] = xq[sb + lo[kk]];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) acc += v[m][kk] * xs[kk];
+                continue;
+            }
             // rr0 = floor(e0 / L): (e0 + 0.5) / L is at least 0.5 / L away from an integer, far above the f32 error
             // (e0 in [-3, 0): the product is in (-1, 0) and truncates to row 0)
             const int rr0 = (int)__builtin_fmaf((float)e0, invL, 0.5f * invL);
@@ -734,8 +748,7 @@ __device__ __forceinline__ void banded_stream_block(const float* __restrict__ va
                 accn += same ? 0.f : p;
             }
             // the current row ended inside this iteration (its last element is at or below the iteration's last)
-            const int eend = min(ebase + 255, elast);
-            if ((cur + 1) * L - 1 <= eend) {
+            {
                 const float s = pcmx::wave_sum_to_lane63(acc);
                 if (lane == 63) atomicAdd(&ysum[cur], s);
                 acc = accn, accn = 0.f, ++cur;
@@ -757,7 +770,8 @@ template <int R, int NV, int XW>
 __global__ __launch_bounds__(256) void spmv_banded_stream_kernel(const float* __restrict__ vals,
                                                                  const long long* __restrict__ row_off, int n, int a,
                                                                  int b, int c, int d, int e, int nfront, int back0,
-                                                                 int nclip, long long off0, BandGeo g, int rb_begin,
+                                                                 int nclip, long long off0, BandGeo g,
+                                                                 const pcmx::i32x4* __restrict__ lut_g, int rb_begin,
                                                                  const float* __restrict__ x, float* __restrict__ y) {
     extern __shared__ float sm[];
     const int bid = (int)blockIdx.x;
@@ -766,7 +780,7 @@ __global__ __launch_bounds__(256) void spmv_banded_stream_kernel(const float* __
         banded_rows_body<R, 16, 1>(vals, row_off, n, a, b, c, d, e, x, y, sm, rb * R);
         return;
     }
-    banded_stream_block<R, NV, XW>(vals, off0, g, rb_begin, bid - nclip, x, y, sm);
+    banded_stream_block<R, NV, XW>(vals, off0, g, lut_g, rb_begin, bid - nclip, x, y, sm);
 }
 
 // fallback for rows longer than 16 x 64 nonzeros: one wave per row, strided band loops
@@ -953,6 +967,44 @@ void band_limits_host(int n, int a, int b, int c, int d, int e, int row, int (&l
 
 namespace {
 constexpr int kStreamNotApplicable = -1000;
+
+// Variant 8's slot table for one geometry (see banded_stream_block): lut4[j + 3] for j in [-3, L), entry jj = j + 3
+// stored phase-major at (jj & 3) * ql + (jj >> 2) (the lanes of one row read positions 4 apart, i.e. consecutive entries
+// of one phase table: 16-B lane stride, no bank conflicts). lut4[j][kk] = kk + lut(j + kk), or past the row end
+// kk - (L - 1) + lut(j + kk - L) (the next row); the block's first float4 starts up to 3 values before its first element
+// (j < 0, row 0): those (zeroed) values read slot 0. Built on the host once per (device, geometry) and kept in device
+// memory for the life of the process (a few KB per geometry).
+const pcmx::i32x4* banded_lut_table(const BandGeo& g) {
+    static std::mutex mu;
+    static std::map<std::vector<int>, void*> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::vector<int> key{dev, g.L};
+    key.insert(key.end(), g.wbase, g.wbase + 6);
+    key.insert(key.end(), g.cum, g.cum + 5);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return reinterpret_cast<const pcmx::i32x4*>(it->second);
+    const int L = g.L, ql = (L + 6) >> 2;
+    auto lut = [&](int j) {  // window base - first position of j's band
+        const int k = (j >= g.cum[1]) + (j >= g.cum[2]) + (j >= g.cum[3]) + (j >= g.cum[4]);
+        return g.wbase[k] - g.cum[k];
+    };
+    std::vector<int> tab((size_t)16 * ql, 0);  // 4 * ql entries of 4 ints
+    for (int j = -3; j < L; ++j) {
+        const int jj = j + 3, ent = (jj & 3) * ql + (jj >> 2);
+        for (int kk = 0; kk < 4; ++kk)
+            tab[4 * ent + kk] = j + kk < 0 ? -j : j + kk < L ? kk + lut(j + kk) : kk - (L - 1) + lut(j + kk - L);
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, tab.size() * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    cache.emplace(key, d);
+    return reinterpret_cast<const pcmx::i32x4*>(d);
+}
 // Variant 8/9 launch (block stream over the unclipped rows, the clipped row blocks folded into the same grid);
 // kStreamNotApplicable when the band geometry or the value alignment rules it out.
 template <int RS, int NV, int XW>
@@ -970,7 +1022,8 @@ int launch_banded_stream(const float* vals, const long long* row_off, int n, int
     const size_t lds8 = (size_t)(4 * 256 * XW + ((RS + 3) & ~3) + 16 * ((L + 6) / 4)) * sizeof(float);
     // the wave-iteration rule needs rows of >= 256 nonzeros, the float4 stream a 16-B aligned vals; the register
     // sets hold NV float4s per lane and XW window floats per thread; the clipped body NL = 16 chunks of 64
-    const bool ok = L >= 256 && L <= 16 * 64 && q <= 64 * NV && W + 3 <= XW * 256 && rb_hi > rb_lo &&
+    const bool ok = L >= 256 && L <= 16 * 64 && 4 * ((L + 6) / 4) <= 256 * kLutPer && q <= 64 * NV &&
+                    W + 3 <= XW * 256 && rb_hi > rb_lo &&
                     !((uintptr_t)vals & 15) && lds_rows <= 64 * 1024 && lds8 <= 64 * 1024;
     if (!ok) return kStreamNotApplicable;
     BandGeo g{};
@@ -985,6 +1038,8 @@ int launch_banded_stream(const float* vals, const long long* row_off, int n, int
         }
         g.wbase[5] = wb;
     }
+    const pcmx::i32x4* lut_g = banded_lut_table(g);
+    if (!lut_g) return (int)hipErrorOutOfMemory;
     const int nfront = rb_lo, back0 = rb_hi, nback = nrb - rb_hi;
     // first value of row rb_lo * RS: the nonzeros of the clipped rows before it (host sum of row lengths)
     long long off0 = 0;
@@ -994,7 +1049,7 @@ int launch_banded_stream(const float* vals, const long long* row_off, int n, int
         for (int k = 0; k < 5; ++k) off0 += hi[k] - lo[k];
     }
     spmv_banded_stream_kernel<RS, NV, XW><<<nfront + nback + rb_hi - rb_lo, 256, std::max(lds_rows, lds8), s>>>(
-        vals, row_off, n, a, b, c, d, e, nfront, back0, nfront + nback, off0, g, rb_lo, x, y);
+        vals, row_off, n, a, b, c, d, e, nfront, back0, nfront + nback, off0, g, lut_g, rb_lo, x, y);
     return (int)hipGetLastError();
 }
 }  // namespace

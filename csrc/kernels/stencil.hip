@@ -254,19 +254,20 @@ __device__ __forceinline__ typename RawT<NP>::type update_pairs(const RowP<NP>& 
 // Row spans of one launch: blocks [0, nby_a) of grid.y cover local rows [a0, a1), the rest [b0, b1) (empty when
 // b0 == b1). A distributed step updates both rank-edge row bands in ONE launch after the halo arrives, and a
 // launch covers only its rows (no grid over the whole slab with idle blocks).
+// rpw: rows per wave, a launch parameter (not a template argument): the host picks it per launch so that the grid
+// fills whole residency rounds of the chip (see pick_rpw).
 struct RowSpans {
-    int a0, a1, b0, b1, nby_a;
+    int a0, a1, b0, b1, nby_a, rpw;
 };
 // The rows [rs, re) of this wave (rs >= re: none).
-template <int RPW>
 __device__ __forceinline__ void wave_rows(const RowSpans& sp, int wave, int& rs, int& re) {
     int by = (int)blockIdx.y, base = sp.a0, lim = sp.a1;
     if (by >= sp.nby_a) by -= sp.nby_a, base = sp.b0, lim = sp.b1;
-    rs = base + by * (kWaves * RPW) + wave * RPW;
-    re = min(lim, rs + RPW);
+    rs = base + by * (kWaves * sp.rpw) + wave * sp.rpw;
+    re = min(lim, rs + sp.rpw);
 }
 
-template <int T, int kAhead, int RPW = kRowsPerWave, int CPL = 8>
+template <int T, int kAhead, int CPL = 8>
 __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict__ u, unsigned short* __restrict__ out,
                                                 int rows, int cols, int ld, int halo, int rs, int re, long long grow0,
                                                 long long grows, float k) {
@@ -330,14 +331,14 @@ __device__ __forceinline__ void stencil5xT_body(const unsigned short* __restrict
         }
     }
 }
-template <int T, int kAhead, int RPW = kRowsPerWave>
+template <int T, int kAhead>
 __global__ __launch_bounds__(kWaves * 64) void stencil5xT_kernel(const unsigned short* __restrict__ u,
                                                                  unsigned short* __restrict__ out, int rows, int cols,
                                                                  int ld, int halo, RowSpans sp, long long grow0,
                                                                  long long grows, float k) {
     int rs, re;
-    wave_rows<RPW>(sp, (int)threadIdx.x >> 6, rs, re);
-    stencil5xT_body<T, kAhead, RPW>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
+    wave_rows(sp, (int)threadIdx.x >> 6, rs, re);
+    stencil5xT_body<T, kAhead>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
 }
 
 // ---- v2: the same T-level row pipeline with ~30% fewer VALU ops per level (the kernel is VALU-issue bound):
@@ -466,7 +467,7 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
 // MINW: minimum waves per SIMD the register allocation must allow (__launch_bounds__'s second argument): a short
 // slab has few waves, so fitting one more per SIMD (T=4: 138 -> <= 128 VGPRs, 3 -> 4 waves) can matter more than
 // the few rematerialised values it costs.
-template <int T, int kAhead, int RPW = kRowsPerWave, int MINW = 1, int CPL = 8>
+template <int T, int kAhead, int MINW = 1, int CPL = 8>
 __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
                                                                   unsigned short* __restrict__ out, int rows, int cols,
                                                                   int ld, int halo, RowSpans sp, long long grow0,
@@ -477,7 +478,7 @@ __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const un
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int c0 = G::c0(lane);  // first column of this lane
     int rs, re;
-    wave_rows<RPW>(sp, wave, rs, re);
+    wave_rows(sp, wave, rs, re);
     if (rs >= re) return;
     const bool in_grid = c0 + CPL <= cols;  // cols % 8 == 0
     const bool store_lane = G::store_lane(lane, cols, in_grid);
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const un
     const bool edge_rows = (g0 <= 0 && 0 <= g1) || (g0 <= grows - 1 && grows - 1 <= g1);
     const bool slow = edge_rows || __builtin_amdgcn_ballot_w64(fix0 || fixl) != 0;
     if (slow)  // a few waves per grid: the v1 pipeline (per-column selects, per-row Dirichlet test; same results)
-        stencil5xT_body<T, kAhead, RPW, CPL>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
+        stencil5xT_body<T, kAhead, CPL>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
     else
         pipeline_v2<T, kAhead, G::NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
 }
@@ -526,7 +527,7 @@ int strips_for(int cols, int cpl, int steps) {
     return cols <= 64 * cpl ? 1 : 1 + (cols - 64 * cpl + out - 1) / out;
 }
 // lab override of the launch shape (0 = production rule): columns per lane, rows per wave
-int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0;
+int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0, g_lab_ahead = 0;
 // the halo rule of one row range: a row r reads rows r - steps .. r + steps, which must lie in the slab on a side
 // with a neighbour (at a GLOBAL edge the clamped reads only feed Dirichlet rows)
 bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row0, long long global_rows) {
@@ -591,28 +592,24 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
         cpl = 8, rpw = steps <= 4 ? 24 : 64;
     if (edge ? g_lab_edge_cpl : g_lab_cpl) cpl = edge ? g_lab_edge_cpl : g_lab_cpl;
     if (edge ? g_lab_edge_rpw : g_lab_rpw) rpw = edge ? g_lab_edge_rpw : g_lab_rpw;
-    auto launch_dims = [&](int rpw_, int cpl_, RowSpans& sp) {
-        const int per = kWaves * rpw_;
-        sp = RowSpans{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per};
-        return dim3(strips_for(cols, cpl_, steps), sp.nby_a + (r1b - r0b + per - 1) / per);
-    };
-    RowSpans sp;
-#define PCMX_STENCIL_V2_RPW(T, R, C)                                                                                \
-    case R: {                                                                                                       \
-        const dim3 g = launch_dims(R, C, sp);                                                                       \
-        stencil5xT2_kernel<T, (T >= 6 && R >= 64 ? 9 : R == 18 || R <= 4 ? 3 : 6), R, 1, C><<<g, kWaves * 64, 0, s>>>( \
-            ui, uo, rows, cols, ld, halo, sp, global_row0, global_rows, k);                                         \
-        break;                                                                                                      \
-    }
+    if (steps == 2) cpl = 8, rpw = kRowsPerWave;  // T = 2: the HBM-bound v1 kernel, one shape
+    if (steps == 3) cpl = 8;                      // T = 3: 8-column lanes only
+    // prefetch ring depth (rows in flight per wave; a multiple of 3, see stencil5xT_body)
+    int ahead = (steps >= 6 && rpw >= 64) ? 9 : (rpw <= 4 || (rpw > 16 && rpw <= 20)) ? 3 : 6;
+    if (g_lab_ahead) ahead = g_lab_ahead;
+    const int per = kWaves * rpw;
+    const RowSpans sp{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per, rpw};
+    const dim3 g(strips_for(cols, steps == 2 ? 8 : cpl, steps), sp.nby_a + (r1b - r0b + per - 1) / per);
+#define PCMX_STENCIL_V2_KA(T, KA, C)                                                                                \
+    case KA:                                                                                                        \
+        stencil5xT2_kernel<T, KA, 1, C><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,    \
+                                                                   global_rows, k);                                 \
+        break;
 #define PCMX_STENCIL_V2C(T, C)                                                                                      \
-    switch (rpw) {                                                                                                  \
-        PCMX_STENCIL_V2_RPW(T, 2, C)                                                                                \
-        PCMX_STENCIL_V2_RPW(T, 4, C)                                                                                \
-        PCMX_STENCIL_V2_RPW(T, 16, C)                                                                               \
-        PCMX_STENCIL_V2_RPW(T, 18, C)                                                                               \
-        PCMX_STENCIL_V2_RPW(T, 24, C)                                                                               \
-        PCMX_STENCIL_V2_RPW(T, 32, C)                                                                               \
-        PCMX_STENCIL_V2_RPW(T, 64, C)                                                                               \
+    switch (ahead) {                                                                                                \
+        PCMX_STENCIL_V2_KA(T, 3, C)                                                                                 \
+        PCMX_STENCIL_V2_KA(T, 6, C)                                                                                 \
+        PCMX_STENCIL_V2_KA(T, 9, C)                                                                                 \
         default: return -1;                                                                                         \
     }
 #define PCMX_STENCIL_V2(T)                                                                                          \
@@ -622,11 +619,9 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
         PCMX_STENCIL_V2C(T, 8)                                                                                      \
     }
     switch (steps) {
-        case 2: {
-            const dim3 g = launch_dims(kRowsPerWave, 8, sp);
+        case 2:
             stencil5xT_kernel<2, 6><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0, global_rows, k);
             break;
-        }
         case 3: PCMX_STENCIL_V2C(3, 8) break;
         case 4: PCMX_STENCIL_V2(4) break;
         case 6: PCMX_STENCIL_V2(6) break;
@@ -635,16 +630,21 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
     }
 #undef PCMX_STENCIL_V2
 #undef PCMX_STENCIL_V2C
-#undef PCMX_STENCIL_V2_RPW
+#undef PCMX_STENCIL_V2_KA
     return (int)hipGetLastError();
 }
 
-// Lab knob (scripts/stencil_lanes_lab.py): force columns per lane (4 / 8) and rows per wave (2 / 4 / 16 / 18 / 24 /
-// 32 / 64) of the fused v2 launches over more than 64 rows (which = 0) or of edge launches (which = 1); 0 restores
-// the production rule. Host-global, not thread-safe: labs only.
+// Lab knob (scripts/stencil_lanes_lab.py, scripts/stencil_rpw_lab.py): force columns per lane (4 / 8) and rows per
+// wave (1 .. 256) of the fused v2 launches over more than 64 rows (which = 0) or of edge launches (which = 1), or
+// (which = 2, cpl ignored) the prefetch ring depth (3 / 6 / 9 rows); 0 restores the production rule. Host-global, not
+// thread-safe: labs only.
 extern "C" int pcmx_stencil_lab_set(int which, int cpl, int rpw) {
-    const bool rpw_ok = rpw == 0 || rpw == 2 || rpw == 4 || rpw == 16 || rpw == 18 || rpw == 24 || rpw == 32 || rpw == 64;
-    if ((cpl != 0 && cpl != 4 && cpl != 8) || !rpw_ok || (which != 0 && which != 1)) return -1;
+    if (which == 2) {
+        if (rpw != 0 && rpw != 3 && rpw != 6 && rpw != 9) return -1;
+        g_lab_ahead = rpw;
+        return 0;
+    }
+    if ((cpl != 0 && cpl != 4 && cpl != 8) || rpw < 0 || rpw > 256 || (which != 0 && which != 1)) return -1;
     (which ? g_lab_edge_cpl : g_lab_cpl) = cpl;
     (which ? g_lab_edge_rpw : g_lab_rpw) = rpw;
     return 0;

@@ -241,7 +241,7 @@ def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
 @pytest.mark.parametrize("shape", [(515, 1000), (70, 2056), (200, 264)])
 def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
     """Every launch shape the stencil lab knob can force (4 or 8 columns per lane x 2..64 rows per wave, for full
-    and edge launches) gives the bits of `steps` single steps: ragged column counts (stale-lane rule of 4-column lanes
+    and edge launches; rows per wave is a launch parameter, so odd counts too) gives the bits of `steps` single steps: ragged column counts (stale-lane rule of 4-column lanes
     at T = 8: two stale lanes per strip side), Dirichlet rows and columns, strips ending inside a lane range."""
     import ctypes  # noqa: F401
     from parallel_c_programs_amd._native import hip_lib
@@ -256,7 +256,7 @@ def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
     lib = hip_lib()
     try:
         for cpl in (4, 8):
-            for rpw in (2, 4, 16, 18, 24, 32, 64):
+            for rpw in (2, 4, 7, 16, 18, 24, 32, 64, 67, 133):
                 assert lib.pcmx_stencil_lab_set(0, cpl, rpw) == 0 and lib.pcmx_stencil_lab_set(1, cpl, rpw) == 0
                 b = torch.zeros_like(a)
                 ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps)
