@@ -528,6 +528,30 @@ int strips_for(int cols, int cpl, int steps) {
 }
 // lab override of the launch shape (0 = production rule): columns per lane, rows per wave
 int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0, g_lab_ahead = 0;
+// Rows per wave for a short slab at T = 6 (4-column lanes): the smallest count >= 18 whose grid fits ONE residency
+// round of the chip (every workgroup resident at once), so no second, partly filled round of waves follows. One N = 8
+// rank's 2048-row slab: 29 rows per wave (1242 workgroups <= 256 CUs x 5) 0.0526 ms against 0.0567 with 18 (1.56
+// rounds); at T = 8 and on tall grids the round count measured no effect (scripts/stencil_rpw_lab.py,
+// profiles/r4_stencil/rpw_sweep.txt).
+int one_round_rpw(int span_a, int span_b, int cols, int steps) {
+    static const int slots = [] {
+        int dev = 0, cus = 256, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, stencil5xT2_kernel<6, 6, 1, 4>, kWaves * 64, 0) !=
+                hipSuccess ||
+            per <= 0)
+            per = 5;
+        return cus * per;
+    }();
+    const int strips = strips_for(cols, 4, steps);
+    for (int r = 18; r <= 48; ++r) {
+        const int per = kWaves * r;
+        if ((long long)strips * ((span_a + per - 1) / per + (span_b + per - 1) / per) <= slots) return r;
+    }
+    return 18;
+}
 // the halo rule of one row range: a row r reads rows r - steps .. r + steps, which must lie in the slab on a side
 // with a neighbour (at a GLOBAL edge the clamped reads only feed Dirichlet rows)
 bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row0, long long global_rows) {
@@ -583,7 +607,7 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
     if (edge)
         cpl = 4, rpw = 2;
     else if (span_rows < 3072)
-        cpl = steps >= 6 ? 4 : 8, rpw = steps == 6 ? 18 : 24;
+        cpl = steps >= 6 ? 4 : 8, rpw = steps == 6 ? one_round_rpw(r1a - r0a, r1b - r0b, cols, steps) : 24;
     else if (span_rows < 6144)
         cpl = steps >= 6 ? 4 : 8, rpw = steps == 8 ? 32 : 24;
     else if (span_rows < 12288)
