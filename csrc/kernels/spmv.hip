@@ -733,20 +733,23 @@ __device__ __forceinline__ void banded_stream_block(const float* __restrict__ va
             const int j0 = e0 - rr0 * L;
             const pcmx::i32x4 lo = lut4[((j0 + 3) & 3) * ql + ((j0 + 3) >> 2)];
             const int sb = e0 - rr0 * (L - 1);
-            const int split = L - j0;  // elements kk >= split belong to row rr0 + 1
             const int s0 = sb + lo[0];
             pcmx::f32x4 xs = *reinterpret_cast<const pcmx::f32x4*>(xq + (s0 & 3) * wq + (s0 & ~3));
             if (lo[3] - lo[0] != 3) {  // a band or row boundary inside the float4 (a few lanes per iteration)
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) xs[kk] = xq[sb + lo[kk]];
             }
+            // row cur ends inside this iteration: this lane's elements kk < nc are in row cur, the rest in row cur + 1
+            // (the iteration spans at most two rows); one lane-wide total and one masked partial per float4
+            const int nc = (cur + 1) * L - e0;
+            float pall = 0.f, pcur = 0.f;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const float p = v[m][kk] * xs[kk];
-                const bool same = (kk < split ? rr0 : rr0 + 1) == cur;
-                acc += same ? p : 0.f;
-                accn += same ? 0.f : p;
+                pall = __builtin_fmaf(v[m][kk], xs[kk], pall);
+                pcur = __builtin_fmaf(v[m][kk], kk < nc ? xs[kk] : 0.f, pcur);
             }
+            acc += pcur;
+            accn += pall - pcur;
             // the current row ended inside this iteration (its last element is at or below the iteration's last)
             {
                 const float s = pcmx::wave_sum_to_lane63(acc);
@@ -1103,5 +1106,5 @@ extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_
 
 extern "C" int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                                 const float* x, float* y, hipStream_t s) {
-    return pcmx_spmv_banded_variant(vals, row_off, n, a, b, c, d, e, x, y, 1, s);
+    return pcmx_spmv_banded_variant(vals, row_off, n, a, b, c, d, e, x, y, 8, s);  // (falls back to 1 when needed)
 }

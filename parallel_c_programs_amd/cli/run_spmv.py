@@ -42,7 +42,7 @@ def main(argv=None) -> int:
     dims = (a.dim, a.a, a.b, a.c, a.d, a.e)
     runs = (("GPU CSR-adaptive (explicit column indices)", lambda: ops.spmv(g, xg),
              m.nnz * 8 + (m.n_rows + 1) * 8 + m.n_rows * 8),
-            ("GPU banded, implicit columns, LDS-staged x windows", lambda: ops.spmv_banded(g.val, g.row_ptr, *dims, xg),
+            ("GPU banded, implicit columns, 16-B block stream + LDS x windows", lambda: ops.spmv_banded(g.val, g.row_ptr, *dims, xg),
              m.nnz * 4 + m.n_rows * 8))
     scrub = torch.empty(256 << 20, device="cuda").uniform_()  # 1 GiB, READ between cold calls (evicts the MALL)
     for name, fn, bytes_ in runs:

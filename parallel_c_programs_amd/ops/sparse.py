@@ -343,9 +343,11 @@ def spmv(m: CSR, x: torch.Tensor) -> torch.Tensor:
 
 
 def spmv_banded(vals: torch.Tensor, row_off: torch.Tensor, n: int, a: int, b: int, c: int, d: int, e: int,
-                x: torch.Tensor, variant: int = 1) -> torch.Tensor:
-    """Banded product with implicit columns (the reference's s_matrix `multiply`, spmv.c:212-329). GPU variant 1
-    (default): row blocks with the x band windows staged in LDS and in-register band limits; 0: one wave per row."""
+                x: torch.Tensor, variant: int = 8) -> torch.Tensor:
+    """Banded product with implicit columns (the reference's s_matrix `multiply`, spmv.c:212-329). GPU variant 8
+    (default): each 16-row block's values as one aligned 16-B stream, x band windows in LDS (falls back to variant 1
+    when the geometry or alignment rules it out); 1: row blocks with 4-B value loads and in-register band limits;
+    0: one wave per row."""
     if x.is_cuda:
         return ops().spmv_banded(vals, row_off, int(n), int(a), int(b), int(c), int(d), int(e), x, int(variant))
 

@@ -12,6 +12,8 @@ exchange, for the launch shapes a step can take:
 Every variant is checked bit for bit against `full`. Prints ms per step and GLUP/s per GPU; with the 1-GPU
 full-grid time this bounds the strong-scaling efficiency of the compute part (docs/ARCHITECTURE.md, stencil).
 Run: python scripts/stencil_rank_lab.py [fuse ...]
+Env: STENCIL_LAB_WORLDS=8 (subset of 1,2,4,8), STENCIL_LAB_RPW=0,18 (rows per wave forced on the non-edge launches
+through pcmx_stencil_lab_set, 0 = production rule; one line per value, all in one process for an A/B).
 """
 import os
 import sys
@@ -20,6 +22,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from parallel_c_programs_amd import ops  # noqa: E402
+from parallel_c_programs_amd._native import hip_lib  # noqa: E402
 
 N = 16384
 
@@ -41,8 +44,11 @@ def main():
     fuses = [int(a) for a in sys.argv[1:]] or [4, 6, 8]
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(1)
-    for T in fuses:
-        for world in (1, 2, 4, 8):
+    worlds = [int(w) for w in os.environ.get("STENCIL_LAB_WORLDS", "1,2,4,8").split(",")]
+    rpws = [int(r) for r in os.environ.get("STENCIL_LAB_RPW", "0").split(",")]
+    for T, world, rpw in [(T, w, r) for T in fuses for w in worlds for r in rpws]:
+        assert hip_lib().pcmx_stencil_lab_set(0, 0, rpw) == 0
+        if True:
             rows = N // world
             row0 = 0 if world == 1 else rows  # rank 1: both neighbours present (interior rank)
             u = (torch.rand(rows + 2 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
@@ -99,9 +105,11 @@ def main():
                 res[name] = (timed(fn), same)
             line = " ".join(f"{k} {ms:.4f} ms {rows * N * T / ms / 1e6:7.0f} GLUP/s{'' if ok else ' MISMATCH'}"
                             for k, (ms, ok) in res.items())
-            print(f"fuse={T} N={world} rows={rows:5d}  {line}", flush=True)
+            tag = f" rpw={rpw}" if rpw else ""
+            print(f"fuse={T} N={world} rows={rows:5d}{tag}  {line}", flush=True)
             del u, ref, out, u2, v2, w2, ref2, ref3
             torch.cuda.empty_cache()
+    hip_lib().pcmx_stencil_lab_set(0, 0, 0)
 
 
 if __name__ == "__main__":
