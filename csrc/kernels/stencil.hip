@@ -414,45 +414,14 @@ __device__ __forceinline__ void buffer_store_row(const typename RawT<NP>::type& 
 }
 
 // The row pipeline of one interior wave (no Dirichlet row or column in reach).
-// LDS-DMA prefetch (kDma, 8-column lanes): the ring rows travel HBM -> LDS with `buffer_load_dwordx4 ... lds` (one
-// 1-KiB slot per ring row and wave) instead of into registers. The compiler does not count these loads, so the kernel
-// waits for them itself with an exact vmcnt: with every row issuing one ring load and one store (both unconditional),
-// a ring slot's load is followed by a known number of vector-memory operations when row j of the next ring turn
-// reads the slot (each row reads its slot first and issues the slot's next DMA after its store, so 2 kAhead - 2
-// operations separate a DMA from the read of its slot). (With register loads, the compiler's own bookkeeping lost count at the loop head — the trapezoid
-// branches give the loop body several paths — and waited for every access in flight, vmcnt(0), once per ring turn.)
-// Before the loop the kAhead preloads are followed by kAhead dropped stores (out-of-range offset), so the first turn's
-// counts are at least as large. A wave drains its DMA loads (vmcnt(0)) before it ends.
-// (M0 holds the LDS destination; it is compiler-reserved, so the statement saves and restores it)
-__device__ __forceinline__ void dma_row16(__amdgpu_buffer_rsrc_t r, unsigned vo, int so, unsigned lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(vo), "s"(r), "s"(lds_dst), "s"(so)
-                 : "memory");
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(N) : "memory");
-}
-
-template <int T, int kAhead, int NP, bool kDma = false>
+template <int T, int kAhead, int NP>
 __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, const __amdgpu_buffer_rsrc_t ro, unsigned vld,
-                                            unsigned vst, int sr0, int pitch, int slab_rows, int halo, int rs, int re,
-                                            int i0, int i1, unsigned bytes, float k, unsigned lds_ring = 0) {
+                                            unsigned vst, int sr0, int pitch, int slab_rows, int halo, int rs, int i0,
+                                            int i1, float k) {
     using W = typename RawT<NP>::type;
-    static_assert(!kDma || NP == 4, "LDS-DMA ring: 16-B rows");
     auto fetch = [&](int r) __attribute__((always_inline)) {  // local row r, clamped into the slab
         const int sr = min(max(r + halo, 0), slab_rows - 1);
         return buffer_load_row<NP>(ru, vld, (sr - sr0) * pitch);
-    };
-    // kDma: slot j of this wave's ring at LDS byte address lds_ring + 1024 j (64 lanes x 16 B)
-    typedef __attribute__((address_space(3))) const W* LdsW;  // an LDS pointer: ds_read, not a flat load
-    const LdsW slot = (LdsW)(uintptr_t)lds_ring + pcmx::lane_id();
-    auto fetch_dma = [&](int r, int j) __attribute__((always_inline)) {
-        const int sr = min(max(r + halo, 0), slab_rows - 1);
-        dma_row16(ru, vld, (sr - sr0) * pitch, lds_ring + 1024u * (unsigned)j);
     };
     // ring[t][slot]: level t (0 = u) row with (row index - first) % 3 == slot, as exact floats in pair layout
     RowP<NP> ring[T][3];
@@ -463,60 +432,36 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
 #pragma unroll
             for (int p = 0; p < NP; ++p) ring[t][q].p[p] = f2{0.f, 0.f};
     W pre[kAhead];
-    if constexpr (kDma) {
 #pragma unroll
-        for (int j = 0; j < kAhead; ++j) fetch_dma(min(i0 + j, i1 - 1), j);
-#pragma unroll
-        for (int j = 0; j < kAhead; ++j) buffer_store_row<NP>(W{0u}, ro, vst, (int)bytes);  // dropped: count padding
-    } else {
-#pragma unroll
-        for (int j = 0; j < kAhead; ++j) pre[j] = fetch(min(i0 + j, i1 - 1));
-    }
+    for (int j = 0; j < kAhead; ++j) pre[j] = fetch(min(i0 + j, i1 - 1));
     // (a branch-free main loop — the per-level trapezoid / store tests peeled into the first 2T rows — measured no
     // faster at any shape and spilled at 8 columns per lane: profiles/r4_stencil/peel_rpw128_rejected.txt)
-    // Every row of the loop issues exactly one load and one store, with no memory instruction under a branch: the
-    // rows past the wave's last (up to kAhead - 1 of them in the last ring turn) load a clamped row and compute
-    // throw-away values, and the stored level is computed for every row with the store of a row outside [rs, re)
-    // dropped by an out-of-range offset. With a conditional load or store in the loop (round 3: `if (i < i1)` per
-    // row and the store under `r >= rs`), the compiler's wait-count bookkeeping could not tell how many accesses
-    // were in flight at the loop head and waited for ALL of them (vmcnt(0)) once per ring turn.
     for (int ib = i0; ib < i1; ib += kAhead) {
 #pragma unroll
         for (int j = 0; j < kAhead; ++j) {
             const int i = ib + j;
-            const int m0 = j % 3, m1 = (j + 2) % 3, m2 = (j + 1) % 3;  // slots of rows i, i-1, i-2
-            W w;
-            if constexpr (kDma) {
-                wait_vm<2 * kAhead - 2>();
-                w = slot[64 * j];
-                ring[0][m0] = unpack_pairs<NP>(w);
-            } else {
+            if (i < i1) {
+                const int m0 = j % 3, m1 = (j + 2) % 3, m2 = (j + 1) % 3;  // slots of rows i, i-1, i-2
                 ring[0][m0] = unpack_pairs<NP>(pre[j]);
                 pre[j] = fetch(min(i + kAhead, i1 - 1));
-            }
 #pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const int r = i - t - 1;
-                if (t + 1 < T) {
-                    if (i - i0 <= 2 * t + 1) continue;  // outside the wave's trapezoid (see stencil5xT_body)
-                    W unused;
-                    level_pairs<false, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k,
-                                           ring[t + 1 < T ? t + 1 : 0][m0], unused);
-                } else {
-                    W pk;
-                    RowP<NP> unused;
-                    level_pairs<true, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k, unused, pk);
-                    const int so = r >= rs && r < re ? (r + halo - sr0) * pitch : (int)bytes;
-                    buffer_store_row<NP>(pk, ro, vst, so);
+                for (int t = 0; t < T; ++t) {
+                    const int r = i - t - 1;
+                    if (t + 1 < T) {
+                        if (i - i0 <= 2 * t + 1) continue;  // outside the wave's trapezoid (see stencil5xT_body)
+                        W unused;
+                        level_pairs<false, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k,
+                                               ring[t + 1 < T ? t + 1 : 0][m0], unused);
+                    } else if (r >= rs) {
+                        W pk;
+                        RowP<NP> unused;
+                        level_pairs<true, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k, unused, pk);
+                        buffer_store_row<NP>(pk, ro, vst, (r + halo - sr0) * pitch);
+                    }
                 }
-            }
-            if constexpr (kDma) {  // the slot's next row, issued after the row's store (the slot was read into w)
-                asm volatile("" : : "v"(w));
-                fetch_dma(min(i + kAhead, i1 - 1), j);
             }
         }
     }
-    if constexpr (kDma) wait_vm<0>();  // no LDS-DMA write may land after the wave (and its LDS) is gone
 }
 
 // MINW: minimum waves per SIMD the register allocation must allow (__launch_bounds__'s second argument): a short
@@ -526,8 +471,7 @@ template <int T, int kAhead, int MINW = 1, int CPL = 8>
 __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
                                                                   unsigned short* __restrict__ out, int rows, int cols,
                                                                   int ld, int halo, RowSpans sp, long long grow0,
-                                                                  long long grows, float k, int dma) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char stencil_ring[];  // dma: [4 waves][kAhead][1 KiB]
+                                                                  long long grows, float k) {
     using G = Geo<CPL, T>;
     static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
     const int lane = threadIdx.x & 63;
@@ -555,17 +499,8 @@ __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const un
     const bool slow = edge_rows || __builtin_amdgcn_ballot_w64(fix0 || fixl) != 0;
     if (slow)  // a few waves per grid: the v1 pipeline (per-column selects, per-row Dirichlet test; same results)
         stencil5xT_body<T, kAhead, CPL>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
-    else if constexpr (CPL == 8) {
-        if (dma) {
-            const unsigned base = (unsigned)(uintptr_t)stencil_ring + (unsigned)wave * 1024u * kAhead;
-            pipeline_v2<T, kAhead, G::NP, true>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, re, i0, i1, bytes, k,
-                                                __builtin_amdgcn_readfirstlane(base));
-        } else {
-            pipeline_v2<T, kAhead, G::NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, re, i0, i1, bytes, k);
-        }
-    } else {
-        pipeline_v2<T, kAhead, G::NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, re, i0, i1, bytes, k);
-    }
+    else
+        pipeline_v2<T, kAhead, G::NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
 }
 #pragma clang fp contract(on)
 }  // namespace
@@ -592,7 +527,7 @@ int strips_for(int cols, int cpl, int steps) {
     return cols <= 64 * cpl ? 1 : 1 + (cols - 64 * cpl + out - 1) / out;
 }
 // lab override of the launch shape (0 = production rule): columns per lane, rows per wave
-int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0, g_lab_ahead = 0, g_lab_dma = 0;
+int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0, g_lab_ahead = 0;
 // Rows per wave for a short slab at T = 6 (4-column lanes): the smallest count >= 18 whose grid fits ONE residency
 // round of the chip (every workgroup resident at once), so no second, partly filled round of waves follows. One N = 8
 // rank's 2048-row slab: 29 rows per wave (1242 workgroups <= 256 CUs x 5) 0.0526 ms against 0.0567 with 18 (1.56
@@ -686,14 +621,13 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
     // prefetch ring depth (rows in flight per wave; a multiple of 3, see stencil5xT_body)
     int ahead = (steps >= 6 && rpw >= 64) ? 9 : (rpw <= 4 || (rpw > 16 && rpw <= 20)) ? 3 : 6;
     if (g_lab_ahead) ahead = g_lab_ahead;
-    const int dma = g_lab_dma;
     const int per = kWaves * rpw;
     const RowSpans sp{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per, rpw};
     const dim3 g(strips_for(cols, steps == 2 ? 8 : cpl, steps), sp.nby_a + (r1b - r0b + per - 1) / per);
 #define PCMX_STENCIL_V2_KA(T, KA, C)                                                                                \
     case KA:                                                                                                        \
-        stencil5xT2_kernel<T, KA, 1, C><<<g, kWaves * 64, dma && C == 8 ? kWaves * KA * 1024 : 0, s>>>(               \
-            ui, uo, rows, cols, ld, halo, sp, global_row0, global_rows, k, dma && C == 8);                          \
+        stencil5xT2_kernel<T, KA, 1, C><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,    \
+                                                                   global_rows, k);                                 \
         break;
 #define PCMX_STENCIL_V2C(T, C)                                                                                      \
     switch (ahead) {                                                                                                \
@@ -732,11 +666,6 @@ extern "C" int pcmx_stencil_lab_set(int which, int cpl, int rpw) {
     if (which == 2) {
         if (rpw != 0 && rpw != 3 && rpw != 6 && rpw != 9) return -1;
         g_lab_ahead = rpw;
-        return 0;
-    }
-    if (which == 3) {  // LDS-DMA ring prefetch for 8-column lanes: 1 on, 0 off
-        if (rpw != 0 && rpw != 1) return -1;
-        g_lab_dma = rpw;
         return 0;
     }
     if ((cpl != 0 && cpl != 4 && cpl != 8) || rpw < 0 || rpw > 256 || (which != 0 && which != 1)) return -1;

@@ -22,7 +22,8 @@ for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
         k = r["Kernel_Name"]
         if "banded" not in k:
             continue
-        agg[k.split("(")[0][-60:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        name = k.replace("(anonymous namespace)::", "").split("(")[0][-70:]
+        agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 with open(f"{out}/summary.txt", "w") as fo:
     for name, cs in sorted(agg.items()):
         fo.write(f"== {name}\n")

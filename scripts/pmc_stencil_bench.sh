@@ -25,7 +25,7 @@ for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
         k = r["Kernel_Name"]
         if "stencil" not in k:
             continue
-        name = k.split("(")[0].replace("(anonymous namespace)::", "")
+        name = k.replace("(anonymous namespace)::", "").split("(")[0]
         agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 with open(f"{out}/summary.txt", "w") as fo:
     for name, cs in sorted(agg.items()):

@@ -255,15 +255,14 @@ def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
     a = u.to(gpu)
     lib = hip_lib()
     try:
-        for cpl, dma in ((4, 0), (8, 0), (8, 1)):  # dma: the LDS-DMA prefetch ring (8-column lanes)
-            assert lib.pcmx_stencil_lab_set(3, 0, dma) == 0
+        for cpl in (4, 8):
             for rpw in (2, 4, 7, 16, 18, 24, 32, 64, 67, 133):
                 assert lib.pcmx_stencil_lab_set(0, cpl, rpw) == 0 and lib.pcmx_stencil_lab_set(1, cpl, rpw) == 0
                 b = torch.zeros_like(a)
                 ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps)
-                assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16)), (cpl, rpw, dma)
+                assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16)), (cpl, rpw)
     finally:
-        lib.pcmx_stencil_lab_set(0, 0, 0), lib.pcmx_stencil_lab_set(1, 0, 0), lib.pcmx_stencil_lab_set(3, 0, 0)
+        lib.pcmx_stencil_lab_set(0, 0, 0), lib.pcmx_stencil_lab_set(1, 0, 0)
 
 
 @pytest.mark.parametrize("steps", [2, 4, 6])
