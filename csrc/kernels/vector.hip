@@ -82,6 +82,33 @@ __global__ __launch_bounds__(kThreads) void rand_uniform_kernel(float* x, long l
     }
 }
 
+// dst[i] = src[idx[i]] with 32-bit indices (the SpMV ghost exchange's send-buffer pack: per peer an ascending list of
+// this rank's rows). Each thread packs 4 consecutive entries: one 16-B index load, 4 gathers through a buffer
+// descriptor over src (an index outside [0, n_src) reads 0 instead of faulting), one 16-B store; the tail (n % 4)
+// by the first block. torch.index_select with int64 indices moved 8 B of index per entry: 21 us -> (this) for the 5.2M
+// entries of one N = 8 rank's step (scripts/spmv_host_lab.py).
+__global__ __launch_bounds__(kThreads) void gather_kernel(const float* __restrict__ src, long long n_src,
+                                                          const int* __restrict__ idx, float* __restrict__ dst,
+                                                          long long n) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0,
+                                                      (int)(n_src < (1LL << 29) ? n_src * 4 : 0x7ffffffc), 0x00020000);
+    const long long n4 = n >> 2, stride = (long long)gridDim.x * kThreads;
+    const pcmx::i32x4* idx4 = reinterpret_cast<const pcmx::i32x4*>(idx);
+    f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
+    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += stride) {
+        const pcmx::i32x4 k = idx4[i];
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)k[q] * 4u, 0, 0));
+        dst4[i] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const long long i = (n4 << 2) + threadIdx.x;
+        dst[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)idx[i] * 4u, 0, 0));
+    }
+}
+
 inline int stream_grid(long long n, int per_thread) {
     long long blocks = ((n >> 2) + (long long)kThreads * per_thread - 1) / ((long long)kThreads * per_thread);
     if (blocks < 1) blocks = 1;
@@ -110,6 +137,14 @@ extern "C" int pcmx_axpy_f32(float alpha, const float* x, float* y, long long n,
     if (n <= 0) return 0;
     if (!aligned16(x) || !aligned16(y)) return -1;
     axpy_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(alpha, x, y, n);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_gather_f32(const float* src, long long n_src, const int* idx, float* dst, long long n,
+                               hipStream_t s) {
+    if (n <= 0) return 0;
+    if (!aligned16(idx) || !aligned16(dst) || n_src <= 0 || n_src >= (1LL << 29)) return -1;
+    gather_kernel<<<stream_grid(n, 1), kThreads, 0, s>>>(src, n_src, idx, dst, n);
     return (int)hipGetLastError();
 }
 

@@ -58,6 +58,19 @@ at::Tensor vadd(const at::Tensor& a, const at::Tensor& b) {
     return r;
 }
 
+at::Tensor gather_(const at::Tensor& src, const at::Tensor& idx, at::Tensor out) {
+    check_gpu(src, "src", at::kFloat), check_gpu(idx, "idx", at::kInt), check_gpu(out, "out", at::kFloat);
+    TORCH_CHECK(src.is_contiguous() && idx.is_contiguous() && out.is_contiguous() && idx.numel() == out.numel(),
+                "gather_: contiguous src / idx / out, out.numel() == idx.numel()");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(idx.data_ptr()) & 15u) == 0 && (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15u) == 0,
+                "gather_: idx and out must be 16-B aligned");
+    const at::DeviceGuard g(src.device());
+    check_rc(pcmx_gather_f32(src.data_ptr<float>(), src.numel(), idx.data_ptr<int>(), out.data_ptr<float>(), out.numel(),
+                             cur_stream(src)),
+             "gather_");
+    return out;
+}
+
 at::Tensor axpy_(at::Tensor y, double alpha, const at::Tensor& x) {
     check_gpu(y, "y", at::kFloat), check_gpu(x, "x", at::kFloat);
     TORCH_CHECK(y.is_contiguous() && (reinterpret_cast<uintptr_t>(y.data_ptr()) & 15u) == 0, "axpy_: y must be contiguous, 16-B aligned");
@@ -595,6 +608,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("vmul(Tensor a, Tensor b) -> Tensor");
     m.def("vadd(Tensor a, Tensor b) -> Tensor");
     m.def("axpy_(Tensor(a!) y, float alpha, Tensor x) -> Tensor(a!)");
+    m.def("gather_(Tensor src, Tensor idx, Tensor(a!) out) -> Tensor(a!)");
     m.def("fill_(Tensor(a!) x, float v) -> Tensor(a!)");
     m.def("rand_uniform_(Tensor(a!) x, int seed, float lo, float hi) -> Tensor(a!)");
     m.def("reduce(Tensor x, int op) -> Tensor");
@@ -630,6 +644,7 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("vmul", vmul);
     m.impl("vadd", vadd);
     m.impl("axpy_", axpy_);
+    m.impl("gather_", gather_);
     m.impl("fill_", fill_);
     m.impl("rand_uniform_", rand_uniform_);
     m.impl("reduce", reduce);

@@ -43,6 +43,14 @@ def vadd(a: torch.Tensor, b: torch.Tensor, n_threads: int = 0) -> torch.Tensor:
     return r
 
 
+def gather_(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[i] = src[idx[i]] (int32 indices): the HIP gather kernel on the GPU (the SpMV send-buffer pack),
+    torch.index_select on the host."""
+    if src.is_cuda:
+        return ops().gather_(src, idx, out)
+    return torch.index_select(src, 0, idx.long(), out=out)
+
+
 def axpy_(y: torch.Tensor, alpha: float, x: torch.Tensor, n_threads: int = 0) -> torch.Tensor:
     """y <- alpha * x + y in place."""
     if y.is_cuda:

@@ -31,6 +31,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops.sparse import CSR, SlicedCSR, powerlaw_csr_rows, powerlaw_row_ptr, spmv
+from ..ops.vector import gather_
 from .dist import Context
 
 
@@ -221,7 +222,7 @@ class DistributedSpMV:
         gpos = pos[torch.searchsorted(need, g).clamp(max=max(0, need.numel() - 1))] if need.numel() else g
         out = torch.where(mine, own_pos, gpos).to(torch.int32)
         self.ghost_ids, self.ghost_pos = need, pos
-        self.send_idx, self.send_counts, self.sendbuf = [torch.zeros(0, dtype=torch.int64, device=dev)] * C, \
+        self.send_idx, self.send_counts, self.sendbuf = [torch.zeros(0, dtype=torch.int32, device=dev)] * C, \
             [[0] * W for _ in range(C)], [torch.zeros(0, device=dev)] * C
         if ctx.distributed:  # (a Context without a process group only emulates one rank's products)
             # send side: tell every owner which of its rows this rank needs (counts, then ids, owner-major)
@@ -237,7 +238,8 @@ class DistributedSpMV:
             self.send_idx, self.send_counts = [], []
             for c in range(C):
                 sel = gchunk == c  # owner-major order kept: peers in rank order, rows ascending
-                self.send_idx.append((got[sel] - c * L + self.seg[c * W + r]).contiguous())  # layout positions
+                # layout positions, int32: the pack kernel reads 4 B of index per entry (ops.gather_)
+                self.send_idx.append((got[sel] - c * L + self.seg[c * W + r]).to(torch.int32).contiguous())
                 self.send_counts.append(torch.bincount(peer[sel], minlength=W).tolist())
             self.sendbuf = [torch.empty(ix.numel(), dtype=torch.float32, device=dev) for ix in self.send_idx]
         self.n_ghost = int(need.numel())
@@ -330,7 +332,7 @@ class DistributedSpMV:
         host-launch bound (scripts/host_overhead_lab.py)."""
         W, r = self.ctx.world, self.ctx.rank
         if self.send_idx[c].numel():
-            torch.index_select(out, 0, self.send_idx[c], out=self.sendbuf[c])
+            gather_(out, self.send_idx[c], self.sendbuf[c])
         ins, outs, so = [], [], 0
         for q in range(W):
             ns = 0 if q == r else self.send_counts[c][q]

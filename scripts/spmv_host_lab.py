@@ -32,10 +32,12 @@ def main():
         k = max(1, d.ghost_len[c] // (Wd - 1))
         packs.append(torch.cat([s0 + torch.sort(torch.randperm(own, device=dev)[:min(k, own)]).values
                                 for _ in range(Wd - 1)]))
+    packs32 = [p.to(torch.int32) for p in packs]
     bufs = [torch.empty(p.numel(), device=dev) for p in packs]
+    from parallel_c_programs_amd.ops.vector import gather_
     print(f"send entries per step {sum(p.numel() for p in packs)}, ghosts received {d.n_ghost}", flush=True)
 
-    def step(pack=True):
+    def step(pack="gather"):
         for c, (a, b, part) in enumerate(d.parts):
             if b > a:
                 part.product_phase(xp, 0, c)
@@ -43,8 +45,10 @@ def main():
             s0 = d.seg[c * Wd + r]
             if b > a:
                 part.product_phase(xp, 1, c, out[s0:s0 + (b - a)])
-            if pack:
+            if pack == "index_select":
                 torch.index_select(out, 0, packs[c], out=bufs[c])
+            elif pack:
+                gather_(out, packs32[c], bufs[c])
 
     for _ in range(10):
         step()
@@ -65,6 +69,12 @@ def main():
     e1.record()
     e1.synchronize()
     print(f"N={W} products only (no packs): device {e0.elapsed_time(e1) / reps:.4f} ms/step", flush=True)
+    e0.record()
+    for _ in range(reps):
+        step("index_select")
+    e1.record()
+    e1.synchronize()
+    print(f"N={W} with torch.index_select (int64) packs: device {e0.elapsed_time(e1) / reps:.4f} ms/step", flush=True)
     print(f"N={W} rank 0 column-split step: host enqueue {host:.4f} ms/step, device {devt:.4f} ms/step "
           f"({'launch-bound' if host > devt else 'device-bound'}; + ~0.03 ms of host time for the 2 exchange calls)",
           flush=True)

@@ -485,3 +485,20 @@ def test_halo_pack_unpack(gpu, dtype):
     dg = torch.zeros_like(t).to(gpu)
     ops.unpack_halo_(dg, buf_ref.to(gpu))
     assert torch.equal(dg.cpu(), dst)
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 1_000_003])
+def test_gather_int32_vs_torch(gpu, n):
+    """The SpMV send-buffer pack: out[i] = src[idx[i]] with int32 indices (ascending runs, repeats, the n % 4 tail),
+    bit-equal to torch indexing; an index outside src reads 0."""
+    g = torch.Generator(device=gpu).manual_seed(n)
+    src = torch.rand(300_001, generator=g, device=gpu)
+    idx = torch.sort(torch.randint(0, src.numel(), (n,), generator=g, device=gpu)).values.to(torch.int32)
+    out = torch.empty(n, device=gpu)
+    ops.gather_(src, idx, out)
+    assert torch.equal(out, src[idx.long()])
+    if n >= 4:
+        bad = idx.clone()
+        bad[n // 2] = src.numel() + 5
+        ops.gather_(src, bad, out)
+        assert out[n // 2].item() == 0.0 and torch.equal(out[:n // 2], src[idx[:n // 2].long()])
