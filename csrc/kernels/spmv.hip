@@ -1000,9 +1000,13 @@ const pcmx::i32x4* banded_lut_table(const BandGeo& g) {
             tab[4 * ent + kk] = j + kk < 0 ? -j : j + kk < L ? kk + lut(j + kk) : kk - (L - 1) + lut(j + kk - L);
     }
     void* d = nullptr;
-    if (hipMalloc(&d, tab.size() * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMalloc(&d, tab.size() * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();  // (clear it: the caller falls back to variant 1 and reports that launch's status)
+        return nullptr;
+    }
     if (hipMemcpy(d, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(d);
+        (void)hipGetLastError();
         return nullptr;
     }
     cache.emplace(key, d);
@@ -1041,8 +1045,10 @@ int launch_banded_stream(const float* vals, const long long* row_off, int n, int
         }
         g.wbase[5] = wb;
     }
+    // (the first call per geometry allocates and fills the table with blocking HIP calls; if that is impossible — e.g.
+    // inside a stream capture — variant 1 runs instead)
     const pcmx::i32x4* lut_g = banded_lut_table(g);
-    if (!lut_g) return (int)hipErrorOutOfMemory;
+    if (!lut_g) return kStreamNotApplicable;
     const int nfront = rb_lo, back0 = rb_hi, nback = nrb - rb_hi;
     // first value of row rb_lo * RS: the nonzeros of the clipped rows before it (host sum of row lengths)
     long long off0 = 0;
