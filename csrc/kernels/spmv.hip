@@ -1081,11 +1081,13 @@ extern "C" int pcmx_spmv_banded_variant(const float* vals, const long long* row_
         return (int)hipGetLastError();
     }
     const int grid = (n + R - 1) / R;
-    if (variant == 8 || variant == 9) {
-        // 8: 16-row blocks (production), 9: 32-row blocks (lab: the per-block setup — x windows, slot table,
-        // barrier — amortised over twice the values, at 2x the value registers)
-        const int rc = variant == 8 ? launch_banded_stream<16, 10, 3>(vals, row_off, n, a, b, c, d, e, x, y, s)
-                                    : launch_banded_stream<32, 20, 4>(vals, row_off, n, a, b, c, d, e, x, y, s);
+    if (variant >= 8 && variant <= 11) {
+        // 8: 16-row blocks (production); lab: 9 = 32-row blocks (the per-block setup — x windows, slot table,
+        // barrier — amortised over twice the values, at 2x the value registers), 10 = 12-row, 11 = 24-row blocks
+        const int rc = variant == 8    ? launch_banded_stream<16, 10, 3>(vals, row_off, n, a, b, c, d, e, x, y, s)
+                       : variant == 9  ? launch_banded_stream<32, 20, 4>(vals, row_off, n, a, b, c, d, e, x, y, s)
+                       : variant == 10 ? launch_banded_stream<12, 8, 3>(vals, row_off, n, a, b, c, d, e, x, y, s)
+                                       : launch_banded_stream<24, 15, 3>(vals, row_off, n, a, b, c, d, e, x, y, s);
         if (rc == kStreamNotApplicable) return pcmx_spmv_banded_variant(vals, row_off, n, a, b, c, d, e, x, y, 1, s);
         return rc;
     }

@@ -317,7 +317,7 @@ def test_stencil_fused_spans_match_full(gpu, steps, spans):
                                   (3001, 301, 10, 50, 10, 3), (1500, 401, 200, 100, 200, 10)])
 def test_spmv_banded_variants_vs_host(gpu, dims):
     """Every banded kernel variant (0: wave per row; 1/4-7: LDS-staged windows, 4-B loads, block rows x rows in
-    flight; 8 / 9: block stream of 16 / 32 rows, 16-B loads over each row block's contiguous values) against the host product: interior
+    flight; 8 / 9 / 10 / 11: block stream of 16 / 32 / 12 / 24 rows, 16-B loads over each row block's contiguous values) against the host product: interior
     rows, rows clipped at both matrix edges (n smaller than the band reach: variant 8 then runs the variant-1 body in
     every block), a row block past the last row, rows longer than 16 x 64 nonzeros (1301 + 400 + 100: the dispatcher
     falls back to the wave-per-row kernel), and rows shorter than 256 nonzeros (variant 8 falls back to 1)."""
@@ -326,7 +326,7 @@ def test_spmv_banded_variants_vs_host(gpu, dims):
     x = ops.create_vector(n)
     ref = ops.spmv(m, x)
     vals, ro, xg = m.val.to(gpu), m.row_ptr.to(gpu), x.to(gpu)
-    for v in (0, 1, 4, 5, 6, 7, 8, 9):
+    for v in (0, 1, 4, 5, 6, 7, 8, 9, 10, 11):
         out = ops.spmv_banded(vals, ro, *dims, xg, variant=v).cpu()
         assert (out - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item()), (v, dims)
 
