@@ -458,27 +458,12 @@ __global__ __launch_bounds__(256) void spmv_fixup_kernel(const float* __restrict
     if (k >= n_fix) return;
     const int row = fix[k].y;
     if (k > 0 && fix[k - 1].y == row) return;
-    // a row's entries are contiguous: the run ends in the first stripe with a gap. Four stripes (256 entries) per
-    // turn, every index and value load of the turn issued before any is used: a hub row's run costs two dependent
-    // load round trips per 256 entries instead of two per 64.
     float acc = 0.f;
-    for (int j0 = k;; j0 += 4 * kWave) {
-        int2 f[4];
-        bool in[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = j0 + q * kWave + lane;
-            f[q] = j < n_fix ? fix[j] : int2{0, -1};
-        }
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            in[q] = f[q].y == row;
-            v[q] = in[q] ? extra[f[q].x] : 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc += v[q];
-        if (__builtin_amdgcn_ballot_w64(!in[3]) != 0) break;  // (entries past a gap belong to later rows: in = false)
+    for (int j0 = k;; j0 += kWave) {  // a row's entries are contiguous: the run ends in the first stripe with a gap
+        const int j = j0 + lane;
+        const bool in = j < n_fix && fix[j].y == row;
+        if (in) acc += extra[fix[j].x];
+        if (__builtin_amdgcn_ballot_w64(!in) != 0) break;
     }
     acc = pcmx::wave_reduce<float, 0>(acc);
     if (lane == 0) y[row] += acc;
