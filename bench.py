@@ -69,7 +69,7 @@ def parse(argv=None):
     ap.add_argument("--stencil-fuse", type=int, default=0,
                     help="fused updates per kernel / halo depth (0: by slab height, 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8)")
     ap.add_argument("--stencil-halo-mult", type=int, default=0,
-                    help="deep halo: m x fuse halo rows exchanged every m steps (0: 2 at N > 1, 1 at N = 1)")
+                    help="deep halo: m x fuse halo rows exchanged every m steps (0: auto, 3 on slabs of <= 3072 rows at N > 1, else 1)")
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
     ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")

@@ -6,6 +6,7 @@ exchange, for the launch shapes a step can take:
   split3    interior launch + one launch per edge band (round-2 step)
   split2    interior launch + both edge bands in ONE two-span launch
   split2c   split2 with the edge launch on a side stream, concurrent with the interior kernel
+  deep3     the same with m = 3 (3T halo rows: one exchange + one edge launch per 3 steps; time per step)
   deep2     the deep-halo schedule (StencilSlab halo_mult=2): per 2 steps an interior launch + one edge launch over
             the two 2T-row halo-dependent bands, then ONE launch over the own rows; the time is per step (pair / 2)
 
@@ -90,10 +91,25 @@ def main():
             ref3 = ref2.clone()
             ops.stencil5_fused_step_(ref2, ref3, row0, N, halo=2 * T, steps=T, row_range=(0, rows))
 
+            # deep halo m = 3: 3T halo rows, one exchange + one edge launch per 3 steps
+            u3 = (torch.rand(rows + 6 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
+            p3, q3, r3 = u3.clone(), u3.clone(), u3.clone()
+
+            def deep3():
+                ops.stencil5_fused_step_(u3, p3, row0, N, halo=3 * T, steps=T, row_range=(T, rows - T))
+                ops.stencil5_fused_spans_(u3, p3, ((-2 * T, T), (rows - T, rows + 2 * T)), row0, N, halo=3 * T, steps=T)
+                ops.stencil5_fused_step_(p3, q3, row0, N, halo=3 * T, steps=T, row_range=(-T, rows + T))
+                ops.stencil5_fused_step_(q3, r3, row0, N, halo=3 * T, steps=T, row_range=(0, rows))
+
+            s1, s2, s3 = u3.clone(), u3.clone(), u3.clone()
+            ops.stencil5_fused_step_(u3, s1, row0, N, halo=3 * T, steps=T, row_range=(-2 * T, rows + 2 * T))
+            ops.stencil5_fused_step_(s1, s2, row0, N, halo=3 * T, steps=T, row_range=(-T, rows + T))
+            ops.stencil5_fused_step_(s2, s3, row0, N, halo=3 * T, steps=T, row_range=(0, rows))
+
             full()
             res = {}
             for name, fn in (("full", full), ("split3", split3), ("split2", split2), ("split2c", split2c),
-                             ("deep2", deep2)):
+                             ("deep2", deep2), ("deep3", deep3)):
                 out.zero_()
                 fn()
                 torch.cuda.synchronize()
@@ -101,13 +117,17 @@ def main():
                     same = torch.equal(w2[2 * T:-2 * T], ref3[2 * T:-2 * T])
                     res[name] = (timed(fn) / 2, same)
                     continue
+                if name == "deep3":
+                    same = torch.equal(r3[3 * T:-3 * T], s3[3 * T:-3 * T])
+                    res[name] = (timed(fn) / 3, same)
+                    continue
                 same = name == "full" or torch.equal(out[T:-T], ref[T:-T])
                 res[name] = (timed(fn), same)
             line = " ".join(f"{k} {ms:.4f} ms {rows * N * T / ms / 1e6:7.0f} GLUP/s{'' if ok else ' MISMATCH'}"
                             for k, (ms, ok) in res.items())
             tag = f" rpw={rpw}" if rpw else ""
             print(f"fuse={T} N={world} rows={rows:5d}{tag}  {line}", flush=True)
-            del u, ref, out, u2, v2, w2, ref2, ref3
+            del u, ref, out, u2, v2, w2, ref2, ref3, u3, p3, q3, r3, s1, s2, s3
             torch.cuda.empty_cache()
     hip_lib().pcmx_stencil_lab_set(0, 0, 0)
 
