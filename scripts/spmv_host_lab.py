@@ -19,8 +19,11 @@ def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     dev = torch.device("cuda", 0)
-    d = DistributedSpMV.powerlaw(Context(rank=0, world=W, device=dev), 10_000_000, 100_000_000, slices=16, chunks=2,
-                                 item_nnz=512, colsplit=True)
+    item = int(os.environ.get("SPMV_LAB_ITEM", "512"))
+    slices = int(os.environ.get("SPMV_LAB_SLICES", "16"))
+    d = DistributedSpMV.powerlaw(Context(rank=0, world=W, device=dev), 10_000_000, 100_000_000, slices=slices, chunks=2,
+                                 item_nnz=item, colsplit=True)
+    print(f"item_nnz {item}, slices {slices}", flush=True)
     xp = torch.rand(d.n_pad, device=dev)
     out = torch.zeros_like(xp)
     Wd, r = d.ctx.world, d.ctx.rank
@@ -107,6 +110,21 @@ def main():
     e1.synchronize()
     print(f"N={W} chunk 0's combine + pack on a side stream beside chunk 1's products: device "
           f"{e0.elapsed_time(e1) / reps:.4f} ms/step", flush=True)
+    for pb in (1, 2, 3, 4, 6, 8):  # resident sliced blocks per CU of the product launches (kernel mode bits 8-15)
+        def products_pb():
+            for ph in (0, 1):
+                for c, (a, b, part) in enumerate(d.parts):
+                    half = part.n_slices // 16
+                    part.spmv(xp, mode=16 | (pb << 8), phases=(ph * half, half))
+        for _ in range(3):
+            products_pb()
+        e0.record()
+        for _ in range(reps):
+            products_pb()
+        e1.record()
+        e1.synchronize()
+        print(f"N={W} the 4 product launches alone, {pb} resident blocks per CU: {e0.elapsed_time(e1) / reps:.4f} ms/step",
+              flush=True)
     print(f"N={W} rank 0 column-split step: host enqueue {host:.4f} ms/step, device {devt:.4f} ms/step "
           f"({'launch-bound' if host > devt else 'device-bound'}; + ~0.03 ms of host time for the 2 exchange calls)",
           flush=True)
