@@ -106,16 +106,40 @@ def main():
             ops.stencil5_fused_step_(s1, s2, row0, N, halo=3 * T, steps=T, row_range=(-T, rows + T))
             ops.stencil5_fused_step_(s2, s3, row0, N, halo=3 * T, steps=T, row_range=(0, rows))
 
+            # deep halo m = 4 (generic form of deep2 / deep3)
+            M4 = 4
+            u4 = (torch.rand(rows + 2 * M4 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
+            b4 = [u4.clone() for _ in range(M4 + 1)]
+
+            def deep4():
+                e0 = (M4 - 1) * T
+                ops.stencil5_fused_step_(b4[0], b4[1], row0, N, halo=M4 * T, steps=T, row_range=(T, rows - T))
+                ops.stencil5_fused_spans_(b4[0], b4[1], ((-e0, T), (rows - T, rows + e0)), row0, N, halo=M4 * T,
+                                          steps=T)
+                for ph in range(1, M4):
+                    e = (M4 - 1 - ph) * T
+                    ops.stencil5_fused_step_(b4[ph], b4[ph + 1], row0, N, halo=M4 * T, steps=T, row_range=(-e, rows + e))
+
+            c4 = [u4.clone() for _ in range(M4 + 1)]
+            for ph in range(M4):
+                e = (M4 - 1 - ph) * T
+                ops.stencil5_fused_step_(c4[ph], c4[ph + 1], row0, N, halo=M4 * T, steps=T, row_range=(-e, rows + e))
+
             full()
             res = {}
             for name, fn in (("full", full), ("split3", split3), ("split2", split2), ("split2c", split2c),
-                             ("deep2", deep2), ("deep3", deep3)):
+                             ("deep2", deep2), ("deep3", deep3), ("deep4", deep4)):
                 out.zero_()
                 fn()
                 torch.cuda.synchronize()
                 if name == "deep2":
                     same = torch.equal(w2[2 * T:-2 * T], ref3[2 * T:-2 * T])
                     res[name] = (timed(fn) / 2, same)
+                    continue
+                if name == "deep4":
+                    hh = M4 * T
+                    same = torch.equal(b4[M4][hh:-hh], c4[M4][hh:-hh])
+                    res[name] = (timed(fn) / M4, same)
                     continue
                 if name == "deep3":
                     same = torch.equal(r3[3 * T:-3 * T], s3[3 * T:-3 * T])
@@ -127,7 +151,7 @@ def main():
                             for k, (ms, ok) in res.items())
             tag = f" rpw={rpw}" if rpw else ""
             print(f"fuse={T} N={world} rows={rows:5d}{tag}  {line}", flush=True)
-            del u, ref, out, u2, v2, w2, ref2, ref3, u3, p3, q3, r3, s1, s2, s3
+            del u, ref, out, u2, v2, w2, ref2, ref3, u3, p3, q3, r3, s1, s2, s3, u4, b4, c4
             torch.cuda.empty_cache()
     hip_lib().pcmx_stencil_lab_set(0, 0, 0)
 
