@@ -50,8 +50,11 @@ def main(argv=None) -> int:
         ms = device_time_ms(fn)
         cold = []
         for _ in range(5):
-            scrub.sum()
             torch.cuda.synchronize()
+            # the scrub is still running when the call is enqueued: s0 fires as it ends, with the call already
+            # queued behind it, so the time is the kernel's own (an idle GPU would also count the host's launch
+            # latency between s0 and the kernel)
+            scrub.sum()
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
             fn()

@@ -33,7 +33,8 @@ def test_vmul_reference_demo(gpu):
     torch.testing.assert_close(r, torch.ones_like(r), atol=1e-6, rtol=0)
 
 
-@pytest.mark.parametrize("n", [1, 7, 4096, 123457, 1 << 24])
+# first-pass partial counts 1, 1, 1, 31, 1221, 4096, 16384 (the cap): pass 2 folds float4s plus a 0-3 tail
+@pytest.mark.parametrize("n", [1, 7, 4096, 123457, 5_000_011, 1 << 24, (1 << 26) + 3])
 def test_reduce_sum_min_max(gpu, n):
     x = torch.randn(n, device=gpu)
     ref = x.double().sum().item()
@@ -43,6 +44,7 @@ def test_reduce_sum_min_max(gpu, n):
     xi = torch.randint(-1000, 1000, (n,), device=gpu, dtype=torch.int32)
     assert ops.reduce(xi, "sum").item() == xi.long().sum().item()
     assert ops.reduce(xi, "min").item() == xi.min().item()
+    assert ops.reduce(xi, "max").item() == xi.max().item()
 
 
 def test_reduce_deterministic(gpu):
