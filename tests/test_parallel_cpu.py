@@ -563,3 +563,25 @@ def test_run_workload_failed_check_exits_1(monkeypatch):
     with pytest.raises(SystemExit) as e:
         run_workload.run("histeq", ["--steps", "1", "--warmup", "0", "--device", "cpu", "--set", "side=64"])
     assert e.value.code == 1
+
+
+def test_auto_halo_mult_rule():
+    """Deep halo m = 3 only on short distributed slabs (the N = 8 rank of the 16384-row bench grid), else 1."""
+    from parallel_c_programs_amd.parallel.stencil import auto_halo_mult
+
+    assert auto_halo_mult(2048, 6, 8) == 3 and auto_halo_mult(2048, 8, 8) == 3
+    assert auto_halo_mult(3072, 6, 4) == 3
+    assert auto_halo_mult(4096, 6, 4) == 1 and auto_halo_mult(8192, 8, 2) == 1  # taller slabs: m = 1
+    assert auto_halo_mult(2048, 6, 1) == 1  # one rank: no exchange to amortise
+    assert auto_halo_mult(2048, 1, 8) == 1  # single-step launches
+    assert auto_halo_mult(40, 6, 8) == 1  # slab shorter than 8 fused levels
+
+
+def test_gather_host_path_matches_index():
+    """ops.gather_ (the SpMV send-buffer pack) on the host: out[i] = src[idx[i]] with int32 indices."""
+    g = torch.Generator().manual_seed(3)
+    src = torch.rand(1000, generator=g)
+    idx = torch.randint(0, 1000, (257,), generator=g, dtype=torch.int32)
+    out = torch.empty(257)
+    ops.gather_(src, idx, out)
+    assert torch.equal(out, src[idx.long()])
