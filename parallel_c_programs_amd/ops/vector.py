@@ -45,8 +45,9 @@ def vadd(a: torch.Tensor, b: torch.Tensor, n_threads: int = 0) -> torch.Tensor:
 
 def gather_(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     """out[i] = src[idx[i]] (int32 indices): the HIP gather kernel on the GPU (the SpMV send-buffer pack),
-    torch.index_select on the host."""
-    if src.is_cuda:
+    torch.index_select on the host. The kernel addresses src with 32-bit byte offsets: a src of 2^29 or more floats
+    takes torch.index_select on the GPU too."""
+    if src.is_cuda and src.numel() < (1 << 29):
         return ops().gather_(src, idx, out)
     return torch.index_select(src, 0, idx.long(), out=out)
 
