@@ -132,6 +132,27 @@ def test_t6_matrix_demo_stdout():
     assert "Matrix m is sparse: 0" in fixed  # B1 fixed by default
 
 
+def test_matrix_gemm_mode_host():
+    """run_matrix --gemm: the matrix_t multiply at N^3 through the host backend, every element vs fp64."""
+    import json
+
+    r = json.loads(run_cli("run_matrix", "--gemm", 96, "--reps", 1, "--device", "cpu").stdout.splitlines()[-1])
+    assert r["n"] == 96 and r["device"] == "cpu" and r["check_passed"] and r["max_rel_err_vs_fp64"] < 1e-5
+
+
+def test_device_info_json_and_arch_gate_without_gpu():
+    import json
+
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("host-only expectations")
+    r = json.loads(run_cli("run_device_info", "--json").stdout.splitlines()[-1])
+    assert r == {"device_count": 0, "devices": [], "peer_access": []}
+    assert run_cli("run_device_info", "--require-arch", "gfx950", check=False).returncode == 1
+    assert run_cli("run_device_info", "--probe", check=False).returncode == 1
+
+
 def test_t7_vmul_demo():
     i = torch.arange(1024, dtype=torch.float32)
     r = ops.vmul(i + 1, 1.0 / (i + 1))

@@ -73,6 +73,28 @@ def test_raycast_cli_cuda_variant(gpu, tmp_path):
     assert img.shape == (512, 512) and img.max() > 0
 
 
+def test_matrix_gemm_mode_gpu(gpu):
+    """run_matrix --gemm on the GPU backend (the f32-MFMA kernel): every element vs fp64, rc 0."""
+    import json
+
+    r = run_cli("run_matrix", "--gemm", 1024, "--reps", 3)
+    d = json.loads(r.stdout.splitlines()[-1])
+    assert d["device"].startswith("cuda") and d["check_passed"] and d["tflops"] > 1.0
+
+
+def test_device_info_json_arch_and_probe_gpu(gpu):
+    import json
+
+    d = json.loads(run_cli("run_device_info", "--json").stdout.splitlines()[-1])
+    assert d["device_count"] >= 1 and d["devices"][0]["arch"].startswith("gfx950")
+    assert d["peer_access"][0][0] is True
+    assert run_cli("run_device_info", "--require-arch", "gfx950").returncode == 0
+    assert run_cli("run_device_info", "--require-arch", "gfx942", check=False).returncode == 1
+    p = [json.loads(ln) for ln in run_cli("run_device_info", "--probe").stdout.splitlines() if ln.startswith("{")]
+    assert len(p) == d["device_count"]
+    assert p[0]["hbm_read_gbps"] > 1000 and p[0]["hbm_write_gbps"] > 1000 and p[0]["sgemm_4096_tflops"] > 10
+
+
 def test_spmv_cli_gpu(gpu):
     r = run_cli("run_spmv", 20000, 41, 20, 10, 20, 10, "--gpu")
     lines = r.stdout.splitlines()
