@@ -36,8 +36,10 @@ Checks are ENFORCED: fp64-referenced errors must be <= 1e-5 (workloads.REL_ERR_L
 failing check adds "<section>_check_failed" (the failing keys) to the line; a section that raises adds
 "<section>_error". Either way the line is still printed once by rank 0, every rank records the same outcome (a
 collective decision on a separate CPU process group at the end of each section: a failure local to one rank cannot
-pair with a data collective another rank waits in), and the run exits 1. `--inject-fault SECTION:RANK:KIND`
-(KIND perturb = corrupt that rank's timed output after timing, raise = raise in its check) is the test hook.
+pair with a data collective another rank waits in; a rank that fails before a timed region stops the others at the
+next decision point, Runner), and the run exits 1. `--inject-fault SECTION:RANK:KIND` (KIND perturb = corrupt that
+rank's timed output after timing, raise = raise in its check, raise-early = raise right after its set-up, before the
+timed region) is the test hook.
 
 rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra fields
 of the same line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
@@ -60,7 +62,9 @@ SECTIONS = ("sgemm", "reduce", "scan", "stencil", "spmv")
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1); N > 1 without a launcher "
+                         "starts torch.distributed.run itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=8192, help="SGEMM M=N=K")
@@ -85,7 +89,8 @@ def parse(argv=None):
                          "rank's GPU kernels with host-staged messages: N ranks may share ONE GPU (tests of the N>1 "
                          "path)")
     ap.add_argument("--inject-fault", default=None, metavar="SECTION:RANK:KIND",
-                    help="test hook: KIND perturb (corrupt that rank's timed output) or raise (raise in its check)")
+                    help="test hook: KIND perturb (corrupt that rank's timed output), raise (raise in its check) or "
+                         "raise-early (raise after its set-up, before the timed region)")
     a = ap.parse_args(argv)
     if a.small:
         a.size, a.reduce_n, a.stencil_n, a.spmv_rows, a.spmv_nnz = 256, 1e5, 256, 2e4, 2e5
@@ -168,9 +173,19 @@ class Checks:
         self.items[key] = (value, agg, None)
 
 
+class PeerFailed(Exception):
+    """Raised at a decision point when another rank's section has already failed."""
+
+
 class Runner:
-    """Runs bench sections; at the end of each one every rank joins ONE decision on a separate gloo group (each
-    rank's error and local check values), so all ranks record the same outcome and go on together."""
+    """Runs bench sections. A section is a generator: every `yield` is a DECISION POINT (before each timed region and
+    before the checks), where all ranks join one all_gather_object on a separate gloo group. A rank whose section
+    raised no longer yields: it enters the FINAL exchange (its error and local check values), repeated until every
+    rank is final. A healthy rank that meets a failed peer's final message at a decision point stops its section there
+    (PeerFailed) and turns final too, so a rank that failed early is reported and the others do not walk into a data
+    collective it will never join. All ranks then merge the same final states and record the same outcome. (A failure
+    INSIDE a data collective sequence — one rank raising between two collectives with no decision point in between —
+    still ends the job through the process group's timeout, PCMX_PG_TIMEOUT_S.)"""
 
     def __init__(self, ctx, out: dict, fault: str | None, log):
         from parallel_c_programs_amd.parallel.dist import side_group
@@ -181,15 +196,15 @@ class Runner:
         self.fault = None
         if fault:
             sec, rank, kind = fault.split(":")
-            if kind not in ("perturb", "raise"):
-                raise ValueError("--inject-fault SECTION:RANK:perturb|raise")
+            if kind not in ("perturb", "raise", "raise-early"):
+                raise ValueError("--inject-fault SECTION:RANK:perturb|raise|raise-early")
             self.fault = (sec, int(rank), kind)
 
     def injected(self, section: str, kind: str) -> bool:
         return self.fault is not None and self.fault == (section, self.ctx.rank, kind)
 
-    def maybe_raise(self, section: str):
-        if self.injected(section, "raise"):
+    def maybe_raise(self, section: str, kind: str = "raise"):
+        if self.injected(section, kind):
             raise RuntimeError(f"injected fault in {section} on rank {self.ctx.rank}")
 
     def run(self, name: str, fn) -> None:
@@ -197,19 +212,27 @@ class Runner:
 
         chk, err = Checks(), None
         try:
-            fn(chk)
+            for _ in fn(chk):  # a decision point
+                states = gather_objects(("point", None, None), self.side)
+                bad = [r for r, (kind, e, _) in enumerate(states) if kind == "final"]
+                if bad:
+                    raise PeerFailed(f"rank {bad[0]} failed earlier in the section")
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             err = f"{type(e).__name__}: {e}"[:300]
         if self.ctx.device.type == "cuda":
             torch.cuda.empty_cache()  # (after the except block: no traceback pins the section's tensors)
-        states = gather_objects((err, chk.items), self.side)
-        errs = [(r, e) for r, (e, _) in enumerate(states) if e]
+        while True:  # the final exchange, until every rank has left its section
+            states = gather_objects(("final", err, chk.items), self.side)
+            if all(kind == "final" for kind, _, _ in states):
+                break
+        errs = [(r, e) for r, (_, e, _) in enumerate(states) if e and not e.startswith("PeerFailed")]
+        errs = errs or [(r, e) for r, (_, e, _) in enumerate(states) if e]
         if errs:
             r, e = errs[0]
             self.out[f"{name}_error"] = e if r == 0 and len(errs) == 1 else f"rank {r}: {e}" + (
                 f" (+{len(errs) - 1} more ranks)" if len(errs) > 1 else "")
         merged = {}
-        for _, items in states:
+        for _, _, items in states:
             for k, (v, agg, limit) in items.items():
                 if k not in merged:
                     merged[k] = (v, agg, limit)
@@ -239,9 +262,13 @@ def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
     world_env = os.environ.get("WORLD_SIZE")
-    if world_env is None and args.gpus > 1:
-        return launch(args, argv)
-    if world_env is not None and int(world_env) != args.gpus:
+    if world_env is None:
+        args.gpus = args.gpus or 1
+        if args.gpus > 1:
+            return launch(args, argv)
+    elif args.gpus is None:  # under a launcher without --gpus: its WORLD_SIZE ranks
+        args.gpus = int(world_env)
+    elif int(world_env) != args.gpus:  # --gpus given explicitly and different from the launcher's
         print(f"[bench] error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks",
               file=sys.stderr, flush=True)
         return 2
@@ -276,6 +303,8 @@ def main(argv=None):
 
     def sgemm(chk):
         g = W.Sgemm(ctx, n=n)
+        runner.maybe_raise("sgemm", "raise-early")
+        yield
         ms = []
         t = timed(ctx, g.step, K, Wm, ms)
         rep = g.report(t, K)
@@ -286,6 +315,7 @@ def main(argv=None):
             # the vendor library timed exactly like our kernel (same warm-up and step count), into its own buffer:
             # g.c keeps the output of our timed steps for the check
             cref = torch.empty_like(g.c)
+            yield
             t_ref = timed(ctx, lambda: torch.matmul(g.a, g.b, out=cref), K, Wm)
             out["hipblaslt_torch_matmul_tflops"] = _r(world * g.work_per_step() * K / t_ref / 1e12, 3)
             del cref
@@ -297,12 +327,14 @@ def main(argv=None):
             gx = W.Sgemm.__new__(W.Sgemm)
             gx.__dict__.update(g.__dict__)
             gx.variant, gx.c = 20, torch.empty_like(g.c)
+            yield
             ms6 = []
             t_x6 = timed(ctx, gx.step, K, Wm, ms6)
             out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * gx.work_per_step() * K / t_x6 / 1e12, 3)
             device_times(chk, "sgemm_fp32_via_bf16x6", ms6)
         if runner.injected("sgemm", "perturb"):
             g.c[n // 3, n // 5] += 1.0
+        yield
         runner.maybe_raise("sgemm")
         chk.error("sgemm_max_rel_err_vs_fp64", g.check(reduce=False)["max_rel_err_vs_fp64"], LIM)
         if x6:
@@ -324,6 +356,7 @@ def main(argv=None):
                 chk.error(f"{name}_strong_rel_err_vs_fp64", v, lim)
                 continue
             w = cls(ctx, n=per_rank)
+            yield
             ms = []
             t = timed(ctx, w.step, K, Wm, ms)
             rep = w.report(t, K)
@@ -332,6 +365,7 @@ def main(argv=None):
             device_times(chk, f"{name}_{mode}", ms)
             if mode == "weak" and not args.no_ref and dev.type == "cuda":
                 # the vendor library on the same per-GPU data, timed exactly like our kernel (rocPRIM behind both)
+                yield
                 if name == "reduce":
                     t_ref = timed(ctx, lambda: torch.sum(w.x), K, Wm)
                     out["torch_sum_gbps"] = _r(world * 4.0 * w.x.numel() * K / t_ref / 1e9, 1)
@@ -345,6 +379,7 @@ def main(argv=None):
                     w.total.mul_(1.001)
                 else:
                     w.y[w.y.numel() // 3] += 1.0
+            yield
             c = w.check(reduce=False)
             chk.error(f"{name}_{mode}_rel_err_vs_fp64", c["rel_err_vs_fp64"], LIM)
             if name == "scan":  # every timed output checked (not a prefix), rank offsets included
@@ -364,6 +399,8 @@ def main(argv=None):
     # ---- stencil 16384^2 bf16, strong scaling over row slabs with the overlapped fused halo exchange
     def stencil(chk):
         s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse, halo_mult=args.stencil_halo_mult)
+        runner.maybe_raise("stencil", "raise-early")
+        yield
         ms = []
         t = timed(ctx, s.step, K, Wm, ms)
         rep = s.report(t, K)
@@ -372,12 +409,15 @@ def main(argv=None):
         device_times(chk, "stencil", ms)
         if runner.injected("stencil", "perturb"):
             s.slab.interior()[s.slab.rows // 2, 7] += 1.0
+        yield
         c = s.check(reduce=False)  # (its small-grid distributed run first, then local-only work)
         runner.maybe_raise("stencil")
         out["stencil_timed_grid_updates"] = c["timed_grid_updates"]
         chk.flag("stencil_timed_grid_bit_exact", c["timed_grid_bit_exact"])
         chk.flag("stencil_bit_exact", c["bit_exact_vs_single_step_oracle"])
         chk.flag("stencil_finite", c["finite"])
+        if c["halo_selftest"] is not None:  # the deep halo proven on this backend before timing (N > 1)
+            out["stencil_halo_selftest_bit_exact"] = c["halo_selftest"]
         del s
         log(f"stencil {out['stencil_glups']} GLUP/s")
 
@@ -389,6 +429,8 @@ def main(argv=None):
         vendor = not args.no_ref and dev.type == "cuda"
         sp = W.SpMV(ctx, n_rows=int(args.spmv_rows), nnz=int(args.spmv_nnz), chunks=args.spmv_chunks,
                     exchange=args.spmv_exchange, keep_plain=vendor)
+        runner.maybe_raise("spmv", "raise-early")
+        yield
         ms = []
         t = timed(ctx, sp.step, K, Wm, ms)
         rep = sp.report(t, K)
@@ -398,6 +440,7 @@ def main(argv=None):
                     "spmv_colsplit": sp.d.colsplit})
         device_times(chk, "spmv", ms)
         if vendor:  # hipSPARSE (torch sparse CSR x dense vector) on each rank's own rows, the same matrix and x
+            yield
             try:
                 A = sp.d.vendor_matrix()
                 yv = torch.mv(A, sp.xp)
@@ -410,7 +453,14 @@ def main(argv=None):
                 out["torch_sparse_csr_gflops"] = f"unsupported on this torch build: {type(e).__name__}: {e}"[:200]
         if runner.injected("spmv", "perturb"):
             sp.y[0] += 1.0
-        chk.error("spmv_max_rel_err_vs_fp64", sp.check(reduce=False)["max_rel_err_vs_fp64"], LIM)
+        yield
+        c = sp.check(reduce=False)
+        chk.error("spmv_max_rel_err_vs_fp64", c["max_rel_err_vs_fp64"], LIM)
+        # chained steps x <- A x (the power-iteration pattern, exchanges deferred across step boundaries) vs fp64
+        chk.error("spmv_iterated_max_rel_err_vs_fp64", c["iterated_max_rel_err_vs_fp64"], LIM)
+        out["spmv_iterated_steps"], out["spmv_deferred_exchange"] = c["iterated_steps"], c["deferred"]
+        if c["pipeline_selftest"] is not None:  # deferred vs finished-in-step chained steps, bit for bit (N > 1)
+            out["spmv_pipeline_selftest_bit_identical"] = c["pipeline_selftest"]
         runner.maybe_raise("spmv")
         del sp
         log(f"spmv {out['spmv_gflops']} GFLOP/s")
@@ -425,6 +475,7 @@ def main(argv=None):
         import torch.distributed as dist
 
         v = torch.ones(64 << 20, device=dev)
+        yield
         kr = max(3, K // 2)
         t_ar = timed(ctx, lambda: dist.all_reduce(v), kr, 1)
         out["allreduce_256MiB_busbw_gbps"] = _r(v.numel() * 4 * 2 * (world - 1) / world * kr / t_ar / 1e9, 1)

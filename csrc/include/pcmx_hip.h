@@ -159,6 +159,11 @@ int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols, int ld, i
 int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0a,
                                int r1a, int r0b, int r1b, long long global_row0, long long global_rows, float k,
                                hipStream_t s);
+/* the same with an explicit launch shape of this launch (0 = production rule; bits 0-7 columns per lane 4 / 8, 8-15 rows
+ * per wave, 16-23 prefetch ring depth 3 / 6 / 9): the lab sweeps, no state kept in the library */
+int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0a,
+                                     int r1a, int r0b, int r1b, long long global_row0, long long global_rows, float k,
+                                     int shape, hipStream_t s);
 int pcmx_stencil5x2_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int r0, int r1,
                          long long global_row0, long long global_rows, float k, hipStream_t s);
 

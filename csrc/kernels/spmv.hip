@@ -854,18 +854,11 @@ extern "C" int pcmx_spmv_csr(const long long* row_ptr, const int* col, const flo
     return (int)hipGetLastError();
 }
 
-namespace {
-// temporal partial stores in the sliced product (default since round 4: the ~340 MB of compact partials are re-read
-// by the combine right after the product, and non-temporal stores evicted them early: 0.633-0.652 -> 0.628 ms per
-// step at 1e8 nnz, bit-identical; scripts/spmv_store_lab.py, profiles/r4_spmv/store_temporal_partials.txt).
-// pcmx_spmv_lab_set(0, 0) restores the nt stores.
-int g_spmv_ts = 1;
-}
-extern "C" int pcmx_spmv_lab_set(int key, int val) {
-    if (key != 0 || val < 0 || val > 1) return -1;
-    g_spmv_ts = val;
-    return 0;
-}
+// Partial stores of the sliced product are temporal (round 4: the ~340 MB of compact partials are re-read by the
+// combine right after the product, and non-temporal stores evicted them early: 0.633-0.652 -> 0.628 ms per step at
+// 1e8 nnz, bit-identical; scripts/spmv_store_lab.py, profiles/r4_spmv/store_temporal_partials.txt). mode bit 26 (lab,
+// an explicit per-call parameter): non-temporal partial stores instead.
+constexpr int kModeNtPartials = 1 << 26;
 
 extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x,
                                 float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
@@ -910,12 +903,12 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
 #define PCMX_SLICED(M, PL) spmv_sliced_kernel<M, PL><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp, ph_lo)
         // slice_colbase != NULL: col holds the packed words (production layout when every slice is < 2^21 columns)
         if (slice_colbase) {
-            // lab knob (pcmx_spmv_lab_set(0, 1)): temporal partial stores
 #define PCMX_SLICED_TS(M, PL) spmv_sliced_kernel<M, PL, true><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp, ph_lo)
+            const bool ts = !(mode & kModeNtPartials);
             if ((mode & 7) == 2)
-                (g_spmv_ts ? PCMX_SLICED_TS(12, 8) : PCMX_SLICED(12, 8));
+                (ts ? PCMX_SLICED_TS(12, 8) : PCMX_SLICED(12, 8));
             else if ((mode & 7) == 0)
-                (g_spmv_ts ? PCMX_SLICED_TS(12, 16) : PCMX_SLICED(12, 16));
+                (ts ? PCMX_SLICED_TS(12, 16) : PCMX_SLICED(12, 16));
             else
                 return (int)hipErrorInvalidValue;  // the lab modes read the unpacked layout
 #undef PCMX_SLICED_TS
@@ -976,10 +969,13 @@ constexpr int kStreamNotApplicable = -1000;
 // of one phase table: 16-B lane stride, no bank conflicts). lut4[j][kk] = kk + lut(j + kk), or past the row end
 // kk - (L - 1) + lut(j + kk - L) (the next row); the block's first float4 starts up to 3 values before its first element
 // (j < 0, row 0): those (zeroed) values read slot 0. Built on the host once per (device, geometry) and kept in device
-// memory for the life of the process (a few KB per geometry).
-const pcmx::i32x4* banded_lut_table(const BandGeo& g) {
+// memory for the life of the process (a few KB per geometry). The first call per geometry allocates and copies on
+// stream s (stream-ordered: the copy lands before the launch that reads it; the host table stays cached so the async
+// copy never reads freed memory). Inside a stream capture no HIP allocation may run: an uncached table returns nullptr
+// there and the caller launches variant 1 instead.
+const pcmx::i32x4* banded_lut_table(const BandGeo& g, hipStream_t s) {
     static std::mutex mu;
-    static std::map<std::vector<int>, void*> cache;
+    static std::map<std::vector<int>, std::pair<void*, std::vector<int>>> cache;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::vector<int> key{dev, g.L};
@@ -987,7 +983,13 @@ const pcmx::i32x4* banded_lut_table(const BandGeo& g) {
     key.insert(key.end(), g.cum, g.cum + 5);
     std::lock_guard<std::mutex> lock(mu);
     auto it = cache.find(key);
-    if (it != cache.end()) return reinterpret_cast<const pcmx::i32x4*>(it->second);
+    if (it != cache.end()) return reinterpret_cast<const pcmx::i32x4*>(it->second.first);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (cap != hipStreamCaptureStatusNone) return nullptr;
     const int L = g.L, ql = (L + 6) >> 2;
     auto lut = [&](int j) {  // window base - first position of j's band
         const int k = (j >= g.cum[1]) + (j >= g.cum[2]) + (j >= g.cum[3]) + (j >= g.cum[4]);
@@ -1004,12 +1006,15 @@ const pcmx::i32x4* banded_lut_table(const BandGeo& g) {
         (void)hipGetLastError();  // (clear it: the caller falls back to variant 1 and reports that launch's status)
         return nullptr;
     }
-    if (hipMemcpy(d, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+    auto& ent = cache[key];
+    ent.second = std::move(tab);
+    if (hipMemcpyAsync(d, ent.second.data(), ent.second.size() * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) {
+        cache.erase(key);
         (void)hipFree(d);
         (void)hipGetLastError();
         return nullptr;
     }
-    cache.emplace(key, d);
+    ent.first = d;
     return reinterpret_cast<const pcmx::i32x4*>(d);
 }
 // Variant 8/9 launch (block stream over the unclipped rows, the clipped row blocks folded into the same grid);
@@ -1045,9 +1050,9 @@ int launch_banded_stream(const float* vals, const long long* row_off, int n, int
         }
         g.wbase[5] = wb;
     }
-    // (the first call per geometry allocates and fills the table with blocking HIP calls; if that is impossible — e.g.
-    // inside a stream capture — variant 1 runs instead)
-    const pcmx::i32x4* lut_g = banded_lut_table(g);
+    // (the first call per geometry allocates the table and copies it on s; inside a stream capture, or if that fails,
+    // variant 1 runs instead)
+    const pcmx::i32x4* lut_g = banded_lut_table(g, s);
     if (!lut_g) return kStreamNotApplicable;
     const int nfront = rb_lo, back0 = rb_hi, nback = nrb - rb_hi;
     // first value of row rb_lo * RS: the nonzeros of the clipped rows before it (host sum of row lengths)

@@ -375,8 +375,16 @@ __device__ __forceinline__ void level_pairs(const RowP<NP>& n, const RowP<NP>& c
                                             RowP<NP>& nx, typename RawT<NP>::type& pk) {
     const f2 kk = f2{k, k}, m4 = f2{-4.f, -4.f};
     f2 we[NP];
+#ifndef PCMX_FAULT_INJECT
     const float em1 = pcmx::wave_from_prev(c.p[NP - 1].y);  // e_{-1}: previous lane's last element
-    const float eL = pcmx::wave_from_next(c.p[0].x);        // e_{2NP}: next lane's first element
+#else
+    // test-only build (libpcmx_faultinj.so): lane 17 of every strip takes its EAST neighbour e_1 as the west neighbour
+    // of its first column, a one-lane neighbour swap that is invisible on a constant grid (tests/test_gpu_errors.py:
+    // the bench's timed-grid check must catch it on the random grid)
+    float em1 = pcmx::wave_from_prev(c.p[NP - 1].y);
+    if (pcmx::lane_id() == 17) em1 = c.p[1].x;
+#endif
+    const float eL = pcmx::wave_from_next(c.p[0].x);  // e_{2NP}: next lane's first element
     // pair 0: (e_{-1} + e_1, e_{NP-1} + e_{NP+1}); pair NP-1: (e_{NP-2} + e_NP, e_{2NP-2} + e_{2NP})
     we[0] = f2{add_scalar(em1, c.p[1].x), add_scalar(c.p[NP - 1].x, c.p[1].y)};
 #pragma unroll
@@ -526,8 +534,6 @@ int strips_for(int cols, int cpl, int steps) {
     const int L = (steps + cpl - 1) / cpl, out = (64 - 2 * L) * cpl;
     return cols <= 64 * cpl ? 1 : 1 + (cols - 64 * cpl + out - 1) / out;
 }
-// lab override of the launch shape (0 = production rule): columns per lane, rows per wave
-int g_lab_cpl = 0, g_lab_rpw = 0, g_lab_edge_cpl = 0, g_lab_edge_rpw = 0, g_lab_ahead = 0;
 // Rows per wave for a short slab at T = 6 (4-column lanes): the smallest count >= 18 whose grid fits ONE residency
 // round of the chip (every workgroup resident at once), so no second, partly filled round of waves follows. One N = 8
 // rank's 2048-row slab: 29 rows per wave (1242 workgroups <= 256 CUs x 5) 0.0526 ms against 0.0567 with 18 (1.56
@@ -565,11 +571,18 @@ bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row
 // region (local rows -(halo - T) .. rows + halo - T): the deep-halo schedule of the distributed stencil computes
 // those rows redundantly so the next step needs no exchange (parallel/stencil.py); at a global edge spans are
 // clamped to [0, rows).
-extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, int cols, int ld, int halo, int steps,
-                                          int r0a, int r1a, int r0b, int r1b, long long global_row0,
-                                          long long global_rows, float k, hipStream_t s) {
+// shape: an EXPLICIT launch-shape override of this one launch (0 = the production rule below): bits 0-7 columns per
+// lane (4 / 8), bits 8-15 rows per wave (1 .. 255), bits 16-23 prefetch ring depth (3 / 6 / 9); each field 0 keeps the
+// rule's value. The lab scripts sweep shapes through it (scripts/stencil_*_lab.py); no launch state lives in the library.
+extern "C" int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int rows, int cols, int ld, int halo,
+                                                int steps, int r0a, int r1a, int r0b, int r1b, long long global_row0,
+                                                long long global_rows, float k, int shape, hipStream_t s) {
     if (rows <= 0 || cols <= 0 || ld < cols || (ld & 7) || (cols & 7) || halo < 1 || steps < 1 ||
         (((uintptr_t)u | (uintptr_t)out) & 15))
+        return -1;
+    const int o_cpl = shape & 0xff, o_rpw = (shape >> 8) & 0xff, o_ahead = (shape >> 16) & 0xff;
+    if ((o_cpl != 0 && o_cpl != 4 && o_cpl != 8) || (o_ahead != 0 && o_ahead != 3 && o_ahead != 6 && o_ahead != 9) ||
+        (shape >> 24) != 0)
         return -1;
     const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
     const int lo_lim = top_global ? 0 : -max(0, halo - steps), hi_lim = bot_global ? rows : rows + max(0, halo - steps);
@@ -614,13 +627,13 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
         cpl = steps == 8 ? 4 : 8, rpw = 32;
     else
         cpl = 8, rpw = steps <= 4 ? 24 : 64;
-    if (edge ? g_lab_edge_cpl : g_lab_cpl) cpl = edge ? g_lab_edge_cpl : g_lab_cpl;
-    if (edge ? g_lab_edge_rpw : g_lab_rpw) rpw = edge ? g_lab_edge_rpw : g_lab_rpw;
+    if (o_cpl) cpl = o_cpl;
+    if (o_rpw) rpw = o_rpw;
     if (steps == 2) cpl = 8, rpw = kRowsPerWave;  // T = 2: the HBM-bound v1 kernel, one shape
     if (steps == 3) cpl = 8;                      // T = 3: 8-column lanes only
     // prefetch ring depth (rows in flight per wave; a multiple of 3, see stencil5xT_body)
     int ahead = (steps >= 6 && rpw >= 64) ? 9 : (rpw <= 4 || (rpw > 16 && rpw <= 20)) ? 3 : 6;
-    if (g_lab_ahead) ahead = g_lab_ahead;
+    if (o_ahead) ahead = o_ahead;
     const int per = kWaves * rpw;
     const RowSpans sp{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per, rpw};
     const dim3 g(strips_for(cols, steps == 2 ? 8 : cpl, steps), sp.nby_a + (r1b - r0b + per - 1) / per);
@@ -658,20 +671,11 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
     return (int)hipGetLastError();
 }
 
-// Lab knob (scripts/stencil_lanes_lab.py, scripts/stencil_rpw_lab.py): force columns per lane (4 / 8) and rows per
-// wave (1 .. 256) of the fused v2 launches over more than 64 rows (which = 0) or of edge launches (which = 1), or
-// (which = 2, cpl ignored) the prefetch ring depth (3 / 6 / 9 rows); 0 restores the production rule. Host-global, not
-// thread-safe: labs only.
-extern "C" int pcmx_stencil_lab_set(int which, int cpl, int rpw) {
-    if (which == 2) {
-        if (rpw != 0 && rpw != 3 && rpw != 6 && rpw != 9) return -1;
-        g_lab_ahead = rpw;
-        return 0;
-    }
-    if ((cpl != 0 && cpl != 4 && cpl != 8) || rpw < 0 || rpw > 256 || (which != 0 && which != 1)) return -1;
-    (which ? g_lab_edge_cpl : g_lab_cpl) = cpl;
-    (which ? g_lab_edge_rpw : g_lab_rpw) = rpw;
-    return 0;
+extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, int cols, int ld, int halo, int steps,
+                                          int r0a, int r1a, int r0b, int r1b, long long global_row0,
+                                          long long global_rows, float k, hipStream_t s) {
+    return pcmx_stencil5xT_bf16_spans_shape(u, out, rows, cols, ld, halo, steps, r0a, r1a, r0b, r1b, global_row0,
+                                            global_rows, k, 0, s);
 }
 
 // T fused updates over local rows [r0, r1) of a slab with `halo` rows above and below (T = 2, 3, 4, 6, 8).

@@ -450,28 +450,30 @@ void stencil5_(const at::Tensor& u, at::Tensor out, int64_t r0, int64_t r1, int6
 }
 
 void stencil5xT_(const at::Tensor& u, at::Tensor out, int64_t halo, int64_t steps, int64_t r0, int64_t r1,
-                 int64_t global_row0, int64_t global_rows, double k) {
+                 int64_t global_row0, int64_t global_rows, double k, int64_t shape) {
     check_gpu(u, "u", at::kBFloat16), check_gpu(out, "out", at::kBFloat16);
     TORCH_CHECK(u.dim() == 2 && u.sizes() == out.sizes() && u.is_contiguous() && out.is_contiguous() && halo >= 1 &&
                     u.size(0) > 2 * halo,
                 "stencil5xT: slabs of shape (rows + 2*halo, cols)");
     const at::DeviceGuard g(u.device());
     const int rows = (int)(u.size(0) - 2 * halo), cols = (int)u.size(1);
-    check_rc(pcmx_stencil5xT_bf16(u.data_ptr(), out.data_ptr(), rows, cols, cols, (int)halo, (int)steps, (int)r0, (int)r1,
-                                  global_row0, global_rows, (float)k, cur_stream(u)),
+    check_rc(pcmx_stencil5xT_bf16_spans_shape(u.data_ptr(), out.data_ptr(), rows, cols, cols, (int)halo, (int)steps,
+                                              (int)r0, (int)r1, 0, 0, global_row0, global_rows, (float)k, (int)shape,
+                                              cur_stream(u)),
              "stencil5xT_");
 }
 
 void stencil5xT_spans_(const at::Tensor& u, at::Tensor out, int64_t halo, int64_t steps, int64_t r0a, int64_t r1a,
-                       int64_t r0b, int64_t r1b, int64_t global_row0, int64_t global_rows, double k) {
+                       int64_t r0b, int64_t r1b, int64_t global_row0, int64_t global_rows, double k, int64_t shape) {
     check_gpu(u, "u", at::kBFloat16), check_gpu(out, "out", at::kBFloat16);
     TORCH_CHECK(u.dim() == 2 && u.sizes() == out.sizes() && u.is_contiguous() && out.is_contiguous() && halo >= 1 &&
                     u.size(0) > 2 * halo,
                 "stencil5xT_spans: slabs of shape (rows + 2*halo, cols)");
     const at::DeviceGuard g(u.device());
     const int rows = (int)(u.size(0) - 2 * halo), cols = (int)u.size(1);
-    check_rc(pcmx_stencil5xT_bf16_spans(u.data_ptr(), out.data_ptr(), rows, cols, cols, (int)halo, (int)steps, (int)r0a,
-                                        (int)r1a, (int)r0b, (int)r1b, global_row0, global_rows, (float)k, cur_stream(u)),
+    check_rc(pcmx_stencil5xT_bf16_spans_shape(u.data_ptr(), out.data_ptr(), rows, cols, cols, (int)halo, (int)steps,
+                                              (int)r0a, (int)r1a, (int)r0b, (int)r1b, global_row0, global_rows, (float)k,
+                                              (int)shape, cur_stream(u)),
              "stencil5xT_spans_");
 }
 
@@ -631,8 +633,8 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
     m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, int batch=0, int segments=0) -> Tensor");
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
-    m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
-    m.def("stencil5xT_spans_(Tensor u, Tensor(a!) out, int halo, int steps, int r0a, int r1a, int r0b, int r1b, int global_row0, int global_rows, float k) -> ()");
+    m.def("stencil5xT_(Tensor u, Tensor(a!) out, int halo, int steps, int r0, int r1, int global_row0, int global_rows, float k, int shape=0) -> ()");
+    m.def("stencil5xT_spans_(Tensor u, Tensor(a!) out, int halo, int steps, int r0a, int r1a, int r0b, int r1b, int global_row0, int global_rows, float k, int shape=0) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
     m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor row_mask, Tensor chunk_base, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None, int mode=0) -> Tensor");
     m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x, int variant=8) -> Tensor");

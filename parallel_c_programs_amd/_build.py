@@ -6,7 +6,8 @@ Artefacts (all git-ignored, all shipped to the GPU box by gpurun's snapshot):
   parallel_c_programs_amd/_C.so                torch op registrations (TORCH_LIBRARY(pcmx, ...))
   bin/<tool>                                   reference-style CLIs (spmv, histogram_*, matrix_demo, ...)
   parallel_c_programs_amd/lib/libpcmx_faultinj.so  TEST ONLY: kernels built with -DPCMX_FAULT_INJECT (a forced
-                                               scan look-back stall) so tests can observe the error paths
+                                               scan look-back stall, a one-lane stencil neighbour swap) so tests can
+                                               observe the error paths and the power of the checks
 
 Everything is compiled for gfx950 only (`--offload-arch=gfx950`). Native libraries link the HIP runtime
 that ships inside torch (torch/lib/libamdhip64.so, same SONAME as /opt/rocm's) with an rpath to it, so a
@@ -122,7 +123,7 @@ def build_hip(force=False, jobs=8):
     return so
 
 
-FAULT_SRCS = ["kernels/scan.hip"]
+FAULT_SRCS = ["kernels/scan.hip", "kernels/stencil.hip"]
 
 
 def build_faultinj(force=False):

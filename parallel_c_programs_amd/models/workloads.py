@@ -167,16 +167,26 @@ class Stencil(Workload):
     fuse=T (default 0: auto_fuse of the slab height): T time steps per kernel (temporal blocking, bit-identical to single steps) and a T-row
     halo exchange every T steps; one step() then advances T time steps and counts T updates per cell."""
 
-    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, fuse=0, halo_mult=0, **_):
+    def __init__(self, ctx, n=16384, per_rank=False, overlap=True, graph_steps=0, fuse=0, halo_mult=0,
+                 pattern="random", **_):
         from ..parallel.stencil import StencilSlab, auto_fuse, auto_halo_mult
 
         rows = n * (ctx.world if per_rank else 1)
         fuse = int(fuse) or auto_fuse(rows // ctx.world)
+        auto_m = not int(halo_mult)
         halo_mult = int(halo_mult) or auto_halo_mult(rows // ctx.world, fuse, ctx.world)
+        self.ctx, self.overlap, self.pattern = ctx, overlap, pattern
+        # The deep halo (m > 1) is proven on this job's own backend before it is timed: a small grid through the same
+        # slab code at this world size must equal the single-domain oracle bit for bit; an AUTO depth that fails it
+        # falls back to m = 1 (halo_selftest False in the line), an explicit one stays and fails the check.
+        self.halo_selftest = None
+        if halo_mult > 1 and ctx.distributed:
+            self.halo_selftest = self._small_grid_ok(fuse, halo_mult)
+            if not self.halo_selftest and auto_m:
+                halo_mult = 1
         super().__init__(ctx, {"n": n, "rows": rows, "graph_steps": graph_steps, "fuse": fuse,
-                               "halo_mult": halo_mult}, "stencil", "GLUP/s")
-        self.slab = StencilSlab(ctx, rows, n, fuse=fuse, halo_mult=halo_mult)
-        self.overlap = overlap
+                               "halo_mult": halo_mult, "pattern": pattern}, "stencil", "GLUP/s")
+        self.slab = StencilSlab(ctx, rows, n, fuse=fuse, halo_mult=halo_mult, pattern=pattern)
         self.graph_steps = graph_steps  # >0: one step() = graph_steps updates replayed from a HIP graph
         self.cells_local = self.slab.rows * n
 
@@ -204,22 +214,11 @@ class Stencil(Workload):
         timed grid: the grid the timed steps produced (warm-up + timed, `steps_done` updates of the full 16384^2
           problem, this rank's rows) against a plain-PyTorch f32 single-step oracle of the whole grid
           (ops.stencil5_reference, bf16 rounding per step) run on this rank's device (local only)."""
-        from ..parallel.stencil import StencilSlab, reference_run, reference_run_torch
+        from ..parallel.stencil import reference_run_torch
 
         sl = self.slab
-        f = sl.fuse
-        n, cols, steps = max(64, 2 * f * sl.m * self.ctx.world + 8), 200, 4 * f
-        small = StencilSlab(self.ctx, n, cols, fuse=f, halo_mult=sl.m)
-        small.run(steps, self.overlap)
-        full = small.gather()
-        ok = 1.0
-        if self.ctx.is_root:
-            ref = reference_run(n, steps, cols, device=self.ctx.device)
-            ok = float(torch.equal(full.view(torch.int16), ref.view(torch.int16)))
-        ok = self.ctx.broadcast_(self.ctx.scalar(ok)).item() == 1.0
-        del small, full
-
-        ref = reference_run_torch(sl.n, sl.steps_done, sl.cols, sl.k, device=self.ctx.device)
+        ok = self._small_grid_ok(sl.fuse, sl.m)
+        ref = reference_run_torch(sl.n, sl.steps_done, sl.cols, sl.k, device=self.ctx.device, pattern=self.pattern)
         mine = sl.interior()
         timed_ok = torch.equal(mine.view(torch.int16), ref[sl.row0:sl.row0 + sl.rows].view(torch.int16))
         del ref
@@ -228,8 +227,24 @@ class Stencil(Workload):
             timed_ok = self.ctx.max_over_ranks(0.0 if timed_ok else 1.0) == 0.0
             finite = self.ctx.max_over_ranks(0.0 if finite else 1.0) == 0.0
         return {"timed_grid_bit_exact": bool(timed_ok), "timed_grid_updates": sl.steps_done,
-                "bit_exact_vs_single_step_oracle": bool(ok), "finite": bool(finite),
+                "bit_exact_vs_single_step_oracle": bool(ok), "finite": bool(finite), "halo_selftest": self.halo_selftest,
                 "check_passed": bool(timed_ok and ok and finite)}
+
+    def _small_grid_ok(self, f: int, m: int) -> bool:
+        """A small random grid stepped through the same slab code at this world size (row slabs, the fused / deep
+        halo exchange, overlap) equals the single-domain single-step oracle bit for bit (collective; same answer on
+        every rank)."""
+        from ..parallel.stencil import StencilSlab, reference_run
+
+        n, cols, steps = max(64, 2 * f * m * self.ctx.world + 8), 200, 4 * f * max(1, m)
+        small = StencilSlab(self.ctx, n, cols, fuse=f, halo_mult=m, pattern=self.pattern)
+        small.run(steps, self.overlap)
+        full = small.gather()
+        ok = 1.0
+        if self.ctx.is_root:
+            ref = reference_run(n, steps, cols, device=self.ctx.device, pattern=self.pattern)
+            ok = float(torch.equal(full.view(torch.int16), ref.view(torch.int16)))
+        return self.ctx.broadcast_(self.ctx.scalar(ok)).item() == 1.0
 
 
 class SpMV(Workload):
@@ -252,17 +267,36 @@ class SpMV(Workload):
         self.xp = self.d.to_padded(x)
         del x
         self.y = None
+        # The column-split pipeline leaves each step's chunk-1 exchange in flight across the step boundary. Before it
+        # is timed, the SAME job proves it on its own backend: ITERATE_STEPS chained steps x <- A x with the exchange
+        # deferred must equal, bit for bit, the same steps with every exchange finished inside its step (same kernels,
+        # same data: any difference is a missing wait). If they differ on any rank, the timed steps finish their
+        # exchanges (defer off) and the line says so (pipeline_selftest False).
+        self.defer, self.selftest = True, None
+        if self.d.colsplit and ctx.distributed:
+            a = self.d.iterate(self.xp, self.ITERATE_STEPS, defer=True).clone()
+            b = self.d.iterate(self.xp, self.ITERATE_STEPS, defer=False)
+            same = ctx.max_over_ranks(0.0 if torch.equal(a, b) else 1.0) == 0.0
+            self.defer = self.selftest = same
+            del a
+
+    ITERATE_STEPS = 3
 
     def step(self):
         # the column-split pipeline: each step's last exchange overlaps the next step's first products (the next step
         # waits for it before the products that read those columns); check() finishes it
-        self.y = self.d.step_padded(self.xp, defer_exchange=True)
+        self.y = self.d.step_padded(self.xp, defer_exchange=self.defer)
 
     def check(self, reduce: bool = True):
         """Every entry of the timed step's output layout (own rows AND the ghost entries the exchange wrote) against
-        the fp64 product of its owner's row."""
+        the fp64 product of its owner's row; then ITERATE_STEPS chained steps (each output the next input, exchanges
+        deferred across step boundaries as in an iterating caller) against fp64 A^k x."""
         e = self.d.layout_max_rel_err(self.y, self.xp, reduce=reduce)
-        return {"max_rel_err_vs_fp64": e, "check_passed": e <= REL_ERR_LIMIT}
+        self.y = None  # (iterate() reuses the output buffers)
+        ei = self.d.iterate_max_rel_err(self.xp, self.ITERATE_STEPS, defer=self.defer, reduce=reduce)
+        return {"max_rel_err_vs_fp64": e, "iterated_max_rel_err_vs_fp64": ei, "iterated_steps": self.ITERATE_STEPS,
+                "pipeline_selftest": self.selftest, "deferred": self.defer and self.d.colsplit,
+                "check_passed": e <= REL_ERR_LIMIT and ei <= REL_ERR_LIMIT}
 
     def work_per_step(self):
         return 2.0 * self.d.local_nnz

@@ -210,7 +210,8 @@ class SlicedCSR:
             if not (0 <= lo and 0 < n and lo + n <= self.n_slices // 8):
                 raise ValueError(f"phases {phases} outside the {self.n_slices // 8} phases")
             mode |= (lo << 16) | (n << 21)
-        if self.cr is not None and (mode & 0x8F) == 0:  # production: packed index stream (bit 6: ballot combine, 8+: resident blocks)
+        # production: packed index stream (bit 6: ballot combine, 8+: resident blocks, 16-25: phases, 26: nt partials)
+        if self.cr is not None and (mode & 0x8F) == 0:
             if getattr(self, "_meta_packed", None) is None:
                 self._meta_packed = torch.cat([self.meta, torch.tensor(self.colbase, dtype=torch.int64)]).contiguous()
                 self._no_lrow = torch.empty(0, dtype=torch.int16, device=self.cr.device)

@@ -54,15 +54,17 @@ FUSED_STEPS = (2, 3, 4, 6, 8)
 
 def stencil5_fused_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, global_rows: int | None = None,
                          k: float = DEFAULT_K, halo: int = 1, steps: int = 2,
-                         row_range: tuple[int, int] | None = None) -> torch.Tensor:
+                         row_range: tuple[int, int] | None = None, shape: int = 0) -> torch.Tensor:
     """`steps` fused updates u -> out (temporal blocking: one HBM read + write per cell per `steps` updates),
     bit-identical to `steps` stencil5_step_ calls. Slabs are (rows + 2*halo, cols); rows within `steps` of a
-    rank boundary need halo >= steps (the halo rows must hold the neighbour's boundary rows)."""
+    rank boundary need halo >= steps (the halo rows must hold the neighbour's boundary rows). shape: an explicit
+    launch shape for this launch (0: the production rule; see pcmx_stencil5xT_bf16_spans_shape; labs)."""
     rows = u.shape[0] - 2 * halo
     global_rows = rows if global_rows is None else global_rows
     r0, r1 = row_range or (0, rows)
     if u.is_cuda:
-        ops().stencil5xT_(u, out, int(halo), int(steps), int(r0), int(r1), int(global_row0), int(global_rows), float(k))
+        ops().stencil5xT_(u, out, int(halo), int(steps), int(r0), int(r1), int(global_row0), int(global_rows), float(k),
+                          int(shape))
         return out
     # CPU oracle: plain steps. A slab with h halo rows yields the next level on h-1 halo rows (its outermost
     # rows go stale); once h == 1 only global edges are allowed and the (unused) halo rows keep their values.
@@ -79,7 +81,7 @@ def stencil5_fused_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 
 
 def stencil5_fused_spans_(u: torch.Tensor, out: torch.Tensor, spans, global_row0: int = 0,
                           global_rows: int | None = None, k: float = DEFAULT_K, halo: int = 1,
-                          steps: int = 2) -> torch.Tensor:
+                          steps: int = 2, shape: int = 0) -> torch.Tensor:
     """`steps` fused updates over two disjoint local row spans [(a0, a1), (b0, b1)] in ONE kernel launch (the
     distributed step's two rank-edge bands once the halo has arrived); same results as one call per span."""
     (a0, a1), (b0, b1) = spans
@@ -87,7 +89,7 @@ def stencil5_fused_spans_(u: torch.Tensor, out: torch.Tensor, spans, global_row0
         rows = u.shape[0] - 2 * halo
         global_rows = rows if global_rows is None else global_rows
         ops().stencil5xT_spans_(u, out, int(halo), int(steps), int(a0), int(a1), int(b0), int(b1), int(global_row0),
-                                int(global_rows), float(k))
+                                int(global_rows), float(k), int(shape))
         return out
     for r in ((a0, a1), (b0, b1)):
         if r[1] > r[0]:
@@ -95,19 +97,45 @@ def stencil5_fused_spans_(u: torch.Tensor, out: torch.Tensor, spans, global_row0
     return out
 
 
+def launch_shape(cpl: int = 0, rpw: int = 0, ahead: int = 0) -> int:
+    """The `shape` word of an explicit stencil launch shape (each field 0: the production rule's value)."""
+    if cpl not in (0, 4, 8) or not 0 <= rpw <= 255 or ahead not in (0, 3, 6, 9):
+        raise ValueError("launch_shape: cpl 0/4/8, rpw 0..255, ahead 0/3/6/9")
+    return cpl | (rpw << 8) | (ahead << 16)
+
+
 def stencil5x2_step_(u, out, global_row0=0, global_rows=None, k=DEFAULT_K, halo=1, row_range=None):
     """Two fused updates (see stencil5_fused_step_)."""
     return stencil5_fused_step_(u, out, global_row0, global_rows, k, halo, 2, row_range)
 
 
+def _hash32(x: torch.Tensor) -> torch.Tensor:
+    """A 32-bit integer mix of int64 values in [0, 2^32) (two multiply-xorshift rounds). Every product stays below
+    2^59, so the int64 arithmetic is exact and identical on the CPU and the GPU."""
+    m = 0xFFFFFFFF
+    x = ((x >> 16) ^ x) * 0x45D9F3B & m
+    x = ((x >> 16) ^ x) * 0x45D9F3B & m
+    return (x >> 16) ^ x
+
+
 def init_grid(rows: int, cols: int, global_row0: int = 0, global_rows: int | None = None, device="cpu",
-              halo: int = 1) -> torch.Tensor:
-    """Deterministic initial condition: hot top boundary row (1.0), a hot square in the middle, 0 elsewhere."""
+              halo: int = 1, pattern: str = "random", seed: int = 0) -> torch.Tensor:
+    """Deterministic initial condition of the global grid, rows [global_row0 - halo, global_row0 + rows + halo).
+    pattern "random" (default; the north star's random-init arrays): every cell uniform in [-1, 1) from a hash of its
+    GLOBAL index (so any row-slab decomposition generates the same grid), the Dirichlet edge rows and columns
+    included; pattern "hot": a hot top boundary row (1.0) and a hot square in the middle, 0 elsewhere. Rows outside
+    the grid are 0."""
     global_rows = rows if global_rows is None else global_rows
-    g = torch.arange(global_row0 - halo, global_row0 + rows + halo, device=device).view(-1, 1).float()
-    c = torch.arange(cols, device=device).view(1, -1).float()
-    hot = ((g - global_rows / 2).abs() < global_rows / 8) & ((c - cols / 2).abs() < cols / 8)
-    u = hot.float() * 0.5
-    u = torch.where(g == 0, torch.ones_like(u), u)
-    u = torch.where((g < 0) | (g >= global_rows), torch.zeros_like(u), u)
+    gi = torch.arange(global_row0 - halo, global_row0 + rows + halo, device=device).view(-1, 1)
+    ci = torch.arange(cols, device=device).view(1, -1)
+    if pattern == "random":
+        idx = (gi.clamp_min(0) * cols + ci + (seed & 0xFFFF) * 0x9E3779B1) & 0xFFFFFFFF
+        u = (_hash32(idx) & 0xFFFFFF).float() * (2.0 / (1 << 24)) - 1.0
+    elif pattern == "hot":
+        g, c = gi.float(), ci.float()
+        hot = ((g - global_rows / 2).abs() < global_rows / 8) & ((c - cols / 2).abs() < cols / 8)
+        u = torch.where(g == 0, torch.ones_like(hot, dtype=torch.float32), hot.float() * 0.5)
+    else:
+        raise ValueError("pattern: 'random' or 'hot'")
+    u = torch.where((gi < 0) | (gi >= global_rows), torch.zeros_like(u), u)
     return u.to(torch.bfloat16).contiguous()

@@ -3,7 +3,7 @@
 Replaces the reference's MPI programs (1-introduction/mpi.c, 2-mpi-region-growing/region.c).
 """
 from .collectives import allreduce_buckets, gather_rows, global_reduce, global_scan, scatter_rows
-from .dist import Context, finalize, free_port, init, spawn
+from .dist import Context, LazyContext, finalize, free_port, init, spawn
 from .halo import HaloExchanger2D
 from .region2d import gather_tiles, grow_distributed, scatter_tiles
 from .ring import token_ring
@@ -13,6 +13,7 @@ from .topology import CartTopology, dims_create, prime_factors, split
 from .volume3d import DistributedVolume, VolumeSlab, emulate_slabs
 
 __all__ = [
+    "LazyContext",
     "Context", "init", "finalize", "spawn", "free_port",
     "CartTopology", "dims_create", "prime_factors", "split",
     "HaloExchanger2D", "global_reduce", "global_scan", "allreduce_buckets", "scatter_rows", "gather_rows",

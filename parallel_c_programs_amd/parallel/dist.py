@@ -140,6 +140,39 @@ class Context:
         return float(t.item())
 
 
+class _DeferredWork:
+    """An exchange whose data lands in its receive tensors only when waited on."""
+
+    def __init__(self, pairs):
+        self.pairs = pairs
+
+    def wait(self):
+        for dst, src in self.pairs:
+            dst.copy_(src)
+        self.pairs = []
+
+
+class LazyContext(Context):
+    """Test transport: exchange() moves the data at once into private buffers (the send tensors are copied when the
+    exchange is posted, as a real transport reads them) but writes the receive tensors only in wait(). The worst case
+    a real async transport allows — nothing arrives before it is waited for — every time: a schedule that reads an
+    exchange's destination before waiting for it reads stale data deterministically (tests of the deferred SpMV
+    pipeline, tests/test_parallel_cpu.py, tests/test_gpu_multi.py)."""
+
+    def exchange(self, outs: list, ins: list, async_op: bool = False) -> list:
+        tmp = [torch.empty_like(o) for o in outs]
+        Context.exchange(self, tmp, [t.clone() for t in ins], async_op=False)
+        w = _DeferredWork(list(zip(outs, tmp)))
+        if async_op:
+            return [w]
+        w.wait()
+        return []
+
+    @staticmethod
+    def of(ctx: Context) -> LazyContext:
+        return LazyContext(ctx.rank, ctx.world, ctx.local_rank, ctx.device, ctx.backend)
+
+
 _OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
 
 

@@ -154,7 +154,10 @@ class DistributedSpMV:
         # while the chunk-1 exchange is still in flight, and only then the chunk-1 columns (see step_padded)
         B = self.ghost0[1] if self.exchange == "ghost" and C == 2 else 0
         if colsplit is None:
-            colsplit = ctx.distributed and 0 < B < self.n_pad
+            # default only where it pays: the sliced GPU product (its phase launches split the same slice partials, so
+            # the combined row sums do not change order). On the plain CSR path (CPU / gloo) (A0 x) + (A1 x) would only
+            # change the fp32 summation order, so it is opt-in there (ColSplitCSR, tests)
+            colsplit = ctx.distributed and 0 < B < self.n_pad and bool(slices) and dev.type == "cuda"
         self.colsplit = bool(colsplit) and 0 < B < self.n_pad
         self.col_split = B if self.colsplit else 0
         if self.colsplit and slices:
@@ -249,7 +252,7 @@ class DistributedSpMV:
     def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
                  slices: int = 0, head: float = 0.0625, balance: float = 0.0,
                  chunks: int | None = None, item_nnz: int = 0, exchange: str = "ghost",
-                 keep_plain: bool = False, colsplit: bool | None = None) -> "DistributedSpMV":
+                 keep_plain: bool = False, colsplit: bool | None = None) -> DistributedSpMV:
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)
@@ -299,8 +302,14 @@ class DistributedSpMV:
         mine = xp[self.local_positions()]
         if not self.ctx.distributed:
             return mine.clone()
-        buf = torch.zeros(self.block, dtype=mine.dtype, device=mine.device)
-        buf[:self.rows] = mine
+        return self._gather_rows(mine)
+
+    def _gather_rows(self, own: torch.Tensor) -> torch.Tensor:
+        """This rank's rows (local order) of a vector -> the full natural-order vector (one all-gather; collective)."""
+        if not self.ctx.distributed:
+            return own
+        buf = torch.zeros(self.block, dtype=own.dtype, device=own.device)
+        buf[:own.numel()] = own
         parts = self.ctx.all_gather(buf)
         return torch.cat([p[:self.cuts[q + 1] - self.cuts[q]] for q, p in enumerate(parts)])
 
@@ -411,6 +420,40 @@ class DistributedSpMV:
         self.finish()
         return self.from_padded(y)
 
+    def iterate(self, xp: torch.Tensor, steps: int, defer: bool = True) -> torch.Tensor:
+        """x <- A x, `steps` times, in this rank's layout (the power-iteration pattern the schedule is built for): each
+        step's output is the next step's input, and with `defer` (column split) each step's chunk-1 exchange is still
+        in flight when the next step starts its chunk-0-column products. Returns the last layout vector (one of the two
+        internal buffers) with every exchange finished."""
+        for _ in range(steps):
+            xp = self.step_padded(xp, defer_exchange=defer)
+        self.finish()
+        return xp
+
+    def iterate_reference(self, xp: torch.Tensor, steps: int) -> torch.Tensor:
+        """fp64 A^steps xp in this rank's layout (own rows and every ghost), the oracle of iterate(): each step
+        multiplies this rank's rows in fp64 and all-gathers the WHOLE vector (no ghost exchange, no column split, no
+        deferral involved). Collective."""
+        ids = self.layout_ids()
+        m = ids >= 0
+        cur = xp.double()
+        for _ in range(steps):
+            full = self._gather_rows(self.reference_local(cur))
+            cur = torch.zeros(self.n_pad, dtype=torch.float64, device=xp.device)
+            cur[m] = full[ids[m]]
+        return cur
+
+    def iterate_max_rel_err(self, xp: torch.Tensor, steps: int, defer: bool = True, reduce: bool = True) -> float:
+        """Max error of EVERY layout entry after `steps` iterated steps (iterate) against iterate_reference, relative
+        to the largest reference entry. Both runs (and their collectives) come first; reduce=False: this rank's value
+        only."""
+        got = self.iterate(xp, steps, defer).double()
+        want = self.iterate_reference(xp, steps)
+        m = self.layout_ids() >= 0
+        scale = want[m].abs().max().clamp_min(1e-300) if bool(m.any()) else torch.ones((), dtype=torch.float64)
+        err = ((got[m] - want[m]).abs().max() / scale).item() if bool(m.any()) else 0.0
+        return self.ctx.max_over_ranks(err) if reduce else err
+
     def reference_local(self, xp: torch.Tensor) -> torch.Tensor:
         """fp64 product of this rank's rows with xp (its layout), in local row order."""
         outs = []
@@ -433,14 +476,7 @@ class DistributedSpMV:
         product and the exchange that the timed step performs. Same value on every rank (reduce=False: this
         rank's entries only, no collective after the all-gather of the fp64 rows)."""
         self.finish()
-        ref = self.reference_local(xp)
-        if self.ctx.distributed:
-            buf = torch.zeros(self.block, dtype=torch.float64, device=ref.device)
-            buf[:ref.numel()] = ref
-            parts = self.ctx.all_gather(buf)
-            full = torch.cat([p[:self.cuts[q + 1] - self.cuts[q]] for q, p in enumerate(parts)])
-        else:
-            full = ref
+        full = self._gather_rows(self.reference_local(xp))
         ids = self.layout_ids()
         m = ids >= 0
         got, want = y[m].double(), full[ids[m]]

@@ -61,7 +61,7 @@ class StencilSlab:
     to single steps: every computed row follows the same arithmetic from the same inputs."""
 
     def __init__(self, ctx: Context, n: int, cols: int | None = None, k: float = DEFAULT_K, fuse: int = 1,
-                 halo_mult: int = 1):
+                 halo_mult: int = 1, pattern: str = "random"):
         self.ctx, self.n, self.cols, self.k = ctx, n, (n if cols is None else cols), k
         if fuse != 1 and fuse not in FUSED_STEPS:
             raise ValueError(f"fuse: 1 or one of {FUSED_STEPS} updates per kernel")
@@ -74,7 +74,11 @@ class StencilSlab:
         self.rows = row1 - self.row0
         if self.rows < 2 * self.halo:
             raise ValueError(f"each rank needs at least {2 * self.halo} rows")
-        self.u = init_grid(self.rows, self.cols, self.row0, n, device=ctx.device, halo=self.halo)
+        self.pattern = pattern
+        self.u = init_grid(self.rows, self.cols, self.row0, n, device=ctx.device, halo=self.halo, pattern=pattern)
+        # explicit launch shapes (ops.stencil.launch_shape; 0 = the production rule) of the full / interior launches
+        # and of the two-span edge launch: lab sweeps set them per slab, nothing process-global
+        self.shape, self.edge_shape = 0, 0
         self.v = self.u.clone()
         self.steps_done = 0
         self.phase = 0  # step index within the current deep-halo period (0: the exchange step)
@@ -101,7 +105,8 @@ class StencilSlab:
     def _update(self, u, v, row_range=None):
         """`fuse` updates u -> v over local rows row_range (default all)."""
         if self.fuse > 1:
-            stencil5_fused_step_(u, v, self.row0, self.n, self.k, halo=self.halo, steps=self.fuse, row_range=row_range)
+            stencil5_fused_step_(u, v, self.row0, self.n, self.k, halo=self.halo, steps=self.fuse, row_range=row_range,
+                                 shape=self.shape)
         else:
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=row_range)
 
@@ -110,7 +115,7 @@ class StencilSlab:
         T, rows = self.fuse, self.rows
         if self.fuse > 1:
             stencil5_fused_spans_(u, v, ((lo, T), (rows - T, hi)), self.row0, self.n, self.k, halo=self.halo,
-                                  steps=self.fuse)
+                                  steps=self.fuse, shape=self.edge_shape)
         else:
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(0, T))
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(rows - T, rows))
@@ -212,10 +217,11 @@ class StencilSlab:
         return None
 
 
-def reference_run(n: int, steps: int, cols: int | None = None, k: float = DEFAULT_K, device="cpu") -> torch.Tensor:
+def reference_run(n: int, steps: int, cols: int | None = None, k: float = DEFAULT_K, device="cpu",
+                  pattern: str = "random") -> torch.Tensor:
     """Single-domain run (the oracle the distributed result must equal bit for bit)."""
     cols = n if cols is None else cols
-    u = init_grid(n, cols, 0, n, device=device)
+    u = init_grid(n, cols, 0, n, device=device, pattern=pattern)
     v = u.clone()
     for _ in range(steps):
         stencil5_step_(u, v, 0, n, k)
@@ -223,13 +229,14 @@ def reference_run(n: int, steps: int, cols: int | None = None, k: float = DEFAUL
     return u[1:-1]
 
 
-def reference_run_torch(n: int, steps: int, cols: int | None = None, k: float = DEFAULT_K, device="cpu") -> torch.Tensor:
+def reference_run_torch(n: int, steps: int, cols: int | None = None, k: float = DEFAULT_K, device="cpu",
+                        pattern: str = "random") -> torch.Tensor:
     """Single-domain run on plain PyTorch f32 ops (ops.stencil5_reference: no HIP kernel involved), the oracle of
     the bench's timed-grid check."""
     from ..ops.stencil import stencil5_reference
 
     cols = n if cols is None else cols
-    u = init_grid(n, cols, 0, n, device=device)
+    u = init_grid(n, cols, 0, n, device=device, pattern=pattern)
     for _ in range(steps):
         u = stencil5_reference(u, 0, n, k)
     return u[1:-1]

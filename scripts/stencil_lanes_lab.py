@@ -1,4 +1,4 @@
-"""Stencil lanes lab: 8 vs 4 columns per lane (csrc/kernels/stencil.hip Geo / pcmx_stencil_lab_set) for the fused
+"""Stencil lanes lab: 8 vs 4 columns per lane (csrc/kernels/stencil.hip Geo, explicit launch shapes) for the fused
 v2 kernel, per slab height (one rank's interior slab at N = 8 / 4 / 2 / 1 of the 16384^2 grid) and rows per wave.
 Every configuration is checked bit for bit against the production launch; prints ms and GLUP/s of the full-slab
 launch and of the distributed step shape (interior launch + one two-span edge launch).
@@ -13,13 +13,9 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from parallel_c_programs_amd import ops  # noqa: E402
-from parallel_c_programs_amd._native import hip_lib  # noqa: E402
+from parallel_c_programs_amd.ops.stencil import launch_shape  # noqa: E402
 
 N = 16384
-
-
-def lab_set(cpl, rpw, which=0):
-    assert hip_lib().pcmx_stencil_lab_set(which, cpl, rpw) == 0
 
 
 def timed(fn, reps):
@@ -45,14 +41,13 @@ def edge_sweep(argv):
         for rows in heights:
             u = (torch.rand(rows + 2 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
             ref, out = u.clone(), u.clone()
-            lab_set(0, 0, 0), lab_set(0, 0, 1)
             ops.stencil5_fused_step_(u, ref, rows, N, halo=T, steps=T)
             torch.cuda.synchronize()
             for cpl, rpw in ((0, 0), (8, 16), (8, 4), (8, 2), (4, 16), (4, 4), (4, 2)):
-                lab_set(cpl, rpw, 1)
+                es = launch_shape(cpl, rpw)
 
                 def edges():
-                    ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), rows, N, halo=T, steps=T)
+                    ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), rows, N, halo=T, steps=T, shape=es)
 
                 def split2():
                     ops.stencil5_fused_step_(u, out, rows, N, halo=T, steps=T, row_range=(T, rows - T))
@@ -65,7 +60,6 @@ def edge_sweep(argv):
                 te, ts = timed(edges, reps), timed(split2, reps)
                 print(f"T={T} rows={rows:5d} edge cpl={cpl} rpw={rpw:2d} (0 = production)  edge launch {te:.4f} ms"
                       f"  split2 {ts:.4f} ms {rows * N * T / 1e6 / ts:6.0f} GLUP/s{'' if ok else ' MISMATCH'}", flush=True)
-            lab_set(0, 0, 1)
             del u, ref, out
             torch.cuda.empty_cache()
 
@@ -83,18 +77,17 @@ def main():
             row0 = 0 if rows == N else rows  # an interior rank (both neighbours) unless the whole grid
             u = (torch.rand(rows + 2 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
             ref, out = u.clone(), u.clone()
-            lab_set(0, 0)
             ops.stencil5_fused_step_(u, ref, row0, N, halo=T, steps=T)
             torch.cuda.synchronize()
             for cpl in (8, 4):
                 for rpw in (16, 18, 24, 32, 64):
-                    lab_set(cpl, rpw)
+                    fs = launch_shape(cpl, rpw)
 
                     def full():
-                        ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T)
+                        ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, shape=fs)
 
                     def split2():
-                        ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
+                        ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T), shape=fs)
                         ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), row0, N, halo=T, steps=T)
 
                     out.zero_()
@@ -110,7 +103,6 @@ def main():
                     print(f"T={T} rows={rows:5d} cpl={cpl} rpw={rpw:2d}  full {tf:.4f} ms {glup / tf:6.0f} GLUP/s"
                           f"{'' if ok_full else ' MISMATCH'}  split2 {ts:.4f} ms {glup / ts:6.0f} GLUP/s"
                           f"{'' if ok_split else ' MISMATCH'}", flush=True)
-            lab_set(0, 0)
             del u, ref, out
             torch.cuda.empty_cache()
 

@@ -14,7 +14,8 @@ Every variant is checked bit for bit against `full`. Prints ms per step and GLUP
 full-grid time this bounds the strong-scaling efficiency of the compute part (docs/ARCHITECTURE.md, stencil).
 Run: python scripts/stencil_rank_lab.py [fuse ...]
 Env: STENCIL_LAB_WORLDS=8 (subset of 1,2,4,8), STENCIL_LAB_RPW=0,18 (rows per wave forced on the non-edge launches
-through pcmx_stencil_lab_set, 0 = production rule; one line per value, all in one process for an A/B).
+as an explicit launch shape of each call, ops.stencil.launch_shape; 0 = production rule; one line per value, all in one
+process for an A/B).
 """
 import os
 import sys
@@ -23,7 +24,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from parallel_c_programs_amd import ops  # noqa: E402
-from parallel_c_programs_amd._native import hip_lib  # noqa: E402
+from parallel_c_programs_amd.ops.stencil import launch_shape  # noqa: E402
 
 N = 16384
 
@@ -48,7 +49,11 @@ def main():
     worlds = [int(w) for w in os.environ.get("STENCIL_LAB_WORLDS", "1,2,4,8").split(",")]
     rpws = [int(r) for r in os.environ.get("STENCIL_LAB_RPW", "0").split(",")]
     for T, world, rpw in [(T, w, r) for T in fuses for w in worlds for r in rpws]:
-        assert hip_lib().pcmx_stencil_lab_set(0, 0, rpw) == 0
+        shape = launch_shape(0, rpw)
+
+        def step(*a, shape=shape, **kw):  # the non-edge launches take the forced rows per wave
+            return ops.stencil5_fused_step_(*a, shape=shape, **kw)
+
         if True:
             rows = N // world
             row0 = 0 if world == 1 else rows  # rank 1: both neighbours present (interior rank)
@@ -56,15 +61,15 @@ def main():
             ref, out = u.clone(), u.clone()
 
             def full():
-                ops.stencil5_fused_step_(u, ref, row0, N, halo=T, steps=T)
+                step(u, ref, row0, N, halo=T, steps=T)
 
             def split3():
-                ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
-                ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(0, T))
-                ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(rows - T, rows))
+                step(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
+                step(u, out, row0, N, halo=T, steps=T, row_range=(0, T))
+                step(u, out, row0, N, halo=T, steps=T, row_range=(rows - T, rows))
 
             def split2():
-                ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
+                step(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
                 ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), row0, N, halo=T, steps=T)
 
             side = torch.cuda.Stream(dev)
@@ -72,7 +77,7 @@ def main():
             def split2c():  # the edge launch on a side stream, concurrent with the interior kernel
                 main = torch.cuda.current_stream(dev)
                 side.wait_stream(main)
-                ops.stencil5_fused_step_(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
+                step(u, out, row0, N, halo=T, steps=T, row_range=(T, rows - T))
                 with torch.cuda.stream(side):
                     ops.stencil5_fused_spans_(u, out, ((0, T), (rows - T, rows)), row0, N, halo=T, steps=T)
                 main.wait_stream(side)
@@ -83,28 +88,28 @@ def main():
             v2, w2, ref2 = u2.clone(), u2.clone(), u2.clone()
 
             def deep2():
-                ops.stencil5_fused_step_(u2, v2, row0, N, halo=2 * T, steps=T, row_range=(T, rows - T))
+                step(u2, v2, row0, N, halo=2 * T, steps=T, row_range=(T, rows - T))
                 ops.stencil5_fused_spans_(u2, v2, ((-T, T), (rows - T, rows + T)), row0, N, halo=2 * T, steps=T)
-                ops.stencil5_fused_step_(v2, w2, row0, N, halo=2 * T, steps=T, row_range=(0, rows))
+                step(v2, w2, row0, N, halo=2 * T, steps=T, row_range=(0, rows))
 
-            ops.stencil5_fused_step_(u2, ref2, row0, N, halo=2 * T, steps=T, row_range=(-T, rows + T))
+            step(u2, ref2, row0, N, halo=2 * T, steps=T, row_range=(-T, rows + T))
             ref3 = ref2.clone()
-            ops.stencil5_fused_step_(ref2, ref3, row0, N, halo=2 * T, steps=T, row_range=(0, rows))
+            step(ref2, ref3, row0, N, halo=2 * T, steps=T, row_range=(0, rows))
 
             # deep halo m = 3: 3T halo rows, one exchange + one edge launch per 3 steps
             u3 = (torch.rand(rows + 6 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
             p3, q3, r3 = u3.clone(), u3.clone(), u3.clone()
 
             def deep3():
-                ops.stencil5_fused_step_(u3, p3, row0, N, halo=3 * T, steps=T, row_range=(T, rows - T))
+                step(u3, p3, row0, N, halo=3 * T, steps=T, row_range=(T, rows - T))
                 ops.stencil5_fused_spans_(u3, p3, ((-2 * T, T), (rows - T, rows + 2 * T)), row0, N, halo=3 * T, steps=T)
-                ops.stencil5_fused_step_(p3, q3, row0, N, halo=3 * T, steps=T, row_range=(-T, rows + T))
-                ops.stencil5_fused_step_(q3, r3, row0, N, halo=3 * T, steps=T, row_range=(0, rows))
+                step(p3, q3, row0, N, halo=3 * T, steps=T, row_range=(-T, rows + T))
+                step(q3, r3, row0, N, halo=3 * T, steps=T, row_range=(0, rows))
 
             s1, s2, s3 = u3.clone(), u3.clone(), u3.clone()
-            ops.stencil5_fused_step_(u3, s1, row0, N, halo=3 * T, steps=T, row_range=(-2 * T, rows + 2 * T))
-            ops.stencil5_fused_step_(s1, s2, row0, N, halo=3 * T, steps=T, row_range=(-T, rows + T))
-            ops.stencil5_fused_step_(s2, s3, row0, N, halo=3 * T, steps=T, row_range=(0, rows))
+            step(u3, s1, row0, N, halo=3 * T, steps=T, row_range=(-2 * T, rows + 2 * T))
+            step(s1, s2, row0, N, halo=3 * T, steps=T, row_range=(-T, rows + T))
+            step(s2, s3, row0, N, halo=3 * T, steps=T, row_range=(0, rows))
 
             # deep halo m = 4 (generic form of deep2 / deep3)
             M4 = 4
@@ -113,17 +118,17 @@ def main():
 
             def deep4():
                 e0 = (M4 - 1) * T
-                ops.stencil5_fused_step_(b4[0], b4[1], row0, N, halo=M4 * T, steps=T, row_range=(T, rows - T))
+                step(b4[0], b4[1], row0, N, halo=M4 * T, steps=T, row_range=(T, rows - T))
                 ops.stencil5_fused_spans_(b4[0], b4[1], ((-e0, T), (rows - T, rows + e0)), row0, N, halo=M4 * T,
                                           steps=T)
                 for ph in range(1, M4):
                     e = (M4 - 1 - ph) * T
-                    ops.stencil5_fused_step_(b4[ph], b4[ph + 1], row0, N, halo=M4 * T, steps=T, row_range=(-e, rows + e))
+                    step(b4[ph], b4[ph + 1], row0, N, halo=M4 * T, steps=T, row_range=(-e, rows + e))
 
             c4 = [u4.clone() for _ in range(M4 + 1)]
             for ph in range(M4):
                 e = (M4 - 1 - ph) * T
-                ops.stencil5_fused_step_(c4[ph], c4[ph + 1], row0, N, halo=M4 * T, steps=T, row_range=(-e, rows + e))
+                step(c4[ph], c4[ph + 1], row0, N, halo=M4 * T, steps=T, row_range=(-e, rows + e))
 
             full()
             res = {}
@@ -153,7 +158,6 @@ def main():
             print(f"fuse={T} N={world} rows={rows:5d}{tag}  {line}", flush=True)
             del u, ref, out, u2, v2, w2, ref2, ref3, u3, p3, q3, r3, s1, s2, s3, u4, b4, c4
             torch.cuda.empty_cache()
-    hip_lib().pcmx_stencil_lab_set(0, 0, 0)
 
 
 if __name__ == "__main__":

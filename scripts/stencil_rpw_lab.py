@@ -10,7 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from parallel_c_programs_amd import ops  # noqa: E402
-from parallel_c_programs_amd._native import hip_lib  # noqa: E402
+from parallel_c_programs_amd.ops.stencil import launch_shape  # noqa: E402
 
 N = 16384
 # VGPRs of stencil5xT2_kernel<T, ahead, 1, cpl> (hipcc -S, csrc/kernels/stencil.hip) -> waves per SIMD = 512 // VGPRs
@@ -44,24 +44,22 @@ def main():
     rpws = [int(a) for a in sys.argv[4].split(",")]
     aheads = [int(a) for a in sys.argv[5].split(",")] if len(sys.argv) > 5 else [0]
     reps = int(sys.argv[6]) if len(sys.argv) > 6 else 30
-    lib = hip_lib()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(7)
     u = (torch.rand(rows + 2 * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
     ref, out = u.clone(), u.clone()
-    assert lib.pcmx_stencil_lab_set(0, 0, 0) == 0 and lib.pcmx_stencil_lab_set(2, 0, 0) == 0
     fn_ref = lambda: ops.stencil5_fused_step_(u, ref, rows, N, halo=T, steps=T)  # noqa: E731
     fn_ref()
     torch.cuda.synchronize()
     t_prod = timed(fn_ref, reps)
     print(f"T={T} rows={rows} production {t_prod:.4f} ms {rows * N * T / 1e6 / t_prod:6.0f} GLUP/s", flush=True)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    try:
+    if True:
         for cpl in cpls:
             for ahead in aheads:
                 for rpw in rpws:
-                    assert lib.pcmx_stencil_lab_set(0, cpl, rpw) == 0 and lib.pcmx_stencil_lab_set(2, 0, ahead) == 0
-                    fn = lambda: ops.stencil5_fused_step_(u, out, rows, N, halo=T, steps=T)  # noqa: E731
+                    sh = launch_shape(cpl, rpw, ahead)
+                    fn = lambda: ops.stencil5_fused_step_(u, out, rows, N, halo=T, steps=T, shape=sh)  # noqa: E731
                     out.zero_()
                     fn()
                     torch.cuda.synchronize()
@@ -74,8 +72,6 @@ def main():
                     print(f"T={T} rows={rows} cpl={cpl} ahead={ka} rpw={rpw:3d}  {t:.4f} ms "
                           f"{rows * N * T / 1e6 / t:6.0f} GLUP/s  wgs={wgs} waves/SIMD={wps} rounds={rounds:.2f}"
                           f"{'' if ok else ' MISMATCH'}", flush=True)
-    finally:
-        lib.pcmx_stencil_lab_set(0, 0, 0), lib.pcmx_stencil_lab_set(2, 0, 0)
 
 
 if __name__ == "__main__":

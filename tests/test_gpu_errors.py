@@ -5,6 +5,8 @@
     its predecessor and exhausts a 64-poll spin limit).
   * region growing: a fixpoint loop that runs out of max_launches with work left returns
     PCMX_ERR_NOT_CONVERGED (-2), which the torch ops raise.
+  * the bench's stencil check: a one-lane neighbour swap in the fused kernel (the same fault-injection build of
+    stencil.hip) must fail the timed-grid check on the bench's random grid.
 """
 import ctypes
 
@@ -29,6 +31,8 @@ def _faultinj():
     lib.pcmx_scan_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.pcmx_scan_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.pcmx_stencil5xT_bf16_spans_shape.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 9 + [
+        ctypes.c_longlong, ctypes.c_longlong, ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
     return lib
 
 
@@ -88,3 +92,39 @@ def test_region3d_not_converged_raises(gpu, tiled):
     reg[0, 0, 0] = 2 if not tiled else 1
     with pytest.raises(RuntimeError, match="not converged"):
         native().region3d_grow_(reg, data, 1, tiled, 1, 1)
+
+
+def _faulty_fused_step(lib):
+    """ops.stencil5_fused_step_ on the fault-injection build's kernel (lane 17 swaps a neighbour)."""
+    def fused(u, out, global_row0=0, global_rows=None, k=0.2, halo=1, steps=2, row_range=None, shape=0):
+        rows, cols = u.shape[0] - 2 * halo, u.shape[1]
+        global_rows = rows if global_rows is None else global_rows
+        r0, r1 = row_range or (0, rows)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(u.device).cuda_stream)
+        rc = lib.pcmx_stencil5xT_bf16_spans_shape(u.data_ptr(), out.data_ptr(), rows, cols, cols, halo, steps, r0, r1,
+                                                  0, 0, global_row0, global_rows, k, shape, stream)
+        assert rc == 0
+        return out
+    return fused
+
+
+def test_stencil_check_catches_one_lane_neighbour_swap(gpu, monkeypatch):
+    """The bench's stencil check (workloads.Stencil.check: the timed grid bit for bit against plain-PyTorch single
+    steps) on its random grid: it passes on the production kernel and FAILS when one lane of every strip reads its
+    east neighbour as its west one (fault-injection build), a bug a constant grid region would hide."""
+    from parallel_c_programs_amd.models import workloads as W
+    from parallel_c_programs_amd.parallel import stencil as PS
+    from parallel_c_programs_amd.parallel.dist import Context
+
+    lib = _faultinj()
+    ctx = Context(device=gpu)
+    good = W.Stencil(ctx, n=2048, fuse=8)
+    for _ in range(3):
+        good.step()
+    assert good.check()["check_passed"]
+    monkeypatch.setattr(PS, "stencil5_fused_step_", _faulty_fused_step(lib))
+    bad = W.Stencil(ctx, n=2048, fuse=8)
+    for _ in range(3):
+        bad.step()
+    c = bad.check()
+    assert not c["timed_grid_bit_exact"] and not c["check_passed"]

@@ -240,11 +240,12 @@ def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
 @pytest.mark.parametrize("steps", [3, 4, 6, 8])
 @pytest.mark.parametrize("shape", [(515, 1000), (70, 2056), (200, 264)])
 def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
-    """Every launch shape the stencil lab knob can force (4 or 8 columns per lane x 2..64 rows per wave, for full
-    and edge launches; rows per wave is a launch parameter, so odd counts too) gives the bits of `steps` single steps: ragged column counts (stale-lane rule of 4-column lanes
-    at T = 8: two stale lanes per strip side), Dirichlet rows and columns, strips ending inside a lane range."""
-    import ctypes  # noqa: F401
-    from parallel_c_programs_amd._native import hip_lib
+    """Every explicit launch shape (ops.stencil.launch_shape: 4 or 8 columns per lane x 2..133 rows per wave x prefetch
+    ring 3 / 6 / 9, for full and edge launches; rows per wave is a launch parameter, so odd counts too) gives the bits of
+    `steps` single steps: ragged column counts (stale-lane rule of 4-column lanes at T = 8: two stale lanes per strip
+    side), Dirichlet rows and columns, strips ending inside a lane range. The shape is a per-launch argument: no state
+    is left behind in the library."""
+    from parallel_c_programs_amd.ops.stencil import launch_shape
 
     rows, cols = shape
     g = torch.Generator().manual_seed(rows + cols + steps)
@@ -253,16 +254,17 @@ def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
     for _ in range(steps):
         ref = ops.stencil5_reference(ref, 0, rows)
     a = u.to(gpu)
-    lib = hip_lib()
-    try:
-        for cpl in (4, 8):
-            for rpw in (2, 4, 7, 16, 18, 24, 32, 64, 67, 133):
-                assert lib.pcmx_stencil_lab_set(0, cpl, rpw) == 0 and lib.pcmx_stencil_lab_set(1, cpl, rpw) == 0
+    for cpl in (4, 8):
+        for rpw in (2, 4, 7, 16, 18, 24, 32, 64, 67, 133):
+            for ahead in ((0, 3, 9) if rpw in (7, 64) else (0,)):
                 b = torch.zeros_like(a)
-                ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps)
-                assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16)), (cpl, rpw)
-    finally:
-        lib.pcmx_stencil_lab_set(0, 0, 0), lib.pcmx_stencil_lab_set(1, 0, 0)
+                ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps, shape=launch_shape(cpl, rpw, ahead))
+                assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16)), (cpl, rpw, ahead)
+    b = torch.zeros_like(a)
+    ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps)  # the production rule after the sweep: same bits
+    assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16))
+    with pytest.raises(RuntimeError):
+        ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps, shape=5)  # 5 columns per lane: refused
 
 
 @pytest.mark.parametrize("steps", [2, 4, 6])
@@ -342,6 +344,31 @@ def test_spmv_banded_stream_unaligned_values_fall_back(gpu):
     buf[1:] = m.val.to(gpu)
     out = ops.spmv_banded(buf[1:], m.row_ptr.to(gpu), *dims, x.to(gpu), variant=8).cpu()
     assert (out - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item())
+
+
+def test_spmv_banded_stream_inside_graph_capture(gpu):
+    """Variant 8's slot table is built on the first call per band geometry (a HIP allocation + an async copy): inside a
+    stream capture of an UNCACHED geometry no allocation may run, so the launch takes variant 1 and the capture stays
+    valid; the replayed graph gives the host product. The same geometry outside a capture then builds the table (on the
+    stream) and variant 8 runs the stream kernel with the same result."""
+    dims = (7001, 403, 200, 100, 200, 10)  # a geometry no other test uses (the table cache is per process)
+    m = ops.banded_csr(*dims)
+    x = ops.create_vector(dims[0])
+    ref = ops.spmv(m, x)
+    vals, ro, xg = m.val.to(gpu), m.row_ptr.to(gpu), x.to(gpu)
+    side = torch.cuda.Stream(device=gpu)
+    side.wait_stream(torch.cuda.current_stream(gpu))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            out = ops.spmv_banded(vals, ro, *dims, xg, variant=8)
+    torch.cuda.current_stream(gpu).wait_stream(side)
+    g.replay()
+    torch.cuda.synchronize()
+    tol = 1e-3 * max(1.0, ref.abs().max().item())
+    assert (out.cpu() - ref).abs().max().item() < tol
+    out2 = ops.spmv_banded(vals, ro, *dims, xg, variant=8).cpu()
+    assert (out2 - ref).abs().max().item() < tol
 
 
 def test_scan_check_per_stream(gpu):

@@ -9,7 +9,7 @@ import torch
 from conftest import ASSETS, run_cli
 
 from parallel_c_programs_amd import ops
-from parallel_c_programs_amd.parallel import (CartTopology, DistributedSpMV, HaloExchanger2D, StencilSlab,
+from parallel_c_programs_amd.parallel import (CartTopology, DistributedSpMV, HaloExchanger2D, LazyContext, StencilSlab,
                                               dims_create, global_reduce, global_scan, grow_distributed,
                                               nnz_balanced_cuts, reference_run, spawn, split, token_ring)
 from parallel_c_programs_amd.utils import bmp
@@ -250,8 +250,8 @@ def test_stencil_checkpoint_resume_world2(tmp_path):
     assert np.array_equal(fa, reference_run(40, 7, 24).view(torch.int16).numpy())
 
 
-def _spmv(ctx, q, n, nnz, chunks, exchange):
-    d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1, chunks=chunks, exchange=exchange)
+def _spmv(ctx, q, n, nnz, chunks, exchange, colsplit=None):
+    d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1, chunks=chunks, exchange=exchange, colsplit=colsplit)
     x = torch.linspace(0, 1, n)
     y = d.step(x)
     y2 = d.step(y / y.abs().max())
@@ -273,13 +273,9 @@ def test_distributed_spmv_matches_serial(world, chunks, exchange):
     x = torch.linspace(0, 1, n)
     y = ops.spmv(m, x)
     y2 = ops.spmv(m, y / y.abs().max())
-    split = any(res[r][6] for r in range(world))
     for r in range(world):
-        if split:  # column split (ghost, 2 chunks): (A_<B x) + (A_>=B x), a different fp32 summation order
-            assert exchange == "ghost" and chunks == 2
-            assert torch.allclose(torch.from_numpy(res[r][0]), y, rtol=1e-5, atol=1e-5)
-        else:
-            assert torch.equal(torch.from_numpy(res[r][0]), y)  # same rows, same kernel: bit-identical
+        assert not res[r][6]  # the column split is a GPU (sliced) default only
+        assert torch.equal(torch.from_numpy(res[r][0]), y)  # same rows, same kernel: bit-identical
         assert torch.allclose(torch.from_numpy(res[r][1]), y2, rtol=1e-5, atol=1e-5)
         assert torch.allclose(torch.from_numpy(res[r][2]), y2, rtol=1e-5, atol=1e-5)
         # every layout entry (own rows and the ghosts / replicas the exchange delivered) holds y2 of its row
@@ -289,6 +285,74 @@ def test_distributed_spmv_matches_serial(world, chunks, exchange):
             assert res[r][3] >= n
         else:  # compact: own rows + the ghosts its nonzeros reference, never more than the whole vector
             assert res[r][3] <= n and int((ids >= 0).sum()) == res[r][3]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_spmv_colsplit_plain_csr(world):
+    """The column-split schedule on the plain CSR path (ColSplitCSR, asked for explicitly): (A_<B x) + (A_>=B x) is
+    another fp32 summation order, so it matches the serial product to rounding, not bit for bit."""
+    n, nnz = 3000, 40000
+    res = _collect(world, _spmv, n, nnz, 2, "ghost", True)
+    m = ops.powerlaw_csr(n, nnz, seed=1)
+    x = torch.linspace(0, 1, n)
+    y = ops.spmv(m, x)
+    y2 = ops.spmv(m, y / y.abs().max())
+    for r in range(world):
+        assert res[r][6]
+        assert torch.allclose(torch.from_numpy(res[r][0]), y, rtol=1e-5, atol=1e-5)
+        ids, yp2 = torch.from_numpy(res[r][4]), torch.from_numpy(res[r][5])
+        assert torch.allclose(yp2[ids >= 0], y2[ids[ids >= 0]], rtol=1e-5, atol=1e-5)
+
+
+def _late_wait_colsplit(self, xp, out):
+    """_step_colsplit with the previous step's chunk-1 wait moved AFTER the chunk-1-column products (a bug)."""
+    W, r = self.ctx.world, self.ctx.rank
+    self._wait(0)
+    for c, (a, b, part) in enumerate(self.parts):
+        if b > a:
+            part.product_phase(xp, 0, c)
+    pending = [[], []]
+    for c, (a, b, part) in enumerate(self.parts):
+        s0 = self.seg[c * W + r]
+        if b > a:
+            part.product_phase(xp, 1, c, out[s0:s0 + (b - a)])
+        pending[c] = self._post_chunk(out, c)
+    self._wait(1)
+    self._pending = pending
+    return out
+
+
+def _spmv_iterate(ctx, q, n, nnz, steps, buggy):
+    d = DistributedSpMV.powerlaw(LazyContext.of(ctx), n, nnz, seed=1, chunks=2, colsplit=True)
+    if buggy:
+        d._step_colsplit = _late_wait_colsplit.__get__(d)
+    xp = d.to_padded(torch.linspace(0, 1, n))
+    err = d.iterate_max_rel_err(xp, steps, defer=True)
+    y = d.from_padded(d.iterate(xp, steps, defer=True))
+    q.put((ctx.rank, (err, y.numpy(), d.colsplit)))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("buggy", [False, True])
+def test_distributed_spmv_deferred_pipeline_iterates(world, buggy):
+    """The steady-state pipeline as an ITERATION: K = 5 chained steps x <- A x with each step's chunk-1 exchange left
+    in flight into the next step (deferred), through a transport that delivers only on wait, against the serial fp64
+    A^K x. A schedule that waits for the chunk-1 exchange after the products that read it must fail."""
+    n, nnz, K = 3000, 40000, 5
+    res = _collect(world, _spmv_iterate, n, nnz, K, buggy)
+    m = ops.powerlaw_csr(n, nnz, seed=1)
+    A = torch.sparse_csr_tensor(m.row_ptr, m.col.long(), m.val.double(), size=(n, n))
+    ref = torch.linspace(0, 1, n).double()
+    for _ in range(K):
+        ref = A @ ref
+    for r in range(world):
+        err, y, split = res[r]
+        assert split
+        full_err = (torch.from_numpy(y).double() - ref).abs().max().item() / ref.abs().max().item()
+        if buggy:
+            assert err > 1e-3 and full_err > 1e-3, (err, full_err)
+        else:
+            assert err < 1e-5 and full_err < 1e-5, (err, full_err)
 
 
 def _spmv_uneven(ctx, q, cuts, chunks, exchange):
@@ -318,12 +382,9 @@ def test_distributed_spmv_uneven_and_empty_ranks(cuts, chunks, exchange):
     x = torch.linspace(0, 1, n)
     y = ops.spmv(m, x)
     y2 = ops.spmv(m, ops.spmv(m, x))
-    split = any(res[r][2] for r in range(len(cuts) - 1))
     for r in range(len(cuts) - 1):
-        if split:  # column split on some rank: (A_<B x) + (A_>=B x), another fp32 summation order
-            assert torch.allclose(torch.from_numpy(res[r][0]), y, rtol=1e-5, atol=1e-5)
-        else:
-            assert torch.equal(torch.from_numpy(res[r][0]), y)
+        assert not res[r][2]
+        assert torch.equal(torch.from_numpy(res[r][0]), y)
         assert torch.allclose(torch.from_numpy(res[r][1]), y2, rtol=1e-5, atol=1e-4)
 
 
@@ -454,6 +515,39 @@ def test_bench_exception_on_one_rank_is_a_collective_decision():
     assert nlines == 1 and out["reduce_error"].startswith("rank 1: RuntimeError")
     assert out["scan_strong_rel_err_vs_fp64"] < 1e-5 and out["stencil_bit_exact"] and out["spmv_gflops"] > 0
     assert not [k for k in out if k.endswith("_check_failed")]
+
+
+@pytest.mark.parametrize("section", ["stencil", "spmv"])
+def test_bench_early_exception_on_one_rank_does_not_hang(section):
+    """A section that raises on rank 1 right after its set-up, BEFORE its timed region (whose barriers rank 0 would
+    otherwise wait in until the process-group timeout): rank 0 stops at the next decision point, both ranks record
+    "<section>_error" from rank 1, the later sections run, the run exits 1 — well inside the test's time limit."""
+    r, out, nlines = _bench_cpu("--gpus", "2", "--steps", "1", "--warmup", "0", "--inject-fault",
+                                f"{section}:1:raise-early", timeout=300)
+    assert r.returncode == 1, r.stderr[-3000:]
+    assert nlines == 1 and out[f"{section}_error"].startswith("rank 1: RuntimeError: injected"), out
+    assert out["checks_passed"] is False and out["value"] > 0
+    assert f"{section}_glups" not in out and f"{section}_gflops" not in out
+    if section == "stencil":
+        assert out["spmv_gflops"] > 0 and out["spmv_max_rel_err_vs_fp64"] < 1e-5
+
+
+def test_bench_under_launcher_without_gpus_flag():
+    """torchrun --nproc-per-node 2 bench.py (no --gpus): the launcher's WORLD_SIZE is the rank count."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT, cli_env
+    from parallel_c_programs_amd.parallel import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "bench.py"), "--small", "--device", "cpu",
+           "--steps", "1", "--warmup", "0", "--sections", "reduce"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=cli_env(OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 2 and out["reduce_strong_gbps"] > 0
 
 
 # ------------------------------------------------------------------ launcher-level (torch.distributed.run)
