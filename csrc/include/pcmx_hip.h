@@ -118,7 +118,8 @@ int pcmx_region3d_grow_tiled(const unsigned char* data, unsigned char* region, i
 long long pcmx_region3d_slab_workspace_bytes(int dim, int nz);
 int pcmx_region3d_grow_slab(const unsigned char* data, unsigned char* region, int dim, int nz, int halos, int thr,
                             void* ws, int batch, int max_launches, hipStream_t s, int* launches_out);
-/* reference 0/1/2 frontier semantics, one launch per BFS level */
+/* reference 0/1/2 frontier semantics, one launch per BFS level; flag_ws: 4 device ints (the pipelined fixpoint check's
+ * flag ring); region 16-B aligned */
 int pcmx_region3d_grow_naive(const unsigned char* data, unsigned char* region, int dim, int thr, int* flag_ws,
                              int max_launches, hipStream_t s, int* launches_out);
 
@@ -136,6 +137,11 @@ int pcmx_raycast_slab(const unsigned char* data, const unsigned char* region, in
 int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
                         int image_dim, const float* cam12, float pixel_width, float step, int max_steps, int f64_color,
                         hipStream_t s);
+/* the same with an explicit caster variant (0 = production; 1 = one step in flight, 16x16 tiles; 2 / 3 = 4 / 16 steps
+ * in flight): identical images, the lab's A/B (scripts/raycast_global_lab.py) */
+int pcmx_raycast_global_variant(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
+                                int image_dim, const float* cam12, float pixel_width, float step, int max_steps,
+                                int f64_color, int variant, hipStream_t s);
 /* texture path: tex holds dim^3 * 16 + 16 bytes: per-voxel texels with the 2x2x2 footprint of data and region
  * (8-byte texels when every data value < 128, else 16-byte; the format flag is stored behind the texels),
  * dim <= 2048 */
@@ -191,6 +197,23 @@ int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* va
                      const long long* slice_item0, const long long* slice_out0, const void* items,
                      const unsigned* row_mask, const int* chunk_base, const void* fix, int n_fix, int mode,
                      const int* slice_colbase, hipStream_t s);
+/* the combine + split-row fix-up (+ send-buffer pack: sendbuf[send_slot[p]] = y[r] for p in send_ptr[r] ..
+ * send_ptr[r + 1]) of the partials a products-only pcmx_spmv_sliced call (mode bit 4) wrote, in ONE launch.
+ * slice_out0: host array of n_slices + 1 partial offsets; fix: int2 {item, row} sorted by row; fix_chunk0: the fix range
+ * of every 64-row chunk (n_rows / 64 + 2 ints, or NULL: no split rows); send_ptr (n_rows + 1) / send_slot / sendbuf
+ * may be NULL (no pack). Same bits as combine + fix-up. */
+/* products only of phases [a_lo, a_lo + a_n) of sliced matrix A and [b_lo, b_lo + b_n) of B (same x) in ONE launch
+ * (production packed layout; item_mode 2: 512-nnz items); nz0 / item0 / out0 / colbase: host arrays per matrix */
+int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, int mode, const int* col_a, const float* val_a,
+                          const void* items_a, float* ypart_a, float* extra_a, int s_a, const long long* nz0_a,
+                          const long long* item0_a, const long long* out0_a, const int* colbase_a, int a_lo, int a_n,
+                          const int* col_b, const float* val_b, const void* items_b, float* ypart_b, float* extra_b,
+                          int s_b, const long long* nz0_b, const long long* item0_b, const long long* out0_b,
+                          const int* colbase_b, int b_lo, int b_n, hipStream_t s);
+int pcmx_spmv_sliced_combine(const float* ypart, const unsigned* row_mask, const int* chunk_base,
+                             const long long* slice_out0, int n_slices, float* y, int n_rows, const float* extra,
+                             const void* fix, const int* fix_chunk0, const int* send_ptr, const int* send_slot,
+                             float* sendbuf, hipStream_t s);
 int pcmx_spmv_banded(const float* vals, const long long* row_off, int n, int a, int b, int c, int d, int e,
                      const float* x, float* y, hipStream_t s);
 /* variant 0: one wave per row (strided band loops, global x); 1: LDS-staged x windows, row blocks, 4-B loads;

@@ -148,6 +148,114 @@ __global__ __launch_bounds__(256) void raycast_ref_kernel(const unsigned char* _
     image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
 }
 
+// ---- the same march with the samples of B steps in flight (production global caster, round 5).
+// The positions of a ray do not depend on its colour: they are the reference's sequence of f32 adds, so the next B
+// positions are computed ahead and ALL their loads (8 byte loads per volume per sample) issued before the colour
+// of any of them is accumulated in step order. A step's loads no longer wait for the previous step's, which is what
+// bounds a march of ~1000 dependent samples (the reference's raycast kernel on MI355X: 2.95 ms at 64^2; ours with one
+// step in flight: 4.74 ms; profiles/r5_refbase/). Same arithmetic in the same order: bit-identical images.
+struct Taps {
+    float rx, ry, rz;
+    unsigned char t[8];  // zy[x], zy[xu], zyu[x], zyu[xu], zuy[x], zuy[xu], zuyu[x], zuyu[xu]
+    bool ok;
+};
+__device__ __forceinline__ void taps_load(float px, float py, float pz, const unsigned char* __restrict__ d, int dim,
+                                          Taps& T) {
+    T.ok = px >= 0 && px < dim - 1 && py >= 0 && py < dim - 1 && pz >= 0 && pz < dim - 1;
+    if (!T.ok) return;  // (a sample outside the volume reads as 0: no loads)
+    const int x = (int)floorf(px), y = (int)floorf(py), z = (int)floorf(pz);
+    const int xu = (int)ceilf(px), yu = (int)ceilf(py), zu = (int)ceilf(pz);
+    T.rx = px - x, T.ry = py - y, T.rz = pz - z;
+    const size_t P = (size_t)dim * dim;
+    const unsigned char* zy = d + (size_t)z * P + (size_t)y * dim;
+    const unsigned char* zyu = d + (size_t)z * P + (size_t)yu * dim;
+    const unsigned char* zuy = d + (size_t)zu * P + (size_t)y * dim;
+    const unsigned char* zuyu = d + (size_t)zu * P + (size_t)yu * dim;
+    T.t[0] = zy[x], T.t[1] = zy[xu], T.t[2] = zyu[x], T.t[3] = zyu[xu];
+    T.t[4] = zuy[x], T.t[5] = zuy[xu], T.t[6] = zuyu[x], T.t[7] = zuyu[xu];
+}
+__device__ __forceinline__ float taps_value(const Taps& T) {  // value_at_ref's arithmetic, operation for operation
+    if (!T.ok) return 0.f;
+    const float rx = T.rx, ry = T.ry, rz = T.rz;
+    const float a0 = rx * T.t[0] + (1 - rx) * T.t[1];
+    const float a1 = rx * T.t[2] + (1 - rx) * T.t[3];
+    const float a2 = rx * T.t[4] + (1 - rx) * T.t[5];
+    const float a3 = rx * T.t[6] + (1 - rx) * T.t[7];
+    const float b0 = ry * a0 + (1 - ry) * a1;
+    const float b1 = ry * a2 + (1 - ry) * a3;
+    return rz * b0 + (1 - rz) * b1;
+}
+
+template <bool F64COLOR, int B>
+__global__ __launch_bounds__(64) void raycast_ref_batch_kernel(const unsigned char* __restrict__ data,
+                                                               const unsigned char* __restrict__ region, int dim,
+                                                               unsigned char* __restrict__ image, int image_dim, Cam c) {
+    // one wave per 8x8 pixel tile: a small image (the OpenCL program's 64^2: 64 rays per ... 64 waves) spreads over
+    // 64 CUs instead of 16, each wave with a CU's load pipeline to itself
+    const int px = blockIdx.x * 8 + (threadIdx.x & 7);
+    const int py = blockIdx.y * 8 + (threadIdx.x >> 3);
+    if (px >= image_dim || py >= image_dim) return;
+    const int half = image_dim / 2;
+    const int x = px - half, y = py - half;
+    float ray[3], pos[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float sc = c.cam[k] + c.fwd[k];
+        const float t = (sc + c.right[k] * (x * c.pw)) + c.up[k] * (y * c.pw);
+        ray[k] = t + c.cam[k] * -1;
+        pos[k] = c.cam[k];
+    }
+    const float l = (float)sqrt((double)(ray[0] * ray[0] + ray[1] * ray[1] + ray[2] * ray[2]));
+    ray[0] /= l, ray[1] /= l, ray[2] /= l;
+    const float sx = ray[0] * c.step, sy = ray[1] * c.step, sz = ray[2] * c.step;
+    const float hi = (float)(dim - 1);
+    int i = 0;
+    float color = 0.f;
+    // outside the volume's box a sample adds exactly 0: walk the positions to the first sample inside (adds only)
+    while (i < c.max_steps) {
+        const float nx = pos[0] + sx, ny = pos[1] + sy, nz = pos[2] + sz;
+        if (in_box(nx, ny, nz, hi)) break;
+        ++i;
+        pos[0] = nx, pos[1] = ny, pos[2] = nz;
+    }
+    bool done = i >= c.max_steps;
+    while (!done) {
+        float q[B][3];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            pos[0] = pos[0] + sx, pos[1] = pos[1] + sy, pos[2] = pos[2] + sz;
+            q[b][0] = pos[0], q[b][1] = pos[1], q[b][2] = pos[2];
+        }
+        Taps R[B], D[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            taps_load(q[b][0], q[b][1], q[b][2], region, dim, R[b]);
+            taps_load(q[b][0], q[b][1], q[b][2], data, dim, D[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (!done) {
+                if (!(color < 255 && i < c.max_steps)) {
+                    done = true;
+                } else {
+                    ++i;
+                    if (!in_box(q[b][0], q[b][1], q[b][2], hi)) {
+                        done = true;  // left the convex volume: every later sample is 0
+                    } else {
+                        const int r = (int)taps_value(R[b]);
+                        const float v = taps_value(D[b]);
+                        if constexpr (F64COLOR)
+                            color = (float)((double)color + (double)v * (0.01 + r));
+                        else
+                            color += v * (0.01f + r);
+                    }
+                }
+            }
+        }
+    }
+    image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
+}
+
 // value_at_ref on a z-slab buffer whose plane 0 is global plane zoff (identical arithmetic)
 __device__ __forceinline__ float value_at_slab(float px, float py, float pz, const unsigned char* __restrict__ d, int dim,
                                               int zoff) {
@@ -776,12 +884,37 @@ extern "C" int pcmx_raycast_global(const unsigned char* data, const unsigned cha
                                    int image_dim, const float* cam12, float pixel_width, float step, int max_steps,
                                    int f64_color, hipStream_t s) {
     if (dim <= 1 || image_dim <= 0) return -1;
+    return pcmx_raycast_global_variant(data, region, dim, image, image_dim, cam12, pixel_width, step, max_steps,
+                                       f64_color, 0, s);
+}
+
+// variant 0 (production): 8x8-pixel one-wave tiles, the samples of 8 steps in flight (raycast_ref_batch_kernel; 16 on
+// images of more than 2^16 rays); 1: the round-4 caster (16x16 tiles, one step in flight); 2 / 3: batch kernel with 4 /
+// 16 steps in flight (lab). Identical images.
+extern "C" int pcmx_raycast_global_variant(const unsigned char* data, const unsigned char* region, int dim,
+                                           unsigned char* image, int image_dim, const float* cam12, float pixel_width,
+                                           float step, int max_steps, int f64_color, int variant, hipStream_t s) {
+    if (dim <= 1 || image_dim <= 0 || variant < 0 || variant > 3) return -1;
     const Cam c = make_cam(cam12, pixel_width, step, max_steps);
-    dim3 grid((image_dim + 15) / 16, (image_dim + 15) / 16);
-    if (f64_color)
-        raycast_ref_kernel<true><<<grid, 256, 0, s>>>(data, region, dim, image, image_dim, c);
-    else
-        raycast_ref_kernel<false><<<grid, 256, 0, s>>>(data, region, dim, image, image_dim, c);
+    if (variant == 1) {
+        const dim3 grid((image_dim + 15) / 16, (image_dim + 15) / 16);
+        if (f64_color)
+            raycast_ref_kernel<true><<<grid, 256, 0, s>>>(data, region, dim, image, image_dim, c);
+        else
+            raycast_ref_kernel<false><<<grid, 256, 0, s>>>(data, region, dim, image, image_dim, c);
+        return (int)hipGetLastError();
+    }
+    const dim3 grid((image_dim + 7) / 8, (image_dim + 7) / 8);
+    // production: 8 steps in flight up to 2^16 rays (64^2: 1.97 ms vs 2.06 with 16 and 3.1 with one step), 16 above
+    // (512^2: 5.2 ms vs 7.6 with 4 and 7.1 with one step; scripts/raycast_global_lab.py, profiles/r5_refbase/)
+    const int b = variant == 2 ? 4 : variant == 3 ? 16 : (long long)image_dim * image_dim > (1 << 16) ? 16 : 8;
+#define PCMX_RAYCAST_B(BB)                                                                                         \
+    (f64_color ? raycast_ref_batch_kernel<true, BB><<<grid, 64, 0, s>>>(data, region, dim, image, image_dim, c)     \
+               : raycast_ref_batch_kernel<false, BB><<<grid, 64, 0, s>>>(data, region, dim, image, image_dim, c))
+    if (b == 4) PCMX_RAYCAST_B(4);
+    else if (b == 8) PCMX_RAYCAST_B(8);
+    else PCMX_RAYCAST_B(16);
+#undef PCMX_RAYCAST_B
     return (int)hipGetLastError();
 }
 

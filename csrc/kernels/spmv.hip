@@ -127,11 +127,25 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_csr_items_kernel(
 // pipelined 0.99 ms at 8 slices). Every load and store of the loop is a buffer instruction whose descriptor
 // covers exactly the item's bytes: lanes past the end read 0 / drop their store in hardware, so no memory
 // instruction sits under a branch and the compiler's vmcnt bookkeeping stays exact across the loop.
+// The arrays of a second matrix in a PAIRED launch (pcmx_spmv_sliced_pair): slices with part[s] = 1 read these instead
+// of the kernel arguments (the two row chunks of a distributed column-split step multiply their chunk-0 columns in ONE
+// launch, profiles/r5_spmv/).
+struct SlicePart {
+    const int* col;
+    const float* val;
+    const unsigned short* lrow;
+    const Item* items;
+    float* ypart;
+    float* extra;
+};
 struct SliceMeta {
     long long nz0[kMaxSlices];    // first nonzero of slice s in the slice-major col/val/lrow
     long long item0[kMaxSlices + 1];
+    long long item1[kMaxSlices];  // items of slice s: [item0[s], item1[s])
     long long out0[kMaxSlices];   // first compact partial of slice s
     int colbase[kMaxSlices];      // packed layout: first tail column of slice s
+    unsigned char part[kMaxSlices];  // 1: slice s belongs to the paired matrix `b`
+    SlicePart b;
 };
 // Packed layout (kMode bit 3): ONE 32-bit word per nonzero instead of a 4-B column + a 2-B row offset —
 //   bits 0-20 column - colbase[s] (tail) or the column itself (head, bit 21 set), bits 22-31 the row offset in
@@ -323,10 +337,14 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     const int phase = phase_lo + b / (8 * blocks_per_slice);
     const int s = phase * 8 + (b & 7);
     SlicedCtx k;
-    k.i1 = meta.item0[s + 1];
+    k.i1 = meta.item1[s];
     k.stride = (long long)blocks_per_slice * kWavesPerBlock;
     long long it = meta.item0[s] + (long long)((b >> 3) % blocks_per_slice) * kWavesPerBlock + w;
     if (it >= k.i1) return;
+    if (meta.part[s]) {  // (wave-uniform) a slice of the paired matrix
+        col = meta.b.col, val = meta.b.val, lrow = meta.b.lrow, items = meta.b.items;
+        ypart = meta.b.ypart, extra = meta.b.extra;
+    }
     const long long base = meta.nz0[s];
     k.col = col + base, k.val = val + base, k.lrow = lrow + base;
     k.colbase = meta.colbase[s];
@@ -391,18 +409,13 @@ template <int kCtrl, int kRowMask>
 __device__ __forceinline__ unsigned scan_step_u32(unsigned v) {
     return v + (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
 }
+// The combine of one 64-row chunk c for this lane's row r (the value it stores; 0 past n_rows).
 template <int S>
-__global__ __launch_bounds__(256) void spmv_combine_scan_kernel(const float* __restrict__ comp,
-                                                                const unsigned* __restrict__ mask,
-                                                                const int* __restrict__ base, SliceOut so,
-                                                                float* __restrict__ y, int n_rows) {
+__device__ __forceinline__ float combine_scan_row(const float* __restrict__ comp, const unsigned* __restrict__ mask,
+                                                  const int* __restrict__ base, const SliceOut& so, int n_rows, int c,
+                                                  int lane, int r) {
     static_assert(S % 4 == 0 && S <= 32, "byte-packed slice counters");
     constexpr int D = S / 4;
-    const int g = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);  // as above
-    const int c = __builtin_amdgcn_readfirstlane(g * 4 + (int)threadIdx.x / kWave);
-    const int lane = pcmx::lane_id();
-    const int r = c * kWave + lane;
-    if (c * kWave >= n_rows) return;
     const unsigned m = r < n_rows ? __builtin_nontemporal_load(mask + r) : 0u;
     const int* bc = base + (size_t)c * S;
     unsigned own[D], inc[D];
@@ -444,7 +457,74 @@ __global__ __launch_bounds__(256) void spmv_combine_scan_kernel(const float* __r
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < S; ++k) acc += v[k];
+    return acc;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void spmv_combine_scan_kernel(const float* __restrict__ comp,
+                                                                const unsigned* __restrict__ mask,
+                                                                const int* __restrict__ base, SliceOut so,
+                                                                float* __restrict__ y, int n_rows) {
+    const int g = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);  // as above
+    const int c = __builtin_amdgcn_readfirstlane(g * 4 + (int)threadIdx.x / kWave);
+    const int lane = pcmx::lane_id();
+    const int r = c * kWave + lane;
+    if (c * kWave >= n_rows) return;
+    const float acc = combine_scan_row<S>(comp, mask, base, so, n_rows, c, lane, r);
     if (r < n_rows) y[r] = acc;
+}
+
+// Round 5: the combine with the split-row fix-up and the send-buffer pack in its epilogue — ONE launch per row chunk of
+// a distributed step instead of three (combine, fix-up, pack; profiles/r5_spmv/).
+//  * fix-up: fix_chunk0[c] .. fix_chunk0[c + 1] are the fix entries (item, row; sorted by row) of the wave's 64 rows; each
+//    run of one row is summed exactly as spmv_fixup_kernel sums it (lane-strided from the run's first entry, then the
+//    same wave reduction) and added to the row's combined value: bit-identical to combine + fix-up.
+//  * pack: send_ptr[r] .. send_ptr[r + 1] index the send-buffer slots (send_slot) that carry row r to the peers that
+//    reference it (built once at set-up from the same send lists the gather used): the wave writes its rows' values
+//    straight into the send buffer, so no gather pass re-reads y after the combine (send_ptr == nullptr: no pack).
+template <int S>
+__global__ __launch_bounds__(256) void spmv_combine_fused_kernel(const float* __restrict__ comp,
+                                                                 const unsigned* __restrict__ mask,
+                                                                 const int* __restrict__ base, SliceOut so,
+                                                                 float* __restrict__ y, int n_rows,
+                                                                 const float* __restrict__ extra,
+                                                                 const int2* __restrict__ fix,
+                                                                 const int* __restrict__ fix_chunk0,
+                                                                 const int* __restrict__ send_ptr,
+                                                                 const int* __restrict__ send_slot,
+                                                                 float* __restrict__ sendbuf) {
+    const int g = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);  // as above
+    const int c = __builtin_amdgcn_readfirstlane(g * 4 + (int)threadIdx.x / kWave);
+    const int lane = pcmx::lane_id();
+    const int r = c * kWave + lane;
+    if (c * kWave >= n_rows) return;
+    float acc = combine_scan_row<S>(comp, mask, base, so, n_rows, c, lane, r);
+    if (fix_chunk0) {
+        const int f1 = fix_chunk0[c + 1];
+        for (int k = fix_chunk0[c]; k < f1;) {  // wave-uniform: one run (one row) per iteration
+            const int row = __builtin_amdgcn_readfirstlane(fix[k].y);
+            float part = 0.f;
+            int len = 0;
+            for (int j0 = k;; j0 += kWave) {  // a row's entries are contiguous: the run ends in the first stripe with a gap
+                const int j = j0 + lane;
+                const bool in = j < f1 && fix[j].y == row;
+                if (in) part += extra[fix[j].x];
+                const unsigned long long bin = __builtin_amdgcn_ballot_w64(in);
+                len += __popcll(bin);
+                if (__builtin_amdgcn_ballot_w64(!in) != 0) break;
+            }
+            part = pcmx::wave_reduce<float, 0>(part);
+            if (r == row) acc += part;
+            k += len;
+        }
+    }
+    if (r < n_rows) {
+        y[r] = acc;
+        if (send_ptr) {
+            const int p1 = send_ptr[r + 1];
+            for (int p = send_ptr[r]; p < p1; ++p) sendbuf[send_slot[p]] = acc;
+        }
+    }
 }
 
 // later pieces of split long rows: fix[k] = {item index, row}, sorted by row (item order kept within a row). The
@@ -884,7 +964,10 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
             most = slice_item0[k + 1] - slice_item0[k] > most ? slice_item0[k + 1] - slice_item0[k] : most;
     }
     meta.item0[n_slices] = slice_item0[n_slices];
-    for (int k = 0; k < n_slices; ++k) meta.colbase[k] = slice_colbase ? slice_colbase[k] : 0;
+    for (int k = 0; k < n_slices; ++k) {
+        meta.colbase[k] = slice_colbase ? slice_colbase[k] : 0;
+        meta.item1[k] = slice_item0[k + 1];
+    }
     so.out0[n_slices] = slice_out0[n_slices];
     // bit 4: products only (no combine / fix-up), bit 5: combine + fix-up only — a row-chunked caller runs chunk
     // q's combine on a second stream while chunk q + 1's products run
@@ -944,6 +1027,88 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
 #undef PCMX_COMBINE
     if (n_fix > 0)
         spmv_fixup_kernel<<<(n_fix + 3) / 4, 256, 0, s>>>(extra, reinterpret_cast<const int2*>(fix), n_fix, y);
+    return (int)hipGetLastError();
+}
+
+// Round 5: the products (no combine) of phases [a_lo, a_lo + a_n) of sliced matrix A and [b_lo, b_lo + b_n) of sliced
+// matrix B — two matrices over the SAME x, e.g. the two row chunks of a distributed column-split step multiplying their
+// chunk-0 columns — in ONE launch: a launch of a few items per wave pays its ramp and tail once instead of twice.
+// Production layout only (packed index stream, temporal partial stores unless mode bit 26); item_mode 2: 512-nnz items.
+// meta_*: host arrays nz0 (S), item0 (S + 1), out0 (S + 1), colbase (S) of each matrix.
+extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, int mode, const int* col_a,
+                                     const float* val_a, const void* items_a, float* ypart_a, float* extra_a, int s_a,
+                                     const long long* nz0_a, const long long* item0_a, const long long* out0_a,
+                                     const int* colbase_a, int a_lo, int a_n, const int* col_b, const float* val_b,
+                                     const void* items_b, float* ypart_b, float* extra_b, int s_b,
+                                     const long long* nz0_b, const long long* item0_b, const long long* out0_b,
+                                     const int* colbase_b, int b_lo, int b_n, hipStream_t s) {
+    if (s_a % 8 || s_b % 8 || a_lo < 0 || b_lo < 0 || a_n < 0 || b_n < 0 || 8 * (a_lo + a_n) > s_a ||
+        8 * (b_lo + b_n) > s_b || 8 * (a_n + b_n) > kMaxSlices || (item_mode != 0 && item_mode != 2))
+        return (int)hipErrorInvalidValue;
+    if (a_n + b_n == 0) return 0;
+    SliceMeta meta{};
+    long long most = 0;
+    int m = 0;
+    auto add = [&](int k, const long long* nz0, const long long* item0, const long long* out0, const int* colbase,
+                   int part) {
+        meta.nz0[m] = nz0[k], meta.item0[m] = item0[k], meta.item1[m] = item0[k + 1], meta.out0[m] = out0[k];
+        meta.colbase[m] = colbase[k], meta.part[m] = (unsigned char)part;
+        most = std::max(most, item0[k + 1] - item0[k]);
+        return item0[k + 1] >= item0[k];
+    };
+    for (int k = 8 * a_lo; k < 8 * (a_lo + a_n); ++k, ++m)
+        if (!add(k, nz0_a, item0_a, out0_a, colbase_a, 0)) return (int)hipErrorInvalidValue;
+    for (int k = 8 * b_lo; k < 8 * (b_lo + b_n); ++k, ++m)
+        if (!add(k, nz0_b, item0_b, out0_b, colbase_b, 1)) return (int)hipErrorInvalidValue;
+    meta.b = SlicePart{col_b, val_b, nullptr, reinterpret_cast<const Item*>(items_b), ypart_b, extra_b};
+    if (most <= 0) return 0;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const int persist_blocks = (mode >> 8) & 0xff ? (mode >> 8) & 0xff : kPersistBlocks;
+    const long long need = (most + kWavesPerBlock - 1) / kWavesPerBlock;
+    const long long per = (long long)(cus / 8) * persist_blocks;
+    const int bp = (int)(need < per ? need : per);
+    const unsigned nb = (unsigned)(bp * (m / 8) * 8);
+    const Item* ia = reinterpret_cast<const Item*>(items_a);
+    const dim3 blk(kWavesPerBlock * kWave);
+    const bool ts = !(mode & kModeNtPartials);
+#define PCMX_PAIR(PL, TS)                                                                                           \
+    spmv_sliced_kernel<12, PL, TS><<<nb, blk, 0, s>>>(nullptr, col_a, val_a, x, n_cols, ypart_a, extra_a, ia, meta, bp, 0)
+    if (item_mode == 2)
+        ts ? PCMX_PAIR(8, true) : PCMX_PAIR(8, false);
+    else
+        ts ? PCMX_PAIR(16, true) : PCMX_PAIR(16, false);
+#undef PCMX_PAIR
+    return (int)hipGetLastError();
+}
+
+// Round 5: the combine + fix-up (+ send-buffer pack) of a sliced product in ONE launch (spmv_combine_fused_kernel), for
+// a caller that ran the products alone (pcmx_spmv_sliced with mode bit 4). slice_out0: n_slices + 1 partial offsets;
+// fix_chunk0: n_rows / 64 + 2 entries (or null: no split rows); send_ptr / send_slot / sendbuf: the pack (or null).
+extern "C" int pcmx_spmv_sliced_combine(const float* ypart, const unsigned* row_mask, const int* chunk_base,
+                                        const long long* slice_out0, int n_slices, float* y, int n_rows,
+                                        const float* extra, const void* fix, const int* fix_chunk0, const int* send_ptr,
+                                        const int* send_slot, float* sendbuf, hipStream_t s) {
+    if (n_rows <= 0) return 0;
+    if (n_slices <= 0 || n_slices % 8 || n_slices > kMaxSlices || (fix_chunk0 && !fix) ||
+        (send_ptr && (!send_slot || !sendbuf)) || slice_out0[n_slices] >= (1ll << 30))
+        return (int)hipErrorInvalidValue;
+    SliceOut so{};
+    for (int k = 0; k <= n_slices; ++k) so.out0[k] = slice_out0[k];
+    const unsigned cb = (unsigned)((n_rows + 2047) / 2048) * 8;  // 4 waves of 64 rows per block, XCD-contiguous order
+    const int2* fx = reinterpret_cast<const int2*>(fix);
+#define PCMX_FUSED(K)                                                                                              \
+    spmv_combine_fused_kernel<K><<<cb, 256, 0, s>>>(ypart, row_mask, chunk_base, so, y, n_rows, extra, fx, fix_chunk0, \
+                                                    send_ptr, send_slot, sendbuf)
+    switch (n_slices) {
+        case 8: PCMX_FUSED(8); break;
+        case 16: PCMX_FUSED(16); break;
+        case 24: PCMX_FUSED(24); break;
+        case 32: PCMX_FUSED(32); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef PCMX_FUSED
     return (int)hipGetLastError();
 }
 

@@ -368,7 +368,7 @@ std::vector<float> cam_vec(at::ArrayRef<double> cam12) {
 }
 
 at::Tensor raycast_global(const at::Tensor& data, const at::Tensor& region, int64_t image_dim, at::ArrayRef<double> cam12,
-                          double pixel_width, double step, int64_t max_steps, bool f64_color) {
+                          double pixel_width, double step, int64_t max_steps, bool f64_color, int64_t variant) {
     check_u8_gpu(data, "data"), check_u8_gpu(region, "region");
     check_cubic(data, "raycast_global");
     TORCH_CHECK(region.sizes() == data.sizes() && region.device() == data.device(),
@@ -377,9 +377,9 @@ at::Tensor raycast_global(const at::Tensor& data, const at::Tensor& region, int6
     const at::DeviceGuard g(data.device());
     auto img = at::empty({image_dim, image_dim}, data.options());
     auto c = cam_vec(cam12);
-    check_rc(pcmx_raycast_global(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0), img.data_ptr<uint8_t>(),
-                                 (int)image_dim, c.data(), (float)pixel_width, (float)step, (int)max_steps, f64_color ? 1 : 0,
-                                 cur_stream(data)),
+    check_rc(pcmx_raycast_global_variant(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0),
+                                         img.data_ptr<uint8_t>(), (int)image_dim, c.data(), (float)pixel_width, (float)step,
+                                         (int)max_steps, f64_color ? 1 : 0, (int)variant, cur_stream(data)),
              "raycast_global");
     return img;
 }
@@ -550,6 +550,102 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
     return y;
 }
 
+// Products only of phases [a_lo, a_lo + a_n) of sliced matrix A and [b_lo, b_lo + b_n) of B (same x), ONE launch
+// (pcmx_spmv_sliced_pair). meta_*: the packed spmv_sliced meta (nz0 S | item0 S + 1 | out0 S + 1 | colbase S).
+void spmv_sliced_pair(const at::Tensor& x, int64_t item_mode, int64_t mode, const at::Tensor& col_a,
+                      const at::Tensor& val_a, const at::Tensor& items_a, const at::Tensor& meta_a, at::Tensor ypart_a,
+                      at::Tensor extra_a, int64_t s_a, int64_t a_lo, int64_t a_n, const at::Tensor& col_b,
+                      const at::Tensor& val_b, const at::Tensor& items_b, const at::Tensor& meta_b, at::Tensor ypart_b,
+                      at::Tensor extra_b, int64_t s_b, int64_t b_lo, int64_t b_n) {
+    check_gpu(x, "x", at::kFloat);
+    TORCH_CHECK(x.numel() < (int64_t(1) << 30), "spmv_sliced_pair: x must be < 2^30 elements");
+    auto chk = [&](const at::Tensor& col, const at::Tensor& val, const at::Tensor& items, const at::Tensor& meta,
+                   const at::Tensor& ypart, const at::Tensor& extra, int64_t S, int64_t lo, int64_t n) {
+        check_gpu(col, "col", at::kInt), check_gpu(val, "val", at::kFloat), check_gpu(items, "items", at::kLong);
+        check_gpu(ypart, "ypart", at::kFloat), check_gpu(extra, "extra", at::kFloat);
+        TORCH_CHECK(col.device() == x.device() && val.numel() == col.numel(), "spmv_sliced_pair: col / val");
+        TORCH_CHECK(S >= 8 && S % 8 == 0 && S <= PCMX_SPMV_MAX_SLICES && lo >= 0 && n >= 0 && 8 * (lo + n) <= S,
+                    "spmv_sliced_pair: slices / phases");
+        TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous() && meta.numel() == 4 * S + 2,
+                    "spmv_sliced_pair: packed CPU int64 meta");
+        const int64_t* m = meta.data_ptr<int64_t>();
+        const int64_t* out0 = m + 2 * S + 1;
+        TORCH_CHECK(out0[0] == 0 && ypart.numel() >= out0[S] && m[2 * S] <= items.size(0) && extra.numel() >= items.size(0),
+                    "spmv_sliced_pair: ypart / items / extra shape");
+        for (int64_t k = 0; k < S; ++k)
+            TORCH_CHECK(m[k] >= 0 && m[k] <= col.numel() && m[S + k] <= m[S + k + 1] && m[3 * S + 2 + k] >= 0 &&
+                            m[3 * S + 2 + k] < x.numel(),
+                        "spmv_sliced_pair: meta");
+    };
+    chk(col_a, val_a, items_a, meta_a, ypart_a, extra_a, s_a, a_lo, a_n);
+    chk(col_b, val_b, items_b, meta_b, ypart_b, extra_b, s_b, b_lo, b_n);
+    TORCH_CHECK(8 * (a_n + b_n) <= PCMX_SPMV_MAX_SLICES, "spmv_sliced_pair: at most 32 slices per launch");
+    auto cb = [](const at::Tensor& meta, int64_t S) {
+        std::vector<int> v(S);
+        for (int64_t k = 0; k < S; ++k) v[k] = (int)meta.data_ptr<int64_t>()[3 * S + 2 + k];
+        return v;
+    };
+    const auto cba = cb(meta_a, s_a), cbb = cb(meta_b, s_b);
+    const int64_t *ma = meta_a.data_ptr<int64_t>(), *mb = meta_b.data_ptr<int64_t>();
+    const at::DeviceGuard g(x.device());
+    check_rc(pcmx_spmv_sliced_pair(x.data_ptr<float>(), (int)x.numel(), (int)item_mode, (int)mode, col_a.data_ptr<int>(),
+                                   val_a.data_ptr<float>(), items_a.data_ptr(), ypart_a.data_ptr<float>(),
+                                   extra_a.data_ptr<float>(), (int)s_a, (const long long*)ma, (const long long*)ma + s_a,
+                                   (const long long*)ma + 2 * s_a + 1, cba.data(), (int)a_lo, (int)a_n,
+                                   col_b.data_ptr<int>(), val_b.data_ptr<float>(), items_b.data_ptr(),
+                                   ypart_b.data_ptr<float>(), extra_b.data_ptr<float>(), (int)s_b, (const long long*)mb,
+                                   (const long long*)mb + s_b, (const long long*)mb + 2 * s_b + 1, cbb.data(), (int)b_lo,
+                                   (int)b_n, cur_stream(x)),
+             "spmv_sliced_pair");
+}
+
+// The combine + fix-up (+ send-buffer pack) of the partials a products-only spmv_sliced call (mode bit 4) wrote, in one
+// launch (pcmx_spmv_sliced_combine). meta: the spmv_sliced meta of the same matrix (out0 at [2S + 1, 3S + 2)).
+void spmv_sliced_combine(const at::Tensor& ypart, const at::Tensor& row_mask, const at::Tensor& chunk_base,
+                         const at::Tensor& meta, int64_t n_slices, const at::Tensor& extra, const at::Tensor& fix,
+                         const c10::optional<at::Tensor>& fix_chunk0, at::Tensor out, int64_t n_rows,
+                         const c10::optional<at::Tensor>& send_ptr, const c10::optional<at::Tensor>& send_slot,
+                         const c10::optional<at::Tensor>& sendbuf) {
+    check_gpu(ypart, "ypart", at::kFloat), check_gpu(extra, "extra", at::kFloat), check_gpu(fix, "fix", at::kInt);
+    check_gpu(row_mask, "row_mask", at::kInt), check_gpu(chunk_base, "chunk_base", at::kInt);
+    check_gpu(out, "out", at::kFloat);
+    const int64_t S = n_slices;
+    TORCH_CHECK(S >= 8 && S % 8 == 0 && S <= PCMX_SPMV_MAX_SLICES, "spmv_sliced_combine: 8, 16, 24 or 32 slices");
+    TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous() && meta.numel() >= 3 * S + 2,
+                "spmv_sliced_combine: CPU int64 meta");
+    const int64_t* out0 = meta.data_ptr<int64_t>() + 2 * S + 1;
+    const int64_t chunks = (n_rows + 63) / 64;
+    TORCH_CHECK(row_mask.numel() >= n_rows && chunk_base.numel() >= chunks * S, "spmv_sliced_combine: row_mask / chunk_base");
+    TORCH_CHECK(out0[0] == 0 && ypart.numel() >= out0[S], "spmv_sliced_combine: ypart must hold every compact partial");
+    TORCH_CHECK(out.is_contiguous() && out.numel() >= n_rows && out.device() == ypart.device(), "spmv_sliced_combine: out");
+    TORCH_CHECK(fix.dim() == 2 && fix.size(1) == 2, "spmv_sliced_combine: fix [k, 2]");
+    const int* fc = nullptr;
+    if (fix_chunk0.has_value() && fix.size(0) > 0) {
+        check_gpu(*fix_chunk0, "fix_chunk0", at::kInt);
+        TORCH_CHECK(fix_chunk0->is_contiguous() && fix_chunk0->numel() >= chunks + 1, "spmv_sliced_combine: fix_chunk0");
+        fc = fix_chunk0->data_ptr<int>();
+    } else {
+        TORCH_CHECK(fix.size(0) == 0, "spmv_sliced_combine: split rows need fix_chunk0");
+    }
+    const int *sp = nullptr, *ss = nullptr;
+    float* sb = nullptr;
+    if (send_ptr.has_value()) {
+        TORCH_CHECK(send_slot.has_value() && sendbuf.has_value(), "spmv_sliced_combine: send_ptr needs send_slot and sendbuf");
+        check_gpu(*send_ptr, "send_ptr", at::kInt), check_gpu(*send_slot, "send_slot", at::kInt);
+        check_gpu(*sendbuf, "sendbuf", at::kFloat);
+        TORCH_CHECK(send_ptr->is_contiguous() && send_ptr->numel() >= n_rows + 1 && send_slot->is_contiguous() &&
+                        sendbuf->is_contiguous() && send_slot->numel() <= sendbuf->numel(),
+                    "spmv_sliced_combine: send lists");
+        sp = send_ptr->data_ptr<int>(), ss = send_slot->data_ptr<int>(), sb = sendbuf->data_ptr<float>();
+    }
+    const at::DeviceGuard g(ypart.device());
+    check_rc(pcmx_spmv_sliced_combine(ypart.data_ptr<float>(), reinterpret_cast<const unsigned*>(row_mask.data_ptr<int>()),
+                                      chunk_base.data_ptr<int>(), (const long long*)out0, (int)S, out.data_ptr<float>(),
+                                      (int)n_rows, extra.data_ptr<float>(), fix.data_ptr(), fc, sp, ss, sb,
+                                      cur_stream(ypart)),
+             "spmv_sliced_combine");
+}
+
 at::Tensor spmv_banded(const at::Tensor& vals, const at::Tensor& row_off, int64_t n, int64_t a, int64_t b, int64_t c,
                        int64_t d, int64_t e, const at::Tensor& x, int64_t variant) {
     check_gpu(vals, "vals", at::kFloat), check_gpu(row_off, "row_off", at::kLong), check_gpu(x, "x", at::kFloat);
@@ -629,7 +725,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("volume_gen_(Tensor(a!) data, int seed) -> Tensor(a!)");
     m.def("volume_gen_slab_(Tensor(a!) data, int z_first, int seed) -> Tensor(a!)");
     m.def("raycast_slab_(Tensor data, Tensor region, int z0, Tensor(a!) state, bool init, bool bottom, int image_dim, float[] cam12, float pixel_width, float step, int max_steps) -> Tensor");
-    m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True) -> Tensor");
+    m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True, int variant=0) -> Tensor");
     m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
     m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, int batch=0, int segments=0) -> Tensor");
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
@@ -637,6 +733,8 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("stencil5xT_spans_(Tensor u, Tensor(a!) out, int halo, int steps, int r0a, int r1a, int r0b, int r1b, int global_row0, int global_rows, float k, int shape=0) -> ()");
     m.def("spmv_csr(Tensor row_ptr, Tensor col, Tensor val, Tensor x, Tensor items) -> Tensor");
     m.def("spmv_sliced(Tensor lrow, Tensor col, Tensor val, Tensor x, Tensor items, Tensor row_mask, Tensor chunk_base, Tensor fix, Tensor meta, Tensor(a!) ypart, Tensor(b!) extra, int n_rows, Tensor(c!)? out=None, int mode=0) -> Tensor");
+    m.def("spmv_sliced_pair(Tensor x, int item_mode, int mode, Tensor col_a, Tensor val_a, Tensor items_a, Tensor meta_a, Tensor(a!) ypart_a, Tensor(b!) extra_a, int s_a, int a_lo, int a_n, Tensor col_b, Tensor val_b, Tensor items_b, Tensor meta_b, Tensor(c!) ypart_b, Tensor(d!) extra_b, int s_b, int b_lo, int b_n) -> ()");
+    m.def("spmv_sliced_combine(Tensor ypart, Tensor row_mask, Tensor chunk_base, Tensor meta, int n_slices, Tensor extra, Tensor fix, Tensor? fix_chunk0, Tensor(a!) out, int n_rows, Tensor? send_ptr=None, Tensor? send_slot=None, Tensor(b!)? sendbuf=None) -> ()");
     m.def("spmv_banded(Tensor vals, Tensor row_off, int n, int a, int b, int c, int d, int e, Tensor x, int variant=8) -> Tensor");
     m.def("pack_edges(Tensor tile) -> Tensor");
     m.def("unpack_halo_(Tensor(a!) tile, Tensor buf, int mask, Tensor(b!)? changed=None) -> ()");
@@ -671,6 +769,8 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("stencil5xT_spans_", stencil5xT_spans_);
     m.impl("spmv_csr", spmv_csr);
     m.impl("spmv_sliced", spmv_sliced);
+    m.impl("spmv_sliced_pair", spmv_sliced_pair);
+    m.impl("spmv_sliced_combine", spmv_sliced_combine);
     m.impl("spmv_banded", spmv_banded);
     m.impl("pack_edges", pack_edges);
     m.impl("unpack_halo_", unpack_halo_);

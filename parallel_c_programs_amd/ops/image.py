@@ -182,7 +182,7 @@ def default_camera(image_dim: int) -> Camera:
 
 
 def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, method: str = "global",
-            cam: Camera | None = None, batch: int = 0, segments: int = 0) -> torch.Tensor:
+            cam: Camera | None = None, batch: int = 0, segments: int = 0, variant: int = 0) -> torch.Tensor:
     """Render the volume (ray marching, trilinear sampling of data and region).
 
     method: "global" — bit-compatible with the reference's serial/global-memory caster (f64 colour update);
@@ -190,7 +190,9 @@ def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, meth
             (texel-centre addressing, correct weights, 8-bit fractional weights) on a packed brick volume;
             `batch` = its march steps per prefetch batch (1, 4, 8, 16: same image; 0 = 16, the fastest);
             `segments` = waves sharing one ray patch, each marching a contiguous share of the steps (1, 2, 4;
-            0 = the fastest; partial colours are composed in ray order, so images agree up to f32 rounding).
+            0 = the fastest; partial colours are composed in ray order, so images agree up to f32 rounding);
+            `variant` (global methods) = caster variant: 0 the production caster (8 steps' samples in flight), 1 the
+            one-step-in-flight form, 2 / 3 4 / 16 steps in flight (lab; identical images).
     """
     cam = cam or default_camera(image_dim)
     if not data.is_cuda:
@@ -203,7 +205,7 @@ def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, meth
     o = ops()
     if method in ("global", "global_f32"):
         return o.raycast_global(data, region, int(image_dim), cam.cam12(), float(cam.pixel_width),
-                                float(cam.step_size), int(cam.max_steps), method == "global")
+                                float(cam.step_size), int(cam.max_steps), method == "global", int(variant))
     if method == "texture":
         tex = o.brick_pack(data, region)
         return o.raycast_bricked(tex, int(image_dim), cam.cam12(), float(cam.pixel_width), float(cam.step_size),

@@ -168,6 +168,11 @@ class SlicedCSR:
         fix = torch.cat(fix)
         fix = fix[torch.sort(fix[:, 1], stable=True).indices]  # by row, item order kept: deterministic fix-up sums
         self.fix = fix.to(torch.int32).contiguous().to(dev)
+        # fix range of every 64-row combine chunk (the fused combine's fix-up epilogue): entries [fc[c], fc[c + 1])
+        n_ch = (n + 63) // 64
+        self.fix_chunk0 = torch.searchsorted(self.fix[:, 1].contiguous().long(),
+                                             torch.arange(0, n_ch + 2, device=dev) * 64).to(torch.int32).contiguous()
+        self.fused_combine = True  # combine + fix-up (+ pack) in one launch (False: the in-library two-launch form)
         self.row_mask = mask.to(torch.int32).contiguous()  # bit 31 wraps into the sign: read as u32 on device
         self.chunk_base = base.contiguous()
         self.meta = torch.cat([nz0, torch.tensor(item0, dtype=torch.int64), torch.tensor(out0, dtype=torch.int64)])
@@ -199,12 +204,49 @@ class SlicedCSR:
         """Compact partials per product (touched (row, slice) pairs)."""
         return int(self.meta[-1])
 
+    def products_pair(self, other: SlicedCSR, x: torch.Tensor, phases: tuple[int, int],
+                      other_phases: tuple[int, int], mode: int = 0) -> None:
+        """The products (no combine) of phases `phases` = (lo, n) of this matrix and `other_phases` of `other` (another
+        sliced matrix over the same x) in ONE launch; each matrix then combines its own partials as after a
+        products-only call (the distributed column-split step's two row chunks, chunk-0 columns)."""
+        for m in (self, other):
+            if m.cr is None:
+                raise ValueError("products_pair: packed index stream only")
+            if getattr(m, "_meta_packed", None) is None:
+                m._meta_packed = torch.cat([m.meta, torch.tensor(m.colbase, dtype=torch.int64)]).contiguous()
+                m._no_lrow = torch.empty(0, dtype=torch.int16, device=m.cr.device)
+        if self.mode != other.mode:
+            raise ValueError("products_pair: both matrices need the same item size")
+        ops().spmv_sliced_pair(x, self.mode, int(mode), self.cr, self.val, self.items, self._meta_packed, self.ypart,
+                               self.extra, self.n_slices, int(phases[0]), int(phases[1]), other.cr, other.val,
+                               other.items, other._meta_packed, other.ypart, other.extra, other.n_slices,
+                               int(other_phases[0]), int(other_phases[1]))
+
+    def combine(self, out: torch.Tensor, send: tuple | None = None) -> torch.Tensor:
+        """The combine + split-row fix-up of the partials the last products-only call wrote, into out[:n_rows], in ONE
+        launch; send = (send_ptr, send_slot, sendbuf): also write every row's value into the send-buffer slots that
+        carry it to the peers (the distributed step's pack, fused into the same launch)."""
+        meta = self._meta_packed if getattr(self, "_meta_packed", None) is not None else self.meta
+        sp, ss, sb = send if send is not None else (None, None, None)
+        ops().spmv_sliced_combine(self.ypart, self.row_mask, self.chunk_base, meta, self.n_slices, self.extra,
+                                  self.fix, self.fix_chunk0, out, self.n_rows, sp, ss, sb)
+        return out
+
     def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None, mode: int = 0,
-             phases: tuple[int, int] | None = None) -> torch.Tensor:
+             phases: tuple[int, int] | None = None, send: tuple | None = None) -> torch.Tensor:
         """y = A x; `out` (contiguous f32, >= n_rows elements) receives y in place when given. mode bit 4: products
         only (compact partials, no combine), bit 5: combine + fix-up only (of the partials a bit-4 call wrote).
         phases=(lo, n): the products of slices [8 lo, 8 (lo + n)) only (one slice per XCD per phase) — with col_split,
-        phases (0, S/16) multiply the columns below the split and (S/16, S/16) the others."""
+        phases (0, S/16) multiply the columns below the split and (S/16, S/16) the others. A combining call runs the
+        fused combine (combine + fix-up in one launch, and the send-buffer pack when `send` is given; see combine())."""
+        if self.fused_combine and not (mode & 16) and (mode & ~32 & 0xCF) == 0 and self.cr is not None:
+            if out is None:
+                out = torch.empty(self.n_rows, dtype=torch.float32, device=x.device)
+            if not (mode & 32):
+                self.spmv(x, mode=mode | 16, phases=phases)
+            return self.combine(out, send)
+        if send is not None:
+            raise ValueError("send: the fused combine only (production layout)")
         if phases is not None:
             lo, n = phases
             if not (0 <= lo and 0 < n and lo + n <= self.n_slices // 8):

@@ -100,15 +100,16 @@ class ColSplitCSR:
         return y
 
 
-def _sliced_product_phase(self: SlicedCSR, x: torch.Tensor, phase: int, key=0, dst: torch.Tensor | None = None) -> None:
+def _sliced_product_phase(self: SlicedCSR, x: torch.Tensor, phase: int, key=0, dst: torch.Tensor | None = None,
+                          send: tuple | None = None) -> None:
     """Column-split product of a SlicedCSR: phase 0 = the products of the slices below the split (partials only),
-    phase 1 = the products of the others, then the combine + fix-up into dst."""
+    phase 1 = the products of the others, then the combine + fix-up (+ the send-buffer pack, `send`) into dst."""
     half = self.n_slices // 16
     if phase == 0:
         self.spmv(x, mode=16, phases=(0, half))
     else:
         self.spmv(x, mode=16, phases=(half, half))
-        self.spmv(x, dst, mode=32)
+        self.spmv(x, dst, mode=32, send=send)
 
 
 SlicedCSR.product_phase = _sliced_product_phase
@@ -176,6 +177,10 @@ class DistributedSpMV:
                 part = part.plan()
             self.parts.append((a, b, part))
         self._pending = [[], []]  # column split: the exchange works of the previous step's chunks 0 and 1
+        # the send-buffer pack in the sliced product's combine epilogue (False: a separate gather pass, the round-4 form)
+        self.fuse_pack = True
+        # the two chunk-0-column product launches of a column-split step as ONE paired launch (False: two launches)
+        self.pair_phase0 = True
         del col
         if not keep_plain:
             del m
@@ -227,6 +232,7 @@ class DistributedSpMV:
         self.ghost_ids, self.ghost_pos = need, pos
         self.send_idx, self.send_counts, self.sendbuf = [torch.zeros(0, dtype=torch.int32, device=dev)] * C, \
             [[0] * W for _ in range(C)], [torch.zeros(0, device=dev)] * C
+        self.send_csr = None
         if ctx.distributed:  # (a Context without a process group only emulates one rank's products)
             # send side: tell every owner which of its rows this rank needs (counts, then ids, owner-major)
             dev_c = dev if ctx.backend == "nccl" else torch.device("cpu")
@@ -245,6 +251,17 @@ class DistributedSpMV:
                 self.send_idx.append((got[sel] - c * L + self.seg[c * W + r]).to(torch.int32).contiguous())
                 self.send_counts.append(torch.bincount(peer[sel], minlength=W).tolist())
             self.sendbuf = [torch.empty(ix.numel(), dtype=torch.float32, device=dev) for ix in self.send_idx]
+            # the same send lists inverted per own row (send_ptr: CSR over the chunk's rows, send_slot: slots in
+            # sendbuf[c]): the sliced product's fused combine writes each row's value into its slots itself
+            self.send_csr = []
+            for c in range(C):
+                rows_c = max(0, min((c + 1) * L, self.rows) - min(c * L, self.rows))
+                lr = (self.send_idx[c].long() - self.seg[c * W + r])
+                order = torch.sort(lr, stable=True).indices
+                ptr = torch.zeros(rows_c + 1, dtype=torch.int64, device=dev)
+                if rows_c:
+                    ptr[1:] = torch.bincount(lr, minlength=rows_c).cumsum(0)
+                self.send_csr.append((ptr.to(torch.int32).contiguous(), order.to(torch.int32).contiguous()))
         self.n_ghost = int(need.numel())
         return out
 
@@ -333,14 +350,21 @@ class DistributedSpMV:
         else:
             dst.copy_(spmv(part, xp))
 
-    def _post_chunk(self, out: torch.Tensor, c: int):
+    def _send(self, c: int, part) -> tuple | None:
+        """The fused pack of chunk c (send_ptr, send_slot, sendbuf) when its product is a sliced one, else None."""
+        if not self.sliced or self.send_csr is None or self.exchange != "ghost" or not self.fuse_pack:
+            return None
+        ptr, slot = self.send_csr[c]
+        return (ptr, slot, self.sendbuf[c])
+
+    def _post_chunk(self, out: torch.Tensor, c: int, packed: bool = False):
         """Ghost exchange of chunk c: pack this rank's send entries (one index_select), then ONE collective
         (Context.exchange: a list all_to_all on RCCL, the per-peer sends/receives grouped over the xGMI links) whose
         per-peer receive entries are views of the chunk's ghost region (segments in rank order), so the entries
         land in place. One collective call instead of a batch of per-peer P2P ops keeps the N = 8 step off the
         host-launch bound (scripts/host_overhead_lab.py)."""
         W, r = self.ctx.world, self.ctx.rank
-        if self.send_idx[c].numel():
+        if self.send_idx[c].numel() and not packed:
             gather_(out, self.send_idx[c], self.sendbuf[c])
         ins, outs, so = [], [], 0
         for q in range(W):
@@ -370,16 +394,28 @@ class DistributedSpMV:
         no exchange is exposed (4 product launches per step instead of 2)."""
         W, r = self.ctx.world, self.ctx.rank
         self._wait(0)
-        for c, (a, b, part) in enumerate(self.parts):
-            if b > a:
-                part.product_phase(xp, 0, c)
+        (a0, b0, p0), (a1, b1, p1) = self.parts
+        if self.pair_phase0 and b0 > a0 and b1 > a1 and isinstance(p0, SlicedCSR) and isinstance(p1, SlicedCSR) \
+                and p0.cr is not None and p1.cr is not None and p0.n_slices + p1.n_slices <= 64:
+            # both row chunks' chunk-0-column products in ONE launch (a launch of a few items per wave pays its ramp
+            # and tail once: scripts/spmv_host_lab.py, profiles/r5_spmv/)
+            h0, h1 = p0.n_slices // 16, p1.n_slices // 16
+            p0.products_pair(p1, xp, (0, h0), (0, h1))
+        else:
+            for c, (a, b, part) in enumerate(self.parts):
+                if b > a:
+                    part.product_phase(xp, 0, c)
         self._wait(1)
         pending = [[], []]
         for c, (a, b, part) in enumerate(self.parts):
             s0 = self.seg[c * W + r]
+            send = self._send(c, part) if b > a else None
             if b > a:
-                part.product_phase(xp, 1, c, out[s0:s0 + (b - a)])
-            pending[c] = self._post_chunk(out, c)
+                if send is not None:
+                    part.product_phase(xp, 1, c, out[s0:s0 + (b - a)], send=send)
+                else:
+                    part.product_phase(xp, 1, c, out[s0:s0 + (b - a)])
+            pending[c] = self._post_chunk(out, c, packed=send is not None)
         self._pending = pending
         return out
 
@@ -402,14 +438,18 @@ class DistributedSpMV:
             else:
                 s0 = self.seg[c * W + self.ctx.rank]
                 dst = out[s0:s0 + (b - a)]
+            send = self._send(c, part) if b > a and self.ctx.distributed else None
             if b > a:
-                self._mul(part, xp, dst)
+                if send is not None:
+                    part.spmv(xp, dst, send=send)  # product + combine + fix-up + pack
+                else:
+                    self._mul(part, xp, dst)
             if not self.ctx.distributed:
                 continue
             if self.exchange == "allgather":
                 works.append(dist.all_gather_into_tensor(out[c * W * L:(c + 1) * W * L], self.send[c], async_op=True))
             else:
-                works += self._post_chunk(out, c)
+                works += self._post_chunk(out, c, packed=send is not None)
         for w in works:
             w.wait()
         return out

@@ -1,7 +1,7 @@
-"""SpMV host-overhead lab (round 4): is one N = 8 rank's column-split step launch-bound? One rank's products emulated
-on one GPU (no exchange), the step's host work without the collectives (4 product launches, 2 combine + fix-up
-launches, 2 send-buffer packs): host time per step measured by enqueueing K steps back to back with no sync
-(perf_counter) against the device time of the same K steps (events). The two exchange calls a real step adds cost
+"""SpMV rank lab (rounds 4-5): one N = 8 rank's column-split step emulated on one GPU (no exchange): 4 product launches
+and per row chunk either the round-4 combine, fix-up and gather pack (three launches) or the round-5 fused combine
+(combine + fix-up + send-buffer pack in one launch), interleaved A/B rounds in one process, bit-identity checked; and
+the host enqueue time of the production step against its device time. The two exchange calls a real step adds cost
 ~13-19 us of host time each (scripts/host_overhead_lab.py, profiles/r2_bench/host_overhead_lab.txt).
 Run: python scripts/spmv_host_lab.py [world] [reps]"""
 import os
@@ -40,92 +40,70 @@ def main():
     from parallel_c_programs_amd.ops.vector import gather_
     print(f"send entries per step {sum(p.numel() for p in packs)}, ghosts received {d.n_ghost}", flush=True)
 
-    def step(pack="gather"):
+    # the same send lists inverted per own row for the fused pack (DistributedSpMV.send_csr)
+    send_csr = []
+    for c, (a, b, _) in enumerate(d.parts):
+        lr = packs[c] - d.seg[c * Wd + r]
+        order = torch.sort(lr, stable=True).indices
+        ptr = torch.zeros(b - a + 1, dtype=torch.int64, device=dev)
+        ptr[1:] = torch.bincount(lr, minlength=b - a).cumsum(0)
+        send_csr.append((ptr.to(torch.int32), order.to(torch.int32), torch.empty_like(bufs[c])))
+
+    def step(kind="paired"):
+        """kind r4: combine, fix-up and the gather pack as three launches per chunk (round 4); fused_fixup: combine +
+        fix-up in one launch, then the gather; fused_pack: combine + fix-up + pack in ONE launch; paired (production):
+        fused_pack with both chunks' chunk-0-column products in ONE launch"""
         for c, (a, b, part) in enumerate(d.parts):
-            if b > a:
-                part.product_phase(xp, 0, c)
+            part.fused_combine = kind != "r4"
+        if kind == "paired":
+            (_, _, p0), (_, _, p1) = d.parts
+            p0.products_pair(p1, xp, (0, p0.n_slices // 16), (0, p1.n_slices // 16))
+        else:
+            for c, (a, b, part) in enumerate(d.parts):
+                if b > a:
+                    part.product_phase(xp, 0, c)
         for c, (a, b, part) in enumerate(d.parts):
             s0 = d.seg[c * Wd + r]
-            if b > a:
-                part.product_phase(xp, 1, c, out[s0:s0 + (b - a)])
-            if pack == "index_select":
-                torch.index_select(out, 0, packs[c], out=bufs[c])
-            elif pack:
-                gather_(out, packs32[c], bufs[c])
-
-    side = torch.cuda.Stream(device=dev)
-    ev = torch.cuda.Event()
-
-    def step_overlap():
-        """chunk 0's combine + fix-up + pack on a side stream, beside chunk 1's phase-1 products"""
-        main = torch.cuda.current_stream(dev)
-        for c, (a, b, part) in enumerate(d.parts):
-            if b > a:
-                part.product_phase(xp, 0, c)
-        for c, (a, b, part) in enumerate(d.parts):
-            s0 = d.seg[c * Wd + r]
-            half = part.n_slices // 16
-            part.spmv(xp, mode=16, phases=(half, half))
-            if c == 0:
-                ev.record(main)
-                side.wait_event(ev)
-                with torch.cuda.stream(side):
-                    part.spmv(xp, out[s0:s0 + (b - a)], mode=32)
-                    gather_(out, packs32[c], bufs[c])
+            if kind in ("fused_pack", "paired"):
+                part.product_phase(xp, 1, c, out[s0:s0 + (b - a)], send=send_csr[c])
             else:
-                part.spmv(xp, out[s0:s0 + (b - a)], mode=32)
-                gather_(out, packs32[c], bufs[c])
-        main.wait_stream(side)
+                part.product_phase(xp, 1, c, out[s0:s0 + (b - a)])
+                if kind:
+                    gather_(out, packs32[c], bufs[c])
 
-    for _ in range(10):
-        step()
-        step_overlap()
+    def dev_ms(fn):
+        for _ in range(5):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    # bit-identity of the three forms (out rows and send buffers)
+    step("r4")
+    ref_out, ref_bufs = out.clone(), [bb.clone() for bb in bufs]
+    for kind in ("fused_pack", "paired"):
+        out.zero_()
+        step(kind)
+        same = torch.equal(out, ref_out) and all(torch.equal(send_csr[c][2], ref_bufs[c]) for c in range(len(bufs)))
+        print(f"{kind}: bit-identical to the round-4 combine, fix-up, gather: {same}", flush=True)
+    for rnd in range(3):  # interleaved rounds
+        for kind in ("r4", "fused_fixup", "fused_pack", "paired", ""):
+            t = dev_ms(lambda: step(kind))
+            print(f"round {rnd} N={W} step {kind or 'no packs (r4 combine)'}: device {t:.4f} ms/step", flush=True)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
     t0 = time.perf_counter()
     for _ in range(reps):
         step()
     t1 = time.perf_counter()
-    e1.record()
-    e1.synchronize()
+    torch.cuda.synchronize()
     host = (t1 - t0) / reps * 1e3
-    devt = e0.elapsed_time(e1) / reps
-    e0.record()
-    for _ in range(reps):
-        step(False)
-    e1.record()
-    e1.synchronize()
-    print(f"N={W} products only (no packs): device {e0.elapsed_time(e1) / reps:.4f} ms/step", flush=True)
-    e0.record()
-    for _ in range(reps):
-        step("index_select")
-    e1.record()
-    e1.synchronize()
-    print(f"N={W} with torch.index_select (int64) packs: device {e0.elapsed_time(e1) / reps:.4f} ms/step", flush=True)
-    e0.record()
-    for _ in range(reps):
-        step_overlap()
-    e1.record()
-    e1.synchronize()
-    print(f"N={W} chunk 0's combine + pack on a side stream beside chunk 1's products: device "
-          f"{e0.elapsed_time(e1) / reps:.4f} ms/step", flush=True)
-    for pb in (1, 2, 3, 4, 6, 8):  # resident sliced blocks per CU of the product launches (kernel mode bits 8-15)
-        def products_pb():
-            for ph in (0, 1):
-                for c, (a, b, part) in enumerate(d.parts):
-                    half = part.n_slices // 16
-                    part.spmv(xp, mode=16 | (pb << 8), phases=(ph * half, half))
-        for _ in range(3):
-            products_pb()
-        e0.record()
-        for _ in range(reps):
-            products_pb()
-        e1.record()
-        e1.synchronize()
-        print(f"N={W} the 4 product launches alone, {pb} resident blocks per CU: {e0.elapsed_time(e1) / reps:.4f} ms/step",
-              flush=True)
-    print(f"N={W} rank 0 column-split step: host enqueue {host:.4f} ms/step, device {devt:.4f} ms/step "
+    devt = dev_ms(step)
+    print(f"N={W} rank 0 column-split step (production): host enqueue {host:.4f} ms/step, device {devt:.4f} ms/step "
           f"({'launch-bound' if host > devt else 'device-bound'}; + ~0.03 ms of host time for the 2 exchange calls)",
           flush=True)
 

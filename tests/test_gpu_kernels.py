@@ -396,6 +396,40 @@ def test_spmv_banded_vs_host(gpu):
     assert (out_csr - ref).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("slices,item", [(16, 512), (24, 1024)])
+def test_spmv_fused_combine_bit_identical(gpu, slices, item):
+    """The round-5 fused combine (combine + split-row fix-up + send-buffer pack in ONE launch) against the two-launch
+    combine + fix-up and a gather of the same send lists: same y bits, same send-buffer bits, on a power-law matrix
+    whose hub rows are split into many items (fix-up entries)."""
+    from parallel_c_programs_amd.ops.sparse import SlicedCSR
+    from parallel_c_programs_amd.ops.vector import gather_
+
+    m = ops.powerlaw_csr(300_000, 4_000_000, alpha=2.1, seed=5)
+    sc = SlicedCSR(m.to(gpu), slices, item_nnz=item)
+    assert sc.fix.shape[0] > 0  # split rows present
+    x = torch.rand(m.n_cols, device=gpu)
+    sc.fused_combine = False
+    ref = sc.spmv(x)
+    sc.fused_combine = True
+    got = sc.spmv(x)
+    assert torch.equal(got, ref)
+    # a send list: each row to 0..3 slots (random), as the distributed step's per-peer lists
+    g = torch.Generator(device=gpu).manual_seed(1)
+    reps = torch.randint(0, 4, (sc.n_rows,), device=gpu, generator=g)
+    rows = torch.repeat_interleave(torch.arange(sc.n_rows, device=gpu), reps)
+    slot_of = torch.randperm(rows.numel(), device=gpu, generator=g)  # entry k of the row-sorted list -> buffer slot
+    ptr = torch.zeros(sc.n_rows + 1, dtype=torch.int64, device=gpu)
+    ptr[1:] = reps.cumsum(0)
+    buf = torch.full((rows.numel(),), float("nan"), device=gpu)
+    y = torch.empty_like(ref)
+    sc.spmv(x, y, send=(ptr.to(torch.int32), slot_of.to(torch.int32), buf))
+    want = torch.empty_like(buf)
+    idx = torch.empty_like(slot_of)
+    idx[slot_of] = rows  # slot -> row
+    gather_(ref, idx.to(torch.int32), want)
+    assert torch.equal(y, ref) and torch.equal(buf, want)
+
+
 def test_spmv_powerlaw_vs_dense(gpu):
     m = ops.powerlaw_csr(3000, 200_000, alpha=2.2, seed=11)
     x = torch.rand(3000)
