@@ -939,6 +939,9 @@ extern "C" int pcmx_spmv_csr(const long long* row_ptr, const int* col, const flo
 // 1e8 nnz, bit-identical; scripts/spmv_store_lab.py, profiles/r4_spmv/store_temporal_partials.txt). mode bit 26 (lab,
 // an explicit per-call parameter): non-temporal partial stores instead.
 constexpr int kModeNtPartials = 1 << 26;
+// mode bit 27: items of 256 nonzeros (4 per lane; packed layout only) — the short launches of a distributed rank's
+// column-split step give each wave only a few items, so shorter items spread the same work over more of them
+constexpr int kMode256 = 1 << 27;
 
 extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x,
                                 float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
@@ -988,13 +991,17 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
         if (slice_colbase) {
 #define PCMX_SLICED_TS(M, PL) spmv_sliced_kernel<M, PL, true><<<nb, blk, 0, s>>>(lrow, col, val, x, n_cols, ypart, extra, it, meta, bp, ph_lo)
             const bool ts = !(mode & kModeNtPartials);
-            if ((mode & 7) == 2)
+            if (mode & kMode256)
+                (ts ? PCMX_SLICED_TS(12, 4) : PCMX_SLICED(12, 4));
+            else if ((mode & 7) == 2)
                 (ts ? PCMX_SLICED_TS(12, 8) : PCMX_SLICED(12, 8));
             else if ((mode & 7) == 0)
                 (ts ? PCMX_SLICED_TS(12, 16) : PCMX_SLICED(12, 16));
             else
                 return (int)hipErrorInvalidValue;  // the lab modes read the unpacked layout
 #undef PCMX_SLICED_TS
+        } else if (mode & kMode256) {
+            return (int)hipErrorInvalidValue;  // 256-nonzero items: packed layout only
         } else switch (mode & 7) {
             case 0: PCMX_SLICED(4, 16); break;
             case 1: PCMX_SLICED(5, 16); break;
@@ -1033,7 +1040,8 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
 // Round 5: the products (no combine) of phases [a_lo, a_lo + a_n) of sliced matrix A and [b_lo, b_lo + b_n) of sliced
 // matrix B — two matrices over the SAME x, e.g. the two row chunks of a distributed column-split step multiplying their
 // chunk-0 columns — in ONE launch: a launch of a few items per wave pays its ramp and tail once instead of twice.
-// Production layout only (packed index stream, temporal partial stores unless mode bit 26); item_mode 2: 512-nnz items.
+// Production layout only (packed index stream, temporal partial stores unless mode bit 26); item_mode 2 / 4: 512 / 256-nnz
+// items (0: 1024).
 // meta_*: host arrays nz0 (S), item0 (S + 1), out0 (S + 1), colbase (S) of each matrix.
 extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, int mode, const int* col_a,
                                      const float* val_a, const void* items_a, float* ypart_a, float* extra_a, int s_a,
@@ -1043,7 +1051,7 @@ extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, 
                                      const long long* nz0_b, const long long* item0_b, const long long* out0_b,
                                      const int* colbase_b, int b_lo, int b_n, hipStream_t s) {
     if (s_a % 8 || s_b % 8 || a_lo < 0 || b_lo < 0 || a_n < 0 || b_n < 0 || 8 * (a_lo + a_n) > s_a ||
-        8 * (b_lo + b_n) > s_b || 8 * (a_n + b_n) > kMaxSlices || (item_mode != 0 && item_mode != 2))
+        8 * (b_lo + b_n) > s_b || 8 * (a_n + b_n) > kMaxSlices || (item_mode != 0 && item_mode != 2 && item_mode != 4))
         return (int)hipErrorInvalidValue;
     if (a_n + b_n == 0) return 0;
     SliceMeta meta{};
@@ -1075,7 +1083,9 @@ extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, 
     const bool ts = !(mode & kModeNtPartials);
 #define PCMX_PAIR(PL, TS)                                                                                           \
     spmv_sliced_kernel<12, PL, TS><<<nb, blk, 0, s>>>(nullptr, col_a, val_a, x, n_cols, ypart_a, extra_a, ia, meta, bp, 0)
-    if (item_mode == 2)
+    if (item_mode == 4)
+        ts ? PCMX_PAIR(4, true) : PCMX_PAIR(4, false);
+    else if (item_mode == 2)
         ts ? PCMX_PAIR(8, true) : PCMX_PAIR(8, false);
     else
         ts ? PCMX_PAIR(16, true) : PCMX_PAIR(16, false);

@@ -106,6 +106,18 @@ def main():
     print(f"N={W} rank 0 column-split step (production): host enqueue {host:.4f} ms/step, device {devt:.4f} ms/step "
           f"({'launch-bound' if host > devt else 'device-bound'}; + ~0.03 ms of host time for the 2 exchange calls)",
           flush=True)
+    if os.environ.get("SPMV_LAB_N1", "1") == "1":
+        # the same-box N = 1 step (the bench's single-GPU section: 1e8 nnz, one sliced product) for the efficiency model
+        del d, out, bufs, send_csr, packs, packs32
+        torch.cuda.empty_cache()
+        d1 = DistributedSpMV.powerlaw(Context(rank=0, world=1, device=dev), 10_000_000, 100_000_000, slices=-1)
+        x1 = torch.rand(d1.n_pad, device=dev)
+        (_, _, p1), = d1.parts
+        y1 = torch.empty(p1.n_rows, device=dev)
+        t1 = min(dev_ms(lambda: p1.spmv(x1, y1)) for _ in range(3))
+        t8 = devt
+        print(f"N=1 step (same box, same process): device {t1:.4f} ms; N={W} production step {t8:.4f} ms -> modelled "
+              f"N={W} efficiency t1 / ({W} t{W}) = {100 * t1 / (W * t8):.1f}% (exchange hidden)", flush=True)
 
 
 if __name__ == "__main__":
