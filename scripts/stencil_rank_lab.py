@@ -14,7 +14,7 @@ full-grid time this bounds the strong-scaling efficiency of the compute part (do
 Run: python scripts/stencil_rank_lab.py [fuse ...]
 Env: STENCIL_LAB_WORLDS=8 (subset of 1,2,4,8), STENCIL_LAB_RPW=0,18 (rows per wave forced on the non-edge launches
 as an explicit launch shape of each call, ops.stencil.launch_shape; 0 = production rule; one line per value, all in one
-process for an A/B); STENCIL_LAB_DEEP=2,3,4 (halo depths m); STENCIL_LAB_VARIANT=2: the compile-time row-count pipeline where the shape is instantiated.
+process for an A/B); STENCIL_LAB_DEEP=2,3,4 (halo depths m); STENCIL_LAB_VARIANT=2: the skewed level pipeline (ops.stencil.launch_shape).
 """
 import os
 import sys
