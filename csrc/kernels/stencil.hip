@@ -422,14 +422,7 @@ __device__ __forceinline__ void buffer_store_row(const typename RawT<NP>::type& 
 }
 
 // The row pipeline of one interior wave (no Dirichlet row or column in reach).
-// kSkew (round 5, launch variant 2): level t+1 computes row i - 2t - 1 at iteration i instead of row i - t - 1, so it
-// reads only level-t rows finished in EARLIER iterations and the T level updates of one iteration are independent
-// (no level-to-level dependency chain inside an iteration: one wave has T times the instruction-level parallelism).
-// The levels run from the top down so each level reads its input ring before the level below overwrites the oldest
-// slot (3-slot rings still suffice); the loop runs T - 1 iterations longer, with the same level rows computed (the
-// trapezoid tests skip the rows outside it at both ends), so the work and the arithmetic are unchanged: bit-identical.
-// Ring slots: level t row x lives in slot (x - i0) % 3 at every level (compile-time: ib - i0 is a multiple of kAhead).
-template <int T, int kAhead, int NP, bool kSkew = false>
+template <int T, int kAhead, int NP>
 __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, const __amdgpu_buffer_rsrc_t ro, unsigned vld,
                                             unsigned vst, int sr0, int pitch, int slab_rows, int halo, int rs, int i0,
                                             int i1, float k) {
@@ -438,7 +431,7 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
         const int sr = min(max(r + halo, 0), slab_rows - 1);
         return buffer_load_row<NP>(ru, vld, (sr - sr0) * pitch);
     };
-    // ring[t][slot]: level t (0 = u) row x in slot (x - i0) % 3, as exact floats in pair layout
+    // ring[t][slot]: level t (0 = u) row with (row index - first) % 3 == slot, as exact floats in pair layout
     RowP<NP> ring[T][3];
 #pragma unroll
     for (int t = 0; t < T; ++t)
@@ -450,37 +443,31 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
 #pragma unroll
     for (int j = 0; j < kAhead; ++j) pre[j] = fetch(min(i0 + j, i1 - 1));
     // (a branch-free main loop — the per-level trapezoid / store tests peeled into the first 2T rows — measured no
-    // faster at any shape and spilled at 8 columns per lane: profiles/r4_stencil/peel_rpw128_rejected.txt; round 5: a
-    // steady-state turn with no guard at all raised the 8-column kernels to 256 VGPRs, 33% slower, and still carried
-    // the vmcnt(0) at the loop head; a compile-time row count per wave (the loop fully unrolled, exact per-load waits)
-    // was bit-exact and no faster: profiles/r5_stencil/README.md)
-    const int iend = kSkew ? i1 + T - 1 : i1;  // the skewed last level finishes T - 1 iterations later
-    for (int ib = i0; ib < iend; ib += kAhead) {
+    // faster at any shape and spilled at 8 columns per lane: profiles/r4_stencil/peel_rpw128_rejected.txt. Round 5,
+    // profiles/r5_stencil/README.md: a steady-state turn with no guard at all raised the 8-column kernels to 256
+    // VGPRs, 33% slower, and still carried the vmcnt(0) at the loop head; a compile-time row count per wave (the loop
+    // fully unrolled, exact per-load waits) was bit-exact and no faster; a skewed schedule (level t+1 two rows behind
+    // level t, so the T level updates of one iteration are independent) was bit-exact and 2-12% slower)
+    for (int ib = i0; ib < i1; ib += kAhead) {
 #pragma unroll
         for (int j = 0; j < kAhead; ++j) {
             const int i = ib + j;
-            if (i < iend) {
-                if (!kSkew || i < i1) {
-                    ring[0][j % 3] = unpack_pairs<NP>(pre[j]);
-                    pre[j] = fetch(min(i + kAhead, i1 - 1));
-                }
+            if (i < i1) {
+                const int m0 = j % 3, m1 = (j + 2) % 3, m2 = (j + 1) % 3;  // slots of rows i, i-1, i-2
+                ring[0][m0] = unpack_pairs<NP>(pre[j]);
+                pre[j] = fetch(min(i + kAhead, i1 - 1));
 #pragma unroll
-                for (int tt = 0; tt < T; ++tt) {
-                    const int t = kSkew ? T - 1 - tt : tt;
-                    const int d = kSkew ? 2 * t : t, r = i - d - 1;  // level t+1 row r from level t rows r-1, r, r+1
-                    const int sn = (j - d + 31) % 3, sc = (j - d + 32) % 3, ss = (j - d + 33) % 3;  // slots of r-1, r, r+1
-                    // level t+1 row r feeds a stored row only if rs - (T - t - 1) <= r < re + (T - t - 1): outside
-                    // that trapezoid nothing is computed (level T: rows [rs, re))
-                    if (i - i0 <= (kSkew ? 3 : 2) * t + 1) continue;
-                    if (kSkew && i >= i1 + t) continue;
+                for (int t = 0; t < T; ++t) {
+                    const int r = i - t - 1;
                     if (t + 1 < T) {
+                        if (i - i0 <= 2 * t + 1) continue;  // outside the wave's trapezoid (see stencil5xT_body)
                         W unused;
-                        level_pairs<false, NP>(ring[t][sn], ring[t][sc], ring[t][ss], k, ring[t + 1 < T ? t + 1 : 0][sc],
-                                               unused);
-                    } else {
+                        level_pairs<false, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k,
+                                               ring[t + 1 < T ? t + 1 : 0][m0], unused);
+                    } else if (r >= rs) {
                         W pk;
                         RowP<NP> unused;
-                        level_pairs<true, NP>(ring[t][sn], ring[t][sc], ring[t][ss], k, unused, pk);
+                        level_pairs<true, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k, unused, pk);
                         buffer_store_row<NP>(pk, ro, vst, (r + halo - sr0) * pitch);
                     }
                 }
@@ -492,7 +479,7 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
 // MINW: minimum waves per SIMD the register allocation must allow (__launch_bounds__'s second argument): a short
 // slab has few waves, so fitting one more per SIMD (T=4: 138 -> <= 128 VGPRs, 3 -> 4 waves) can matter more than
 // the few rematerialised values it costs.
-template <int T, int kAhead, int MINW = 1, int CPL = 8, bool SKEW = false>
+template <int T, int kAhead, int MINW = 1, int CPL = 8>
 __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const unsigned short* __restrict__ u,
                                                                   unsigned short* __restrict__ out, int rows, int cols,
                                                                   int ld, int halo, RowSpans sp, long long grow0,
@@ -509,8 +496,7 @@ __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const un
     const bool store_lane = G::store_lane(lane, cols, in_grid);
     const bool fix0 = c0 == 0, fixl = c0 + CPL == cols;
     const int slab_rows = rows + 2 * halo;
-    // u rows consumed: [i0, i1); level rows computed: [i0 - T, i1 - 1)
-    const int i0 = rs - T, i1 = re + T;
+    const int i0 = rs - T, i1 = re + T;  // u rows consumed: [i0, i1); level rows computed: [i0 - T, i1 - 1)
     // the wave's slab rows [sr0, sr1) (clamped like the fetch); one descriptor per buffer over exactly them
     const int sr0 = min(max(i0 + halo, 0), slab_rows - 1), sr1 = min(max(i1 - 1 + halo, 0), slab_rows - 1) + 1;
     const int pitch = ld * 2;
@@ -526,7 +512,7 @@ __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const un
     if (slow)  // a few waves per grid: the v1 pipeline (per-column selects, per-row Dirichlet test; same results)
         stencil5xT_body<T, kAhead, CPL>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
     else
-        pipeline_v2<T, kAhead, G::NP, SKEW>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
+        pipeline_v2<T, kAhead, G::NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
 }
 #pragma clang fp contract(on)
 }  // namespace
@@ -599,9 +585,8 @@ extern "C" int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int ro
         (((uintptr_t)u | (uintptr_t)out) & 15))
         return -1;
     const int o_cpl = shape & 0xff, o_rpw = (shape >> 8) & 0xff, o_ahead = (shape >> 16) & 0xff;
-    const int o_var = (shape >> 24) & 0xf;  // 0: rule, 1: level-chained pipeline, 2: skewed pipeline (kSkew)
     if ((o_cpl != 0 && o_cpl != 4 && o_cpl != 8) || (o_ahead != 0 && o_ahead != 3 && o_ahead != 6 && o_ahead != 9) ||
-        o_var > 2 || (shape >> 28) != 0)
+        (shape >> 24) != 0)
         return -1;
     const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
     const int lo_lim = top_global ? 0 : -max(0, halo - steps), hi_lim = bot_global ? rows : rows + max(0, halo - steps);
@@ -656,15 +641,10 @@ extern "C" int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int ro
     const int per = kWaves * rpw;
     const RowSpans sp{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per, rpw};
     const dim3 g(strips_for(cols, steps == 2 ? 8 : cpl, steps), sp.nby_a + (r1b - r0b + per - 1) / per);
-    const bool skew = o_var == 2;
 #define PCMX_STENCIL_V2_KA(T, KA, C)                                                                                \
     case KA:                                                                                                        \
-        if (skew)                                                                                                   \
-            stencil5xT2_kernel<T, KA, 1, C, true><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp,       \
-                                                                             global_row0, global_rows, k);          \
-        else                                                                                                        \
-            stencil5xT2_kernel<T, KA, 1, C><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0, \
-                                                                       global_rows, k);                             \
+        stencil5xT2_kernel<T, KA, 1, C><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,    \
+                                                                   global_rows, k);                                 \
         break;
 #define PCMX_STENCIL_V2C(T, C)                                                                                      \
     switch (ahead) {                                                                                                \

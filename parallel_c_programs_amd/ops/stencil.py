@@ -97,13 +97,11 @@ def stencil5_fused_spans_(u: torch.Tensor, out: torch.Tensor, spans, global_row0
     return out
 
 
-def launch_shape(cpl: int = 0, rpw: int = 0, ahead: int = 0, variant: int = 0) -> int:
-    """The `shape` word of an explicit stencil launch shape (each field 0: the production rule's value); variant 1: the
-    level-chained row pipeline, 2: the skewed pipeline (level t+1 lags level t by two rows, so the T level updates of
-    one iteration are independent; csrc/kernels/stencil.hip pipeline_v2 kSkew)."""
-    if cpl not in (0, 4, 8) or not 0 <= rpw <= 255 or ahead not in (0, 3, 6, 9) or variant not in (0, 1, 2):
-        raise ValueError("launch_shape: cpl 0/4/8, rpw 0..255, ahead 0/3/6/9, variant 0/1/2")
-    return cpl | (rpw << 8) | (ahead << 16) | (variant << 24)
+def launch_shape(cpl: int = 0, rpw: int = 0, ahead: int = 0) -> int:
+    """The `shape` word of an explicit stencil launch shape (each field 0: the production rule's value)."""
+    if cpl not in (0, 4, 8) or not 0 <= rpw <= 255 or ahead not in (0, 3, 6, 9):
+        raise ValueError("launch_shape: cpl 0/4/8, rpw 0..255, ahead 0/3/6/9")
+    return cpl | (rpw << 8) | (ahead << 16)
 
 
 def stencil5x2_step_(u, out, global_row0=0, global_rows=None, k=DEFAULT_K, halo=1, row_range=None):
