@@ -73,7 +73,7 @@ def parse(argv=None):
     ap.add_argument("--stencil-fuse", type=int, default=0,
                     help="fused updates per kernel / halo depth (0: by slab height, 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8)")
     ap.add_argument("--stencil-halo-mult", type=int, default=0,
-                    help="deep halo: m x fuse halo rows exchanged every m steps (0: auto, 3 on slabs of <= 3072 rows at N > 1, else 1)")
+                    help="deep halo: m x fuse halo rows exchanged every m steps (0: auto, 4 on slabs of <= 4096 rows at N > 1, else 1)")
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
     ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")
@@ -134,25 +134,52 @@ def launch(args, argv: list[str]) -> int:
     return rc if rc >= 0 else 128 - rc
 
 
-def rocsparse_bar(n_rows: int, nnz: int, reps: int, warmup: int) -> dict:
+def rocsparse_bar(n_rows: int, nnz: int, reps: int, warmup: int, rows: tuple[int, int] | None = None,
+                  device: int | None = None) -> dict:
     """rocSPARSE's generic SpMV (preprocess once; W warm-up calls, then K back-to-back compute calls between two
     events, the mean; max error against an fp64 host product) on the same power-law matrix: bin/spmv_vendor, a
     child process on /opt/rocm's rocSPARSE + HIP runtime (torch's sparse CSR path re-analyses the matrix per call).
-    Runs after our sections, this process idle on the GPU meanwhile."""
+    Runs after our sections, this process idle on the GPU meanwhile. rows=(row0, row1), device: one rank's block
+    of rows (its local product, no exchange) on that rank's GPU; the result then also holds per-algorithm ms."""
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bin", "spmv_vendor")
     if not os.path.exists(exe):
         return {"rocsparse_spmv_gflops": "not built (bin/spmv_vendor)"}
     try:
-        r = subprocess.run([exe, str(n_rows), str(nnz), str(reps), str(warmup)], capture_output=True, text=True,
-                           timeout=240)
+        cmd = [exe, str(n_rows), str(nnz), str(reps), str(warmup)]
+        if rows is not None:
+            cmd += [str(rows[0]), str(rows[1])] + ([str(device)] if device is not None else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         res = json.loads(line)
         algs = {k[:-7]: v for k, v in res.items() if k.endswith("_gflops") and k != "best_gflops"}
         best = max(algs, key=algs.get)
         return {"rocsparse_spmv_gflops": res["best_gflops"], "rocsparse_spmv_alg": best,
-                "rocsparse_spmv_max_rel_err_vs_fp64": res.get(f"{best}_max_rel_err")}
+                "rocsparse_spmv_max_rel_err_vs_fp64": res.get(f"{best}_max_rel_err"),
+                "_ms": {a: res[f"{a}_ms"] for a in algs}, "_nnz": res["nnz"]}
     except Exception as e:  # the line says why the bar is missing
         return {"rocsparse_spmv_gflops": f"failed: {type(e).__name__}: {e}"[:200]}
+
+
+def rocsparse_bar_ranks(ctx, n_rows: int, nnz: int, reps: int, warmup: int, rows: tuple[int, int]) -> dict:
+    """N > 1: every rank runs rocSPARSE on its own block of rows (bin/spmv_vendor with a row range, on its own GPU),
+    all ranks at once after a barrier; per algorithm the job's time is the SLOWEST rank's (as for our step) and the
+    GFLOP/s the whole matrix's 2 nnz over it. Compute only (no exchange): a bar our full step has to beat with its
+    exchange included. Every rank makes the same collectives whether or not its child process succeeded."""
+    ctx.barrier()
+    res = rocsparse_bar(n_rows, nnz, reps, warmup, rows=rows, device=ctx.device.index)
+    names = ("csr_adaptive", "csr_rowsplit")
+    ms = [float(res.get("_ms", {}).get(a, float("inf"))) for a in names]
+    worst = [ctx.max_over_ranks(v) for v in ms]
+    nnz_all = ctx.scalar(float(res.get("_nnz", 0)))
+    ctx.all_reduce_(nnz_all)
+    err = ctx.max_over_ranks(float(res.get("rocsparse_spmv_max_rel_err_vs_fp64") or 0.0))
+    gf = {a: 2.0 * nnz_all.item() / (w * 1e-3) / 1e9 for a, w in zip(names, worst) if w != float("inf")}
+    if not gf:
+        return {"rocsparse_spmv_gflops": res.get("rocsparse_spmv_gflops") if isinstance(
+            res.get("rocsparse_spmv_gflops"), str) else "failed on a rank"}
+    best = max(gf, key=gf.get)
+    return {"rocsparse_spmv_gflops": _r(gf[best], 2), "rocsparse_spmv_alg": best,
+            "rocsparse_spmv_max_rel_err_vs_fp64": err, "rocsparse_spmv_scope": "local products, no exchange"}
 
 
 # ------------------------------------------------------------------------------------------------ sections
@@ -251,11 +278,15 @@ class Runner:
             self.log(f"{name} FAILED: " + (self.out.get(f"{name}_error", "") + " " + " ".join(bad)).strip())
 
 
-def device_times(chk: Checks, prefix: str, ms: list) -> None:
+def device_times(chk: Checks, prefix: str, ms: list, hms: list | None = None) -> None:
+    """Per-step device times (min / median / max over steps, max over ranks) and the longest host enqueue of a step:
+    a device_ms_max outlier with a small host_ms_max is a device-side stall, not the Python host."""
     from parallel_c_programs_amd.utils.harness import step_stats
 
     for k, v in step_stats(ms).items():
         chk.info(f"{prefix}_device_ms_{k}", v, "max")
+    if hms:
+        chk.info(f"{prefix}_host_ms_max", max(hms), "max")
 
 
 def main(argv=None):
@@ -305,12 +336,12 @@ def main(argv=None):
         g = W.Sgemm(ctx, n=n)
         runner.maybe_raise("sgemm", "raise-early")
         yield
-        ms = []
-        t = timed(ctx, g.step, K, Wm, ms)
+        ms, hms = [], []
+        t = timed(ctx, g.step, K, Wm, ms, hms)
         rep = g.report(t, K)
         head["tflops"], head["ms"] = rep["value"], rep["ms_per_step"]
         out["sgemm_tflops_per_gpu"] = _r(rep["value"] / world, 3)
-        device_times(chk, "sgemm", ms)
+        device_times(chk, "sgemm", ms, hms)
         if not args.no_ref and dev.type == "cuda":
             # the vendor library timed exactly like our kernel (same warm-up and step count), into its own buffer:
             # g.c keeps the output of our timed steps for the check
@@ -328,10 +359,10 @@ def main(argv=None):
             gx.__dict__.update(g.__dict__)
             gx.variant, gx.c = 20, torch.empty_like(g.c)
             yield
-            ms6 = []
-            t_x6 = timed(ctx, gx.step, K, Wm, ms6)
+            ms6, hms6 = [], []
+            t_x6 = timed(ctx, gx.step, K, Wm, ms6, hms6)
             out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * gx.work_per_step() * K / t_x6 / 1e12, 3)
-            device_times(chk, "sgemm_fp32_via_bf16x6", ms6)
+            device_times(chk, "sgemm_fp32_via_bf16x6", ms6, hms6)
         if runner.injected("sgemm", "perturb"):
             g.c[n // 3, n // 5] += 1.0
         yield
@@ -357,12 +388,12 @@ def main(argv=None):
                 continue
             w = cls(ctx, n=per_rank)
             yield
-            ms = []
-            t = timed(ctx, w.step, K, Wm, ms)
+            ms, hms = [], []
+            t = timed(ctx, w.step, K, Wm, ms, hms)
             rep = w.report(t, K)
             out[f"{name}_{mode}_gbps"] = _r(rep["value"], 1)
             out[f"{name}_{mode}_ms_per_step"] = _r(rep["ms_per_step"])
-            device_times(chk, f"{name}_{mode}", ms)
+            device_times(chk, f"{name}_{mode}", ms, hms)
             if mode == "weak" and not args.no_ref and dev.type == "cuda":
                 # the vendor library on the same per-GPU data, timed exactly like our kernel (rocPRIM behind both)
                 yield
@@ -401,12 +432,12 @@ def main(argv=None):
         s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse, halo_mult=args.stencil_halo_mult)
         runner.maybe_raise("stencil", "raise-early")
         yield
-        ms = []
-        t = timed(ctx, s.step, K, Wm, ms)
+        ms, hms = [], []
+        t = timed(ctx, s.step, K, Wm, ms, hms)
         rep = s.report(t, K)
         out.update({"stencil_glups": _r(rep["value"], 1), "stencil_ms_per_step": _r(rep["ms_per_step"]),
                     "stencil_updates_per_step": s.slab.fuse, "stencil_halo_mult": s.slab.m})
-        device_times(chk, "stencil", ms)
+        device_times(chk, "stencil", ms, hms)
         if runner.injected("stencil", "perturb"):
             s.slab.interior()[s.slab.rows // 2, 7] += 1.0
         yield
@@ -431,14 +462,14 @@ def main(argv=None):
                     exchange=args.spmv_exchange, keep_plain=vendor)
         runner.maybe_raise("spmv", "raise-early")
         yield
-        ms = []
-        t = timed(ctx, sp.step, K, Wm, ms)
+        ms, hms = [], []
+        t = timed(ctx, sp.step, K, Wm, ms, hms)
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
                     "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks,
                     "spmv_slices": sp.d.slices, "spmv_exchange": sp.d.exchange if ctx.distributed else None,
                     "spmv_colsplit": sp.d.colsplit})
-        device_times(chk, "spmv", ms)
+        device_times(chk, "spmv", ms, hms)
         if vendor:  # hipSPARSE (torch sparse CSR x dense vector) on each rank's own rows, the same matrix and x
             yield
             try:
@@ -462,10 +493,14 @@ def main(argv=None):
         if c["pipeline_selftest"] is not None:  # deferred vs finished-in-step chained steps, bit for bit (N > 1)
             out["spmv_pipeline_selftest_bit_identical"] = c["pipeline_selftest"]
         runner.maybe_raise("spmv")
+        rows = (sp.d.row0, sp.d.row1)
         del sp
         log(f"spmv {out['spmv_gflops']} GFLOP/s")
         if vendor and world == 1:
-            out.update(rocsparse_bar(int(args.spmv_rows), int(args.spmv_nnz), K, Wm))
+            res = rocsparse_bar(int(args.spmv_rows), int(args.spmv_nnz), K, Wm)
+            out.update({k: v for k, v in res.items() if not k.startswith("_")})
+        elif vendor:
+            out.update(rocsparse_bar_ranks(ctx, int(args.spmv_rows), int(args.spmv_nnz), K, Wm, rows))
 
     if "spmv" in sections:
         runner.run("spmv", spmv)

@@ -326,7 +326,35 @@ __device__ __forceinline__ bool sliced_step(const SlicedCtx& k, long long& it, c
     return more;
 }
 
-template <int kMode, int kPL, bool kTS = false>
+// The item loop of one wave over slice s (items [it, i1), stride apart) of ONE matrix, its arrays as __restrict__
+// parameters (after inlining they keep their no-alias scopes).
+template <int kMode, int kPL, bool kTS>
+__device__ __forceinline__ void sliced_wave(const unsigned short* __restrict__ lrow, const int* __restrict__ col,
+                                            const float* __restrict__ val, const float* __restrict__ x, int n_cols,
+                                            float* __restrict__ ypart, float* __restrict__ extra,
+                                            const Item* __restrict__ items, const SliceMeta& meta, int s, long long it,
+                                            long long i1, long long stride, float* yw) {
+    SlicedCtx k;
+    k.i1 = i1;
+    k.stride = stride;
+    const long long base = meta.nz0[s];
+    k.col = col + base, k.val = val + base, k.lrow = lrow + base;
+    k.colbase = meta.colbase[s];
+    k.rx = rsrc(x, (unsigned)n_cols * 4);
+    k.items = items, k.extra = extra, k.yp = ypart + meta.out0[s], k.yw = yw;
+    k.lane = pcmx::lane_id();
+    Item ia = items[it], ib;
+    StreamRegs<kPL> qa, qb;
+    load_item_stream<kPL, (kMode & 8) != 0>(k.col, k.val, k.lrow, ia, qa, k.lane);
+    while (sliced_step<kMode, kPL, kTS>(k, it, ia, qa, ib, qb) && sliced_step<kMode, kPL, kTS>(k, it, ib, qb, ia, qa)) {
+    }
+}
+
+// kPaired: a paired launch (pcmx_spmv_sliced_pair), whose slices may belong to the second matrix (meta.b). The item
+// loop is instantiated once per matrix with that matrix's arrays as its own __restrict__ parameters: selecting the
+// pointers per slice in front of ONE loop cost the 1e8-nnz single-matrix product 8% (0.639 -> 0.691 ms in the round-5
+// A/B of scripts/spmv_step_time.py: ~400 more instructions in the item loop).
+template <int kMode, int kPL, bool kTS = false, bool kPaired = false>
 __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     const unsigned short* __restrict__ lrow, const int* __restrict__ col, const float* __restrict__ val,
     const float* __restrict__ x, int n_cols, float* __restrict__ ypart, float* __restrict__ extra,
@@ -336,26 +364,15 @@ __global__ __launch_bounds__(kWavesPerBlock * kWave) void spmv_sliced_kernel(
     const int b = blockIdx.x;
     const int phase = phase_lo + b / (8 * blocks_per_slice);
     const int s = phase * 8 + (b & 7);
-    SlicedCtx k;
-    k.i1 = meta.item1[s];
-    k.stride = (long long)blocks_per_slice * kWavesPerBlock;
-    long long it = meta.item0[s] + (long long)((b >> 3) % blocks_per_slice) * kWavesPerBlock + w;
-    if (it >= k.i1) return;
-    if (meta.part[s]) {  // (wave-uniform) a slice of the paired matrix
-        col = meta.b.col, val = meta.b.val, lrow = meta.b.lrow, items = meta.b.items;
-        ypart = meta.b.ypart, extra = meta.b.extra;
-    }
-    const long long base = meta.nz0[s];
-    k.col = col + base, k.val = val + base, k.lrow = lrow + base;
-    k.colbase = meta.colbase[s];
-    k.rx = rsrc(x, (unsigned)n_cols * 4);
-    k.items = items, k.extra = extra, k.yp = ypart + meta.out0[s], k.yw = yl[w];
-    k.lane = pcmx::lane_id();
-    Item ia = items[it], ib;
-    StreamRegs<kPL> qa, qb;
-    load_item_stream<kPL, (kMode & 8) != 0>(k.col, k.val, k.lrow, ia, qa, k.lane);
-    while (sliced_step<kMode, kPL, kTS>(k, it, ia, qa, ib, qb) && sliced_step<kMode, kPL, kTS>(k, it, ib, qb, ia, qa)) {
-    }
+    const long long i1 = kPaired ? meta.item1[s] : meta.item0[s + 1];
+    const long long stride = (long long)blocks_per_slice * kWavesPerBlock;
+    const long long it = meta.item0[s] + (long long)((b >> 3) % blocks_per_slice) * kWavesPerBlock + w;
+    if (it >= i1) return;
+    if (kPaired && meta.part[s])  // (wave-uniform) a slice of the paired matrix
+        sliced_wave<kMode, kPL, kTS>(meta.b.lrow, meta.b.col, meta.b.val, x, n_cols, meta.b.ypart, meta.b.extra,
+                                     meta.b.items, meta, s, it, i1, stride, yl[w]);
+    else
+        sliced_wave<kMode, kPL, kTS>(lrow, col, val, x, n_cols, ypart, extra, items, meta, s, it, i1, stride, yl[w]);
 }
 
 // y[r] = sum over the slices touching row r (bit k of mask[r]) of that slice's compact partial, in slice order.
@@ -1082,7 +1099,8 @@ extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, 
     const dim3 blk(kWavesPerBlock * kWave);
     const bool ts = !(mode & kModeNtPartials);
 #define PCMX_PAIR(PL, TS)                                                                                           \
-    spmv_sliced_kernel<12, PL, TS><<<nb, blk, 0, s>>>(nullptr, col_a, val_a, x, n_cols, ypart_a, extra_a, ia, meta, bp, 0)
+    spmv_sliced_kernel<12, PL, TS, true><<<nb, blk, 0, s>>>(nullptr, col_a, val_a, x, n_cols, ypart_a, extra_a, ia, meta, bp, \
+                                                             0)
     if (item_mode == 4)
         ts ? PCMX_PAIR(4, true) : PCMX_PAIR(4, false);
     else if (item_mode == 2)

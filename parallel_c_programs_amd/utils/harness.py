@@ -10,7 +10,10 @@ launch thread, a page fault) or work outside the step (ref 5-cuda-region-growing
 phase on its own)."""
 from __future__ import annotations
 
+import gc
+import os
 import statistics
+import sys
 import time
 
 import torch
@@ -23,36 +26,57 @@ def sync(ctx: Context) -> None:
         torch.cuda.synchronize(ctx.device)
 
 
-def timed(ctx: Context, step_fn, steps: int, warmup: int, per_step: list | None = None) -> float:
+def timed(ctx: Context, step_fn, steps: int, warmup: int, per_step: list | None = None,
+          host_ms: list | None = None) -> float:
     """Seconds for `steps` calls of step_fn (max over ranks). per_step (a list): this rank's time of each timed step
-    in ms is appended — hipEvent device time on a GPU, host wall time on the CPU."""
+    in ms is appended — hipEvent device time on a GPU, host wall time on the CPU. host_ms (a list): the host wall time
+    of each step_fn call (enqueue time on a GPU): a device-time outlier without a host one is the device's (or a
+    peer's), with one the host's. PCMX_TIMED_DIAG=1 also logs every cyclic-GC pass inside the loop to stderr."""
     for _ in range(warmup):
         step_fn()
+    diag = os.environ.get("PCMX_TIMED_DIAG") == "1"
+    gc_log = []
+    if diag:  # diagnostic: every cyclic-GC pass inside the timed loop, with its host time
+        t_gc = [0.0]
+
+        def on_gc(phase, info):
+            if phase == "start":
+                t_gc[0] = time.perf_counter()
+            else:
+                gc_log.append((info.get("generation"), 1e3 * (time.perf_counter() - t_gc[0])))
     cuda = ctx.device.type == "cuda"
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if per_step is not None and cuda else None
-    host = [] if per_step is not None and not cuda else None
     sync(ctx)
     ctx.barrier()
     sync(ctx)
+    if diag:
+        gc.callbacks.append(on_gc)
     t0 = time.perf_counter()
     if evs:
         evs[0].record()
+    walls = []
     for i in range(steps):
-        if host is not None:
-            h0 = time.perf_counter()
+        h0 = time.perf_counter()
         step_fn()
         if evs:
             evs[i + 1].record()
-        if host is not None:
-            host.append(1e3 * (time.perf_counter() - h0))
+        walls.append(1e3 * (time.perf_counter() - h0))
     sync(ctx)
     ctx.barrier()
     sync(ctx)
     elapsed = time.perf_counter() - t0
+    if diag:
+        gc.callbacks.remove(on_gc)
+        worst = max(range(steps), key=walls.__getitem__)
+        print(f"[timed-diag] {getattr(step_fn, '__qualname__', step_fn)}: host ms per step max {walls[worst]:.3f} at "
+              f"step {worst}, median {statistics.median(walls):.3f}; gc passes in the loop {gc_log}", file=sys.stderr,
+              flush=True)
     if evs:
         per_step.extend(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
-    elif host is not None:
-        per_step.extend(host)
+    elif per_step is not None:
+        per_step.extend(walls)
+    if host_ms is not None:
+        host_ms.extend(walls)
     return ctx.max_over_ranks(elapsed)
 
 
