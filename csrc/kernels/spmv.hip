@@ -471,14 +471,22 @@ __device__ __forceinline__ float combine_scan_row(const float* __restrict__ comp
         v[k] = 0.f;
         if ((own[k / 4] >> (8 * (k % 4))) & 0xffu) v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, boff, off[k], 0));
     }
+    // the sum starts from an OPAQUE +0 (same value, same bits): from a literal 0 the compiler folds 0 + v[0] into the
+    // first predicated load's branch and waits for that load there, a serial round trip per wave (round 5, with the
+    // SGPR cap below: 93 -> 77 us per 1e8-nnz fused combine, profiles/r5_spmv/n1_step_regression_ab.txt)
     float acc = 0.f;
+    asm volatile("" : "+v"(acc));
 #pragma unroll
     for (int k = 0; k < S; ++k) acc += v[k];
     return acc;
 }
 
+// amdgpu_num_sgpr(76): the combine is latency-bound, so residency is its speed. 256-thread blocks are admitted per CU
+// up to floor(800 / (ceil(sgpr / 16) * 16 + 16)): <= 80 SGPRs 8 blocks, 81-96 only 7. Left alone the compiler gives
+// these kernels 90 SGPRs at S = 24 (106 at 32) without needing them (capped: 74, no spills).
+#define PCMX_COMBINE_SGPRS __attribute__((amdgpu_num_sgpr(76)))
 template <int S>
-__global__ __launch_bounds__(256) void spmv_combine_scan_kernel(const float* __restrict__ comp,
+__global__ __launch_bounds__(256) PCMX_COMBINE_SGPRS void spmv_combine_scan_kernel(const float* __restrict__ comp,
                                                                 const unsigned* __restrict__ mask,
                                                                 const int* __restrict__ base, SliceOut so,
                                                                 float* __restrict__ y, int n_rows) {
@@ -500,7 +508,7 @@ __global__ __launch_bounds__(256) void spmv_combine_scan_kernel(const float* __r
 //    reference it (built once at set-up from the same send lists the gather used): the wave writes its rows' values
 //    straight into the send buffer, so no gather pass re-reads y after the combine (send_ptr == nullptr: no pack).
 template <int S>
-__global__ __launch_bounds__(256) void spmv_combine_fused_kernel(const float* __restrict__ comp,
+__global__ __launch_bounds__(256) PCMX_COMBINE_SGPRS void spmv_combine_fused_kernel(const float* __restrict__ comp,
                                                                  const unsigned* __restrict__ mask,
                                                                  const int* __restrict__ base, SliceOut so,
                                                                  float* __restrict__ y, int n_rows,
@@ -515,10 +523,16 @@ __global__ __launch_bounds__(256) void spmv_combine_fused_kernel(const float* __
     const int lane = pcmx::lane_id();
     const int r = c * kWave + lane;
     if (c * kWave >= n_rows) return;
+    // the chunk's fix range [fix_chunk0[c], fix_chunk0[c + 1]) (lanes 0 / 1) and the row's send range as VECTOR loads
+    // issued next to the mask load, so one wait covers them all (loaded after the combine, each was one more dependent
+    // round trip per wave)
+    const int fv = fix_chunk0 ? __builtin_nontemporal_load(fix_chunk0 + c + (lane & 1)) : 0;
+    int p0 = 0, p1 = 0;
+    if (send_ptr && r < n_rows) p0 = send_ptr[r], p1 = send_ptr[r + 1];
     float acc = combine_scan_row<S>(comp, mask, base, so, n_rows, c, lane, r);
     if (fix_chunk0) {
-        const int f1 = fix_chunk0[c + 1];
-        for (int k = fix_chunk0[c]; k < f1;) {  // wave-uniform: one run (one row) per iteration
+        const int f1 = __builtin_amdgcn_readlane(fv, 1);
+        for (int k = __builtin_amdgcn_readlane(fv, 0); k < f1;) {  // wave-uniform: one run (one row) per iteration
             const int row = __builtin_amdgcn_readfirstlane(fix[k].y);
             float part = 0.f;
             int len = 0;
@@ -537,10 +551,7 @@ __global__ __launch_bounds__(256) void spmv_combine_fused_kernel(const float* __
     }
     if (r < n_rows) {
         y[r] = acc;
-        if (send_ptr) {
-            const int p1 = send_ptr[r + 1];
-            for (int p = send_ptr[r]; p < p1; ++p) sendbuf[send_slot[p]] = acc;
-        }
+        for (int p = p0; p < p1; ++p) sendbuf[send_slot[p]] = acc;
     }
 }
 

@@ -171,6 +171,10 @@ class DistributedSpMV:
             part = m.row_block(a, b)
             if self.sliced:
                 part = SlicedCSR(part, slices, head, balance, item_nnz, col_split=self.col_split)
+                # one rank: the in-library combine + fix-up (two launches, 69 + 5 us on the 1e8-nnz matrix) beats the
+                # fused combine (77 us: its waves holding split rows sum their runs serially); distributed steps fuse
+                # (fewer launches on 1/N of the rows, and the send-buffer pack rides along): profiles/r5_spmv/
+                part.fused_combine = ctx.distributed
             elif self.colsplit:
                 part = ColSplitCSR(part, self.col_split)
             elif dev.type == "cuda":
