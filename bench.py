@@ -8,7 +8,9 @@ touches the GPU, and exits with its status (the reference's `mpirun -n P region 
 2-mpi-region-growing/Makefile:4); N larger than the visible GPU count is refused, and so is a launcher whose
 WORLD_SIZE differs from --gpus. Sections, each with its own correctness check, all timed the same way (W untimed
 warm-up steps, then EXACTLY K timed steps bracketed by barrier + torch.cuda.synchronize() on both sides, max over
-ranks; utils/harness.py), each also reporting its per-step hipEvent device time (min / median / max):
+ranks; utils/harness.py; on a GPU each section's W warm-ups follow --settle-ms (30) of untimed steps, so the timed
+steps run at the steady-state shader clock), each also reporting its per-step hipEvent device time (min / median /
+max) and its longest host enqueue:
 
   sgemm    (value) 8192^3 fp32 C = A @ B per GPU on the MFMA kernel, weak scaling; EVERY element of C checked
            against an fp64 GEMM; the hipBLASLt torch.matmul of the same operands is timed alongside for reference,
@@ -19,18 +21,19 @@ ranks; utils/harness.py), each also reporting its per-step hipEvent device time 
   scan     global inclusive prefix sum over the rank-ordered concatenation (reduce-then-scan): weak and
            strong like reduce; fp64 check of EVERY output of every rank incl. its rank offset, and the stream's
            look-back error word
-  stencil  16384^2 bf16 5-point stencil, strong scaling: row slabs, T fused updates per kernel (T by slab
-           height: 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8) and one T-row halo exchange per neighbour overlapped with
-           the interior update; bit-exact checks: the timed grid itself (all warm-up + timed updates) against a
+  stencil  16384^2 bf16 5-point stencil (random grid), strong scaling: row slabs, T fused updates per kernel (T by
+           slab height: 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8), a deep halo at N = 4 / 8 (4T rows exchanged every 4th
+           step, overlapped with the interior update; self-tested on the job's backend first); bit-exact checks: the timed grid itself (all warm-up + timed updates) against a
            plain-PyTorch single-step oracle, and a small grid through the same distributed path
   spmv     power-law CSR, 1e8 nnz / 1e7 rows, strong scaling: nnz-balanced row blocks, XCD-sliced kernel,
            ghost exchange (only the x entries each rank's nonzeros reference, grouped per-peer send/recv) chunked
            and overlapped with the product; fp64 check of every rank's rows and ghosts
   (N > 1)  256 MiB RCCL all-reduce bus bandwidth
   vendor   every section carries the vendor library on the same data: hipBLASLt (torch.matmul), rocPRIM
-           (torch.sum, torch.cumsum), hipSPARSE (torch sparse CSR x vector) timed like our kernels, and, at N = 1,
-           rocSPARSE's generic SpMV with its analysis done once (bin/spmv_vendor, a child process: W warm-ups, then
-           K back-to-back calls between two events, the mean; fp64 reference)
+           (torch.sum, torch.cumsum), hipSPARSE (torch sparse CSR x vector) timed like our kernels, and rocSPARSE's
+           generic SpMV with its analysis done once (bin/spmv_vendor, a child process per rank: W warm-ups, then K
+           back-to-back calls between two events, the mean; fp64 reference; at N > 1 each rank's local product, no
+           exchange, the slowest rank's time)
 
 Checks are ENFORCED: fp64-referenced errors must be <= 1e-5 (workloads.REL_ERR_LIMIT), bit-exact flags true. A
 failing check adds "<section>_check_failed" (the failing keys) to the line; a section that raises adds
@@ -67,6 +70,9 @@ def parse(argv=None):
                          "starts torch.distributed.run itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle-ms", type=float, default=30.0,
+                    help="GPU: untimed steps for this much wall time before each section's W warm-up steps, so the "
+                         "timed steps run at the steady-state clock (0: off)")
     ap.add_argument("--size", type=int, default=8192, help="SGEMM M=N=K")
     ap.add_argument("--reduce-n", type=float, default=1e9, help="f32 elements (per GPU weak, in total strong)")
     ap.add_argument("--stencil-n", type=int, default=16384)
@@ -319,6 +325,7 @@ def main(argv=None):
             raise SystemExit(f"[bench] {world} RCCL ranks but {torch.cuda.device_count()} GPU(s) visible")
     sections = [s for s in args.sections.split(",") if s]
     K, Wm = args.steps, args.warmup
+    SETTLE = args.settle_ms
     LIM = W.REL_ERR_LIMIT
     out = {}
 
@@ -337,7 +344,7 @@ def main(argv=None):
         runner.maybe_raise("sgemm", "raise-early")
         yield
         ms, hms = [], []
-        t = timed(ctx, g.step, K, Wm, ms, hms)
+        t = timed(ctx, g.step, K, Wm, ms, hms, settle_ms=SETTLE)
         rep = g.report(t, K)
         head["tflops"], head["ms"] = rep["value"], rep["ms_per_step"]
         out["sgemm_tflops_per_gpu"] = _r(rep["value"] / world, 3)
@@ -347,7 +354,7 @@ def main(argv=None):
             # g.c keeps the output of our timed steps for the check
             cref = torch.empty_like(g.c)
             yield
-            t_ref = timed(ctx, lambda: torch.matmul(g.a, g.b, out=cref), K, Wm)
+            t_ref = timed(ctx, lambda: torch.matmul(g.a, g.b, out=cref), K, Wm, settle_ms=SETTLE)
             out["hipblaslt_torch_matmul_tflops"] = _r(world * g.work_per_step() * K / t_ref / 1e12, 3)
             del cref
         x6 = not args.no_x6 and dev.type == "cuda" and n % 256 == 0
@@ -360,7 +367,7 @@ def main(argv=None):
             gx.variant, gx.c = 20, torch.empty_like(g.c)
             yield
             ms6, hms6 = [], []
-            t_x6 = timed(ctx, gx.step, K, Wm, ms6, hms6)
+            t_x6 = timed(ctx, gx.step, K, Wm, ms6, hms6, settle_ms=SETTLE)
             out["sgemm_fp32_via_bf16x6_tflops"] = _r(world * gx.work_per_step() * K / t_x6 / 1e12, 3)
             device_times(chk, "sgemm_fp32_via_bf16x6", ms6, hms6)
         if runner.injected("sgemm", "perturb"):
@@ -389,7 +396,7 @@ def main(argv=None):
             w = cls(ctx, n=per_rank)
             yield
             ms, hms = [], []
-            t = timed(ctx, w.step, K, Wm, ms, hms)
+            t = timed(ctx, w.step, K, Wm, ms, hms, settle_ms=SETTLE)
             rep = w.report(t, K)
             out[f"{name}_{mode}_gbps"] = _r(rep["value"], 1)
             out[f"{name}_{mode}_ms_per_step"] = _r(rep["ms_per_step"])
@@ -398,11 +405,11 @@ def main(argv=None):
                 # the vendor library on the same per-GPU data, timed exactly like our kernel (rocPRIM behind both)
                 yield
                 if name == "reduce":
-                    t_ref = timed(ctx, lambda: torch.sum(w.x), K, Wm)
+                    t_ref = timed(ctx, lambda: torch.sum(w.x), K, Wm, settle_ms=SETTLE)
                     out["torch_sum_gbps"] = _r(world * 4.0 * w.x.numel() * K / t_ref / 1e9, 1)
                 else:
                     ybuf = torch.empty_like(w.x)
-                    t_ref = timed(ctx, lambda: torch.cumsum(w.x, 0, out=ybuf), K, Wm)
+                    t_ref = timed(ctx, lambda: torch.cumsum(w.x, 0, out=ybuf), K, Wm, settle_ms=SETTLE)
                     out["torch_cumsum_gbps"] = _r(world * 8.0 * w.x.numel() * K / t_ref / 1e9, 1)
                     del ybuf
             if runner.injected(name, "perturb") and mode == "weak":
@@ -433,7 +440,7 @@ def main(argv=None):
         runner.maybe_raise("stencil", "raise-early")
         yield
         ms, hms = [], []
-        t = timed(ctx, s.step, K, Wm, ms, hms)
+        t = timed(ctx, s.step, K, Wm, ms, hms, settle_ms=SETTLE)
         rep = s.report(t, K)
         out.update({"stencil_glups": _r(rep["value"], 1), "stencil_ms_per_step": _r(rep["ms_per_step"]),
                     "stencil_updates_per_step": s.slab.fuse, "stencil_halo_mult": s.slab.m})
@@ -463,7 +470,7 @@ def main(argv=None):
         runner.maybe_raise("spmv", "raise-early")
         yield
         ms, hms = [], []
-        t = timed(ctx, sp.step, K, Wm, ms, hms)
+        t = timed(ctx, sp.step, K, Wm, ms, hms, settle_ms=SETTLE)
         rep = sp.report(t, K)
         out.update({"spmv_gflops": _r(rep["value"], 2), "spmv_ms_per_step": _r(rep["ms_per_step"]),
                     "spmv_effective_gbps": _r(rep["effective_gbps"], 1), "spmv_chunks": sp.d.chunks,
@@ -475,7 +482,7 @@ def main(argv=None):
             try:
                 A = sp.d.vendor_matrix()
                 yv = torch.mv(A, sp.xp)
-                t_ref = timed(ctx, lambda: torch.mv(A, sp.xp), K, Wm)
+                t_ref = timed(ctx, lambda: torch.mv(A, sp.xp), K, Wm, settle_ms=SETTLE)
                 nnz_all = ctx.scalar(float(sp.d.local_nnz))
                 ctx.all_reduce_(nnz_all)
                 out["torch_sparse_csr_gflops"] = _r(2.0 * nnz_all.item() * K / t_ref / 1e9, 2)
@@ -533,7 +540,7 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{world}",
             },
-            device=dev.type, **out)
+            device=dev.type, settle_ms_before_warmup=SETTLE if dev.type == "cuda" else 0, **out)
         try:
             line = bench_line(partial="sgemm" not in sections or "sgemm" in runner.failed, **fields)
         except ValueError as e:  # still print what was measured (with the reason), then fail the run after finalize

@@ -638,7 +638,8 @@ void spmv_sliced_combine(const at::Tensor& ypart, const at::Tensor& row_mask, co
         TORCH_CHECK(send_ptr->is_contiguous() && send_ptr->numel() >= n_rows + 1 && send_slot->is_contiguous() &&
                         sendbuf->is_contiguous() && send_slot->numel() <= sendbuf->numel(),
                     "spmv_sliced_combine: send lists");
-        sp = send_ptr->data_ptr<int>(), ss = send_slot->data_ptr<int>(), sb = sendbuf->data_ptr<float>();
+        if (send_slot->numel() > 0)  // (no peer references any row, e.g. one rank: nothing to pack)
+            sp = send_ptr->data_ptr<int>(), ss = send_slot->data_ptr<int>(), sb = sendbuf->data_ptr<float>();
     }
     const at::DeviceGuard g(ypart.device());
     check_rc(pcmx_spmv_sliced_combine(ypart.data_ptr<float>(), reinterpret_cast<const unsigned*>(row_mask.data_ptr<int>()),

@@ -27,11 +27,26 @@ def sync(ctx: Context) -> None:
 
 
 def timed(ctx: Context, step_fn, steps: int, warmup: int, per_step: list | None = None,
-          host_ms: list | None = None) -> float:
+          host_ms: list | None = None, settle_ms: float = 0.0) -> float:
     """Seconds for `steps` calls of step_fn (max over ranks). per_step (a list): this rank's time of each timed step
     in ms is appended — hipEvent device time on a GPU, host wall time on the CPU. host_ms (a list): the host wall time
     of each step_fn call (enqueue time on a GPU): a device-time outlier without a host one is the device's (or a
-    peer's), with one the host's. PCMX_TIMED_DIAG=1 also logs every cyclic-GC pass inside the loop to stderr."""
+    peer's), with one the host's. PCMX_TIMED_DIAG=1 also logs every cyclic-GC pass inside the loop to stderr.
+    settle_ms > 0 (GPU): before the W warm-up steps, untimed steps until that much wall time has passed, so the timed
+    steps run at the clock a running job sees: a VALU-bound kernel measured right after an idle set-up runs up to 12%
+    slow while the shader clock ramps (profiles/r5_bench/README.md: 2.14 -> 2.26 GHz over the first 25 stencil
+    launches, 2.33-2.42 in steady state)."""
+    if settle_ms > 0 and ctx.device.type == "cuda":
+        # the step count is agreed over the ranks (steps may hold collectives): 4 probe steps price one step, the
+        # slowest rank's price sets the count
+        sync(ctx)
+        t0 = time.perf_counter()
+        for _ in range(4):
+            step_fn()
+        sync(ctx)
+        per = ctx.max_over_ranks((time.perf_counter() - t0) / 4)
+        for _ in range(min(10_000, int(settle_ms / 1e3 / max(per, 1e-6)))):
+            step_fn()
     for _ in range(warmup):
         step_fn()
     diag = os.environ.get("PCMX_TIMED_DIAG") == "1"
