@@ -22,7 +22,7 @@ max) and its longest host enqueue:
            strong like reduce; fp64 check of EVERY output of every rank incl. its rank offset, and the stream's
            look-back error word
   stencil  16384^2 bf16 5-point stencil (random grid), strong scaling: row slabs, T fused updates per kernel (T by
-           slab height: 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8), a deep halo at N = 4 / 8 (4T rows exchanged every 4th
+           slab height: 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8), a deep halo at N = 4 / 8 (5T rows exchanged every 5th
            step, overlapped with the interior update; self-tested on the job's backend first); bit-exact checks: the timed grid itself (all warm-up + timed updates) against a
            plain-PyTorch single-step oracle, and a small grid through the same distributed path
   spmv     power-law CSR, 1e8 nnz / 1e7 rows, strong scaling: nnz-balanced row blocks, XCD-sliced kernel,
@@ -79,7 +79,7 @@ def parse(argv=None):
     ap.add_argument("--stencil-fuse", type=int, default=0,
                     help="fused updates per kernel / halo depth (0: by slab height, 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8)")
     ap.add_argument("--stencil-halo-mult", type=int, default=0,
-                    help="deep halo: m x fuse halo rows exchanged every m steps (0: auto, 4 on slabs of <= 4096 rows at N > 1, else 1)")
+                    help="deep halo: m x fuse halo rows exchanged every m steps (0: auto, 5 on slabs of <= 4096 rows at N > 1, else 1)")
     ap.add_argument("--spmv-rows", type=float, default=1e7)
     ap.add_argument("--spmv-nnz", type=float, default=1e8)
     ap.add_argument("--spmv-chunks", type=int, default=0, help="exchange pipeline depth (0: 1 at N=1, else 2)")

@@ -538,30 +538,6 @@ int strips_for(int cols, int cpl, int steps) {
     const int L = (steps + cpl - 1) / cpl, out = (64 - 2 * L) * cpl;
     return cols <= 64 * cpl ? 1 : 1 + (cols - 64 * cpl + out - 1) / out;
 }
-// Rows per wave for a short slab at T = 6 (4-column lanes): the smallest count >= 18 whose grid fits ONE residency
-// round of the chip (every workgroup resident at once), so no second, partly filled round of waves follows. One N = 8
-// rank's 2048-row slab: 29 rows per wave (1242 workgroups <= 256 CUs x 5) 0.0526 ms against 0.0567 with 18 (1.56
-// rounds); at T = 8 and on tall grids the round count measured no effect (scripts/stencil_rpw_lab.py,
-// profiles/r4_stencil/rpw_sweep.txt).
-int one_round_rpw(int span_a, int span_b, int cols, int steps) {
-    static const int slots = [] {
-        int dev = 0, cus = 256, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, stencil5xT2_kernel<6, 6, 1, 4>, kWaves * 64, 0) !=
-                hipSuccess ||
-            per <= 0)
-            per = 5;
-        return cus * per;
-    }();
-    const int strips = strips_for(cols, 4, steps);
-    for (int r = 18; r <= 48; ++r) {
-        const int per = kWaves * r;
-        if ((long long)strips * ((span_a + per - 1) / per + (span_b + per - 1) / per) <= slots) return r;
-    }
-    return 18;
-}
 // the halo rule of one row range: a row r reads rows r - steps .. r + steps, which must lie in the slab on a side
 // with a neighbour (at a GLOBAL edge the clamped reads only feed Dirichlet rows)
 bool halo_ok(int rows, int halo, int steps, int r0, int r1, long long global_row0, long long global_rows) {
@@ -619,12 +595,17 @@ extern "C" int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int ro
     // lane (twice the waves, half the registers) pays at T >= 6 below 12288 rows; an EDGE launch (the two halo
     // bands of a distributed step, <= 2T rows) is a few waves whose row pipeline is the whole cost, so it runs
     // 2-row waves of 4 columns per lane (shorter dependency chains, 8-16x the waves).
+    // Short slabs at T = 6 (one N = 8 rank, 2048 rows): 18 rows per wave with the 3-row ring. Round 4 sized the grid to
+    // one residency round (29 rows per wave: 0.0526 against 0.0567 ms for a full launch, rpw_sweep.txt); round 5's
+    // interleaved A/B (profiles/r5_stencil/rpw_deep_ab.txt, 6 alternations in one process) finds the full launch equal
+    // at 18 / 24 / 29 (0.0531 / 0.0532 / 0.0533 ms) and the deep-halo steps the production schedule runs faster at 18
+    // (m = 5: 0.0539 / 0.0547 / 0.0558 ms per step).
     const bool edge = span_rows <= 64;
     int cpl, rpw;
     if (edge)
         cpl = 4, rpw = 2;
     else if (span_rows < 3072)
-        cpl = steps >= 6 ? 4 : 8, rpw = steps == 6 ? one_round_rpw(r1a - r0a, r1b - r0b, cols, steps) : 24;
+        cpl = steps >= 6 ? 4 : 8, rpw = steps == 6 ? 18 : 24;
     else if (span_rows < 6144)
         cpl = steps >= 6 ? 4 : 8, rpw = steps == 8 ? 32 : 24;
     else if (span_rows < 12288)

@@ -39,16 +39,18 @@ def auto_fuse(slab_rows: int) -> int:
 
 
 def auto_halo_mult(slab_rows: int, fuse: int, world: int) -> int:
-    """Halo depth in units of `fuse` rows (the deep-halo schedule, see StencilSlab): 4 on distributed slabs of up to
+    """Halo depth in units of `fuse` rows (the deep-halo schedule, see StencilSlab): 5 on distributed slabs of up to
     4096 rows, 1 otherwise. Measured per step of one interior rank (scripts/stencil_rank_lab.py, T = 6): round 4
     (profiles/r4_stencil/rank_lab_deep_halo.txt, rank_lab_deep3.txt): 2048 rows (N = 8) interior + edge launch every
     step 0.0595-0.0603 ms, m = 2 0.0550-0.0624, m = 3 0.0581; 8192 rows 0.163 -> 0.175 with m = 2 (taller slabs lose:
     their two-launch step hides the edge launch better than the extended launches cost). Round 5, m swept 3..8 in one
     process (profiles/r5_stencil/halo_depth_sweep.txt and the A/B files beside it): 2048 rows m = 3 0.0569-0.0581,
-    m = 4 0.0552-0.0559, m = 5 0.0549, m = 6 0.0569, m = 8 0.0563; 4096 rows (N = 4) edge launch every step 0.0966,
-    m = 3 0.0955, m = 4 0.0902, m = 5 0.0893, m = 8 0.0893. m = 4 rather than 5: within 1%, a smaller halo to
-    exchange, and step counts that are multiples of 4 keep every timed window on whole periods."""
-    return 4 if world > 1 and fuse > 1 and 8 * fuse <= slab_rows <= 4096 else 1
+    m = 4 0.0552-0.0559, m = 5 0.0549, m = 6 0.0569, m = 8 0.0563; with 18 rows per wave (rpw_deep_ab.txt, 6
+    alternations) m = 4 0.0547, m = 5 0.0539; 4096 rows (N = 4) edge launch every step 0.0966, m = 3 0.0955, m = 4
+    0.0902, m = 5 0.0893, m = 8 0.0893 (another box, rpw_n4_ab.txt: m = 4 0.0957, m = 5 0.0928). A timed window of a
+    multiple of 5 steps (the bench's 10 / 20) holds whole periods whatever step it starts at. At 8192 rows (N = 2, T = 8)
+    depth does not matter (halo_depth_n2_n8_n1.txt)."""
+    return 5 if world > 1 and fuse > 1 and 10 * fuse <= slab_rows <= 4096 else 1
 
 
 class StencilSlab:

@@ -3,7 +3,9 @@ and per row chunk either the round-4 combine, fix-up and gather pack (three laun
 (combine + fix-up + send-buffer pack in one launch), interleaved A/B rounds in one process, bit-identity checked; and
 the host enqueue time of the production step against its device time. The two exchange calls a real step adds cost
 ~13-19 us of host time each (scripts/host_overhead_lab.py, profiles/r2_bench/host_overhead_lab.txt).
-Run: python scripts/spmv_host_lab.py [world] [reps]"""
+Run: python scripts/spmv_host_lab.py [world] [reps]
+Env: SPMV_LAB_KINDS=paired (comma list of the A/B kinds; "none": no packs), SPMV_LAB_ITEM, SPMV_LAB_SLICES,
+SPMV_LAB_N1=0 (skip the same-box N = 1 step)."""
 import os
 import sys
 import time
@@ -91,8 +93,9 @@ def main():
         step(kind)
         same = torch.equal(out, ref_out) and all(torch.equal(send_csr[c][2], ref_bufs[c]) for c in range(len(bufs)))
         print(f"{kind}: bit-identical to the round-4 combine, fix-up, gather: {same}", flush=True)
+    kinds = os.environ.get("SPMV_LAB_KINDS", "r4,fused_fixup,fused_pack,paired,none").split(",")
     for rnd in range(3):  # interleaved rounds
-        for kind in ("r4", "fused_fixup", "fused_pack", "paired", ""):
+        for kind in [k if k != "none" else "" for k in kinds]:
             t = dev_ms(lambda: step(kind))
             print(f"round {rnd} N={W} step {kind or 'no packs (r4 combine)'}: device {t:.4f} ms/step", flush=True)
     torch.cuda.synchronize()

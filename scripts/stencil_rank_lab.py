@@ -14,7 +14,8 @@ full-grid time this bounds the strong-scaling efficiency of the compute part (do
 Run: python scripts/stencil_rank_lab.py [fuse ...]
 Env: STENCIL_LAB_WORLDS=8 (subset of 1,2,4,8), STENCIL_LAB_RPW=0,18 (rows per wave forced on the non-edge launches
 as an explicit launch shape of each call, ops.stencil.launch_shape; 0 = production rule; one line per value, all in one
-process for an A/B); STENCIL_LAB_DEEP=2,3,4 (halo depths m).
+process for an A/B); STENCIL_LAB_DEEP=2,3,4 (halo depths m); STENCIL_LAB_ONLY=full (subset of full, split3, split2, split2c); STENCIL_LAB_AHEAD=3 / 6 / 9 (prefetch ring
+of the forced shapes).
 """
 import os
 import sys
@@ -48,7 +49,7 @@ def main():
     worlds = [int(w) for w in os.environ.get("STENCIL_LAB_WORLDS", "1,2,4,8").split(",")]
     rpws = [int(r) for r in os.environ.get("STENCIL_LAB_RPW", "0").split(",")]
     for T, world, rpw in [(T, w, r) for T in fuses for w in worlds for r in rpws]:
-        shape = launch_shape(0, rpw)
+        shape = launch_shape(0, rpw, int(os.environ.get("STENCIL_LAB_AHEAD", "0")))
 
         def step(*a, shape=shape, **kw):  # the non-edge launches take the forced rows per wave
             return ops.stencil5_fused_step_(*a, shape=shape, **kw)
@@ -108,6 +109,9 @@ def main():
             full()
             res = {}
             variants = [("full", full), ("split3", split3), ("split2", split2), ("split2c", split2c)]
+            only = os.environ.get("STENCIL_LAB_ONLY")  # e.g. "full,split2": a subset of the single-step shapes
+            if only:
+                variants = [v for v in variants if v[0] in only.split(",")]
             for name, fn in variants + [(k, v[1]) for k, v in deeps.items()]:
                 out.zero_()
                 fn()

@@ -660,16 +660,16 @@ def test_run_workload_failed_check_exits_1(monkeypatch):
 
 
 def test_auto_halo_mult_rule():
-    """Deep halo m = 4 on distributed slabs of up to 4096 rows (the N = 8 and N = 4 ranks of the 16384-row bench
+    """Deep halo m = 5 on distributed slabs of up to 4096 rows (the N = 8 and N = 4 ranks of the 16384-row bench
     grid), else 1."""
     from parallel_c_programs_amd.parallel.stencil import auto_halo_mult
 
-    assert auto_halo_mult(2048, 6, 8) == 4 and auto_halo_mult(2048, 8, 8) == 4
-    assert auto_halo_mult(3072, 6, 4) == 4 and auto_halo_mult(4096, 6, 4) == 4
+    assert auto_halo_mult(2048, 6, 8) == 5 and auto_halo_mult(2048, 8, 8) == 5
+    assert auto_halo_mult(3072, 6, 4) == 5 and auto_halo_mult(4096, 6, 4) == 5
     assert auto_halo_mult(6144, 8, 3) == 1 and auto_halo_mult(8192, 8, 2) == 1  # taller slabs: m = 1
     assert auto_halo_mult(2048, 6, 1) == 1  # one rank: no exchange to amortise
     assert auto_halo_mult(2048, 1, 8) == 1  # single-step launches
-    assert auto_halo_mult(40, 6, 8) == 1  # slab shorter than 8 fused levels
+    assert auto_halo_mult(50, 6, 8) == 1  # slab shorter than 10 fused levels (two 5T halos)
 
 
 def test_gather_host_path_matches_index():
