@@ -180,9 +180,8 @@ def rocsparse_bar_ranks(ctx, n_rows: int, nnz: int, reps: int, warmup: int, rows
     ctx.all_reduce_(nnz_all)
     err = ctx.max_over_ranks(float(res.get("rocsparse_spmv_max_rel_err_vs_fp64") or 0.0))
     gf = {a: 2.0 * nnz_all.item() / (w * 1e-3) / 1e9 for a, w in zip(names, worst) if w != float("inf")}
-    if not gf:
-        return {"rocsparse_spmv_gflops": res.get("rocsparse_spmv_gflops") if isinstance(
-            res.get("rocsparse_spmv_gflops"), str) else "failed on a rank"}
+    if not gf:  # (the same answer on every rank)
+        return {"rocsparse_spmv_gflops": "failed on a rank (bin/spmv_vendor child process)"}
     best = max(gf, key=gf.get)
     return {"rocsparse_spmv_gflops": _r(gf[best], 2), "rocsparse_spmv_alg": best,
             "rocsparse_spmv_max_rel_err_vs_fp64": err, "rocsparse_spmv_scope": "local products, no exchange"}

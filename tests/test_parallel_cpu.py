@@ -680,3 +680,46 @@ def test_gather_host_path_matches_index():
     out = torch.empty(257)
     ops.gather_(src, idx, out)
     assert torch.equal(out, src[idx.long()])
+
+
+def _rocsparse_ranks(ctx, q, fail_rank):
+    """bench.rocsparse_bar_ranks with the child process replaced: rank r 'measures' (r + 1) ms for csr_adaptive and
+    2 (r + 1) ms for csr_rowsplit on (r + 1) * 1e6 nonzeros; `fail_rank`'s child fails."""
+    import bench
+
+    def fake(n_rows, nnz, reps, warmup, rows=None, device=None):
+        r = ctx.rank
+        if r == fail_rank:
+            return {"rocsparse_spmv_gflops": "failed: RuntimeError: boom"}
+        return {"rocsparse_spmv_gflops": 1.0, "rocsparse_spmv_max_rel_err_vs_fp64": 1e-7 * (r + 1),
+                "_ms": {"csr_adaptive": float(r + 1), "csr_rowsplit": 2.0 * (r + 1)}, "_nnz": (r + 1) * 1_000_000}
+
+    bench.rocsparse_bar = fake
+    q.put((ctx.rank, bench.rocsparse_bar_ranks(ctx, 100, 100, 1, 0, (0, 1))))
+
+
+def test_rocsparse_bar_ranks_takes_the_slowest_rank():
+    """N > 1 vendor bar: per algorithm the slowest rank's time, over the whole matrix's nonzeros (sum over ranks), the
+    best algorithm; every rank makes the same collectives, also when one rank's child process failed."""
+    res = _collect(2, _rocsparse_ranks, -1)
+    # nnz 3e6 over the slower rank's 2 ms (adaptive) / 4 ms (rowsplit): 3 / 1.5 GFLOP/s
+    assert res[0] == res[1]
+    assert res[0]["rocsparse_spmv_alg"] == "csr_adaptive" and abs(res[0]["rocsparse_spmv_gflops"] - 3.0) < 1e-9
+    assert abs(res[0]["rocsparse_spmv_max_rel_err_vs_fp64"] - 2e-7) < 1e-15
+    res = _collect(2, _rocsparse_ranks, 1)  # rank 1 failed: its time counts as infinite -> no bar
+    assert res[0] == res[1] and isinstance(res[0]["rocsparse_spmv_gflops"], str)
+
+
+def _timed_host(ctx, q):
+    from parallel_c_programs_amd.utils.harness import timed
+
+    calls, ms, hms = [], [], []
+    timed(ctx, lambda: calls.append(1), 5, 2, ms, hms, settle_ms=50.0)
+    q.put((ctx.rank, (len(calls), len(ms), len(hms))))
+
+
+def test_timed_collects_host_times_and_settles_only_on_gpu():
+    """timed(): W + K calls on the CPU (the settle phase is for the GPU clock only), per-step times and host enqueue
+    times for every timed step."""
+    res = _collect(2, _timed_host)
+    assert res[0] == res[1] == (7, 5, 5)
