@@ -170,7 +170,11 @@ def rocsparse_bar_ranks(ctx, n_rows: int, nnz: int, reps: int, warmup: int, rows
     """N > 1: every rank runs rocSPARSE on its own block of rows (bin/spmv_vendor with a row range, on its own GPU),
     all ranks at once after a barrier; per algorithm the job's time is the SLOWEST rank's (as for our step) and the
     GFLOP/s the whole matrix's 2 nnz over it. Compute only (no exchange): a bar our full step has to beat with its
-    exchange included. Every rank makes the same collectives whether or not its child process succeeded."""
+    exchange included. Every rank makes the same collectives whether or not its child process succeeded. Ranks that
+    share a GPU (gloo rehearsals) skip it: a child per rank would double the processes on that GPU."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world))
+    if local > torch.cuda.device_count():  # (the same answer on every rank of the node)
+        return {"rocsparse_spmv_gflops": "not measured: ranks share a GPU"}
     ctx.barrier()
     res = rocsparse_bar(n_rows, nnz, reps, warmup, rows=rows, device=ctx.device.index)
     names = ("csr_adaptive", "csr_rowsplit")

@@ -695,6 +695,7 @@ def _rocsparse_ranks(ctx, q, fail_rank):
                 "_ms": {"csr_adaptive": float(r + 1), "csr_rowsplit": 2.0 * (r + 1)}, "_nnz": (r + 1) * 1_000_000}
 
     bench.rocsparse_bar = fake
+    bench.torch.cuda.device_count = lambda: ctx.world if fail_rank != -2 else 1  # one GPU per rank (-2: shared)
     q.put((ctx.rank, bench.rocsparse_bar_ranks(ctx, 100, 100, 1, 0, (0, 1))))
 
 
@@ -708,6 +709,8 @@ def test_rocsparse_bar_ranks_takes_the_slowest_rank():
     assert abs(res[0]["rocsparse_spmv_max_rel_err_vs_fp64"] - 2e-7) < 1e-15
     res = _collect(2, _rocsparse_ranks, 1)  # rank 1 failed: its time counts as infinite -> no bar
     assert res[0] == res[1] and isinstance(res[0]["rocsparse_spmv_gflops"], str)
+    res = _collect(2, _rocsparse_ranks, -2)  # two ranks on one GPU: no child processes at all
+    assert res[0] == res[1] == {"rocsparse_spmv_gflops": "not measured: ranks share a GPU"}
 
 
 def _timed_host(ctx, q):
