@@ -105,10 +105,11 @@ def _sliced_product_phase(self: SlicedCSR, x: torch.Tensor, phase: int, key=0, d
     """Column-split product of a SlicedCSR: phase 0 = the products of the slices below the split (partials only),
     phase 1 = the products of the others, then the combine + fix-up (+ the send-buffer pack, `send`) into dst."""
     half = self.n_slices // 16
+    blocks = self.phase_blocks[phase] << 8  # resident product blocks per CU of this phase's launch (0: the default)
     if phase == 0:
-        self.spmv(x, mode=16, phases=(0, half))
+        self.spmv(x, mode=16 | blocks, phases=(0, half))
     else:
-        self.spmv(x, mode=16, phases=(half, half))
+        self.spmv(x, mode=16 | blocks, phases=(half, half))
         self.spmv(x, dst, mode=32, send=send)
 
 
@@ -404,7 +405,7 @@ class DistributedSpMV:
             # both row chunks' chunk-0-column products in ONE launch (a launch of a few items per wave pays its ramp
             # and tail once: scripts/spmv_host_lab.py, profiles/r5_spmv/)
             h0, h1 = p0.n_slices // 16, p1.n_slices // 16
-            p0.products_pair(p1, xp, (0, h0), (0, h1))
+            p0.products_pair(p1, xp, (0, h0), (0, h1), mode=p0.phase_blocks[0] << 8)
         else:
             for c, (a, b, part) in enumerate(self.parts):
                 if b > a:

@@ -5,6 +5,7 @@ the host enqueue time of the production step against its device time. The two ex
 ~13-19 us of host time each (scripts/host_overhead_lab.py, profiles/r2_bench/host_overhead_lab.txt).
 Run: python scripts/spmv_host_lab.py [world] [reps]
 Env: SPMV_LAB_KINDS=paired (comma list of the A/B kinds; "none": no packs), SPMV_LAB_ITEM, SPMV_LAB_SLICES,
+SPMV_LAB_PB=2,4 (resident product blocks per CU of the phase-0 / phase-1 launches),
 SPMV_LAB_N1=0 (skip the same-box N = 1 step)."""
 import os
 import sys
@@ -51,6 +52,12 @@ def main():
         ptr[1:] = torch.bincount(lr, minlength=b - a).cumsum(0)
         send_csr.append((ptr.to(torch.int32), order.to(torch.int32), torch.empty_like(bufs[c])))
 
+    if os.environ.get("SPMV_LAB_PB"):  # resident blocks per CU of the phase-0 / phase-1 product launches (0: 3)
+        pb = tuple(int(v) for v in os.environ["SPMV_LAB_PB"].split(","))
+        for _, _, part in d.parts:
+            part.phase_blocks = pb
+        print(f"phase_blocks {pb}", flush=True)
+
     def step(kind="paired"):
         """kind r4: combine, fix-up and the gather pack as three launches per chunk (round 4); fused_fixup: combine +
         fix-up in one launch, then the gather; fused_pack: combine + fix-up + pack in ONE launch; paired (production):
@@ -59,7 +66,7 @@ def main():
             part.fused_combine = kind != "r4"
         if kind == "paired":
             (_, _, p0), (_, _, p1) = d.parts
-            p0.products_pair(p1, xp, (0, p0.n_slices // 16), (0, p1.n_slices // 16))
+            p0.products_pair(p1, xp, (0, p0.n_slices // 16), (0, p1.n_slices // 16), mode=p0.phase_blocks[0] << 8)
         else:
             for c, (a, b, part) in enumerate(d.parts):
                 if b > a:
