@@ -174,11 +174,9 @@ class SlicedCSR:
         self.fix_chunk0 = torch.searchsorted(self.fix[:, 1].contiguous().long(),
                                              torch.arange(0, n_ch + 2, device=dev) * 64).to(torch.int32).contiguous()
         self.fused_combine = True  # combine + fix-up (+ pack) in one launch (False: the in-library two-launch form)
-        # resident product blocks per CU of the column-split phase 0 / phase 1 launches (0: the library default, 3).
-        # Phase 0 runs as ONE paired launch of two matrices (two slices per XCD): 1 block per slice and CU there, i.e.
-        # 2 per CU — one N = 8 rank's step 0.1181-0.1190 -> 0.1157-0.1158 ms; phase 1 indifferent
-        # (profiles/r5_spmv/phase_blocks_sweep.txt)
-        self.phase_blocks = (1, 0)
+        # resident product blocks per CU of the column-split phase 0 / phase 1 launches (0: the library default, 3;
+        # DistributedSpMV sets them by rank size)
+        self.phase_blocks = (0, 0)
         self.row_mask = mask.to(torch.int32).contiguous()  # bit 31 wraps into the sign: read as u32 on device
         self.chunk_base = base.contiguous()
         self.meta = torch.cat([nz0, torch.tensor(item0, dtype=torch.int64), torch.tensor(out0, dtype=torch.int64)])

@@ -176,6 +176,10 @@ class DistributedSpMV:
                 # fused combine (77 us: its waves holding split rows sum their runs serially); distributed steps fuse
                 # (fewer launches on 1/N of the rows, and the send-buffer pack rides along): profiles/r5_spmv/
                 part.fused_combine = ctx.distributed
+                # the paired phase-0 launch (two matrices, two slices per XCD) of a small rank: 1 resident block per
+                # slice and CU instead of 3 — N = 8 0.1182 -> 0.1161 ms per step, N = 4 0.2026 -> 0.2005, N = 2 0.3932 ->
+                # 0.3951 (kept at 3 there); phase 1 indifferent (profiles/r5_spmv/phase_blocks_sweep.txt)
+                part.phase_blocks = (1, 0) if W >= 4 else (0, 0)
             elif self.colsplit:
                 part = ColSplitCSR(part, self.col_split)
             elif dev.type == "cuda":
