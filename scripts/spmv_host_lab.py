@@ -58,12 +58,28 @@ def main():
             part.phase_blocks = pb
         print(f"phase_blocks {pb}", flush=True)
 
+    side = torch.cuda.Stream(dev)
+
     def step(kind="paired"):
         """kind r4: combine, fix-up and the gather pack as three launches per chunk (round 4); fused_fixup: combine +
         fix-up in one launch, then the gather; fused_pack: combine + fix-up + pack in ONE launch; paired (production):
         fused_pack with both chunks' chunk-0-column products in ONE launch"""
         for c, (a, b, part) in enumerate(d.parts):
             part.fused_combine = kind != "r4"
+        if kind == "paired_side":  # paired, with row chunk 0's combine + pack on a side stream beside chunk 1's products
+            (_, _, p0), (_, _, p1) = d.parts
+            half = p0.n_slices // 16
+            p0.products_pair(p1, xp, (0, half), (0, p1.n_slices // 16), mode=p0.phase_blocks[0] << 8)
+            main = torch.cuda.current_stream(dev)
+            p0.spmv(xp, mode=16 | (p0.phase_blocks[1] << 8), phases=(half, half))
+            side.wait_stream(main)
+            s0, (a0, b0, _) = d.seg[0 * Wd + r], d.parts[0]
+            with torch.cuda.stream(side):
+                p0.spmv(xp, out[s0:s0 + (b0 - a0)], mode=32, send=send_csr[0])
+            s1, (a1, b1, _) = d.seg[1 * Wd + r], d.parts[1]
+            p1.product_phase(xp, 1, 1, out[s1:s1 + (b1 - a1)], send=send_csr[1])
+            main.wait_stream(side)
+            return
         if kind == "paired":
             (_, _, p0), (_, _, p1) = d.parts
             p0.products_pair(p1, xp, (0, p0.n_slices // 16), (0, p1.n_slices // 16), mode=p0.phase_blocks[0] << 8)
@@ -95,7 +111,7 @@ def main():
     # bit-identity of the three forms (out rows and send buffers)
     step("r4")
     ref_out, ref_bufs = out.clone(), [bb.clone() for bb in bufs]
-    for kind in ("fused_pack", "paired"):
+    for kind in ("fused_pack", "paired", "paired_side"):
         out.zero_()
         step(kind)
         same = torch.equal(out, ref_out) and all(torch.equal(send_csr[c][2], ref_bufs[c]) for c in range(len(bufs)))
