@@ -301,6 +301,10 @@ def device_times(chk: Checks, prefix: str, ms: list, hms: list | None = None) ->
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
+    if os.environ.get("PCMX_STACK_DUMP_S"):  # diagnostic: every rank prints its Python stacks every N seconds
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["PCMX_STACK_DUMP_S"]), repeat=True, file=sys.stderr)
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None:
         args.gpus = args.gpus or 1

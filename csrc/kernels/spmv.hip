@@ -970,6 +970,8 @@ constexpr int kModeNtPartials = 1 << 26;
 // mode bit 27: items of 256 nonzeros (4 per lane; packed layout only) — the short launches of a distributed rank's
 // column-split step give each wave only a few items, so shorter items spread the same work over more of them
 constexpr int kMode256 = 1 << 27;
+// mode bit 28: items of 384 nonzeros (6 per lane; packed layout only), between the 256 and 512 of a distributed rank
+constexpr int kMode384 = 1 << 28;
 
 extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, const float* val, const float* x,
                                 float* ypart, float* extra, float* y, int n_rows, int n_cols, int n_slices,
@@ -1021,6 +1023,8 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
             const bool ts = !(mode & kModeNtPartials);
             if (mode & kMode256)
                 (ts ? PCMX_SLICED_TS(12, 4) : PCMX_SLICED(12, 4));
+            else if (mode & kMode384)
+                (ts ? PCMX_SLICED_TS(12, 6) : PCMX_SLICED(12, 6));
             else if ((mode & 7) == 2)
                 (ts ? PCMX_SLICED_TS(12, 8) : PCMX_SLICED(12, 8));
             else if ((mode & 7) == 0)
@@ -1028,8 +1032,8 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
             else
                 return (int)hipErrorInvalidValue;  // the lab modes read the unpacked layout
 #undef PCMX_SLICED_TS
-        } else if (mode & kMode256) {
-            return (int)hipErrorInvalidValue;  // 256-nonzero items: packed layout only
+        } else if (mode & (kMode256 | kMode384)) {
+            return (int)hipErrorInvalidValue;  // 256 / 384-nonzero items: packed layout only
         } else switch (mode & 7) {
             case 0: PCMX_SLICED(4, 16); break;
             case 1: PCMX_SLICED(5, 16); break;
@@ -1068,7 +1072,7 @@ extern "C" int pcmx_spmv_sliced(const unsigned short* lrow, const int* col, cons
 // Round 5: the products (no combine) of phases [a_lo, a_lo + a_n) of sliced matrix A and [b_lo, b_lo + b_n) of sliced
 // matrix B — two matrices over the SAME x, e.g. the two row chunks of a distributed column-split step multiplying their
 // chunk-0 columns — in ONE launch: a launch of a few items per wave pays its ramp and tail once instead of twice.
-// Production layout only (packed index stream, temporal partial stores unless mode bit 26); item_mode 2 / 4: 512 / 256-nnz
+// Production layout only (packed index stream, temporal partial stores unless mode bit 26); item_mode 2 / 4 / 6: 512 / 256 / 384-nnz
 // items (0: 1024).
 // meta_*: host arrays nz0 (S), item0 (S + 1), out0 (S + 1), colbase (S) of each matrix.
 extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, int mode, const int* col_a,
@@ -1079,7 +1083,8 @@ extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, 
                                      const long long* nz0_b, const long long* item0_b, const long long* out0_b,
                                      const int* colbase_b, int b_lo, int b_n, hipStream_t s) {
     if (s_a % 8 || s_b % 8 || a_lo < 0 || b_lo < 0 || a_n < 0 || b_n < 0 || 8 * (a_lo + a_n) > s_a ||
-        8 * (b_lo + b_n) > s_b || 8 * (a_n + b_n) > kMaxSlices || (item_mode != 0 && item_mode != 2 && item_mode != 4))
+        8 * (b_lo + b_n) > s_b || 8 * (a_n + b_n) > kMaxSlices ||
+        (item_mode != 0 && item_mode != 2 && item_mode != 4 && item_mode != 6))
         return (int)hipErrorInvalidValue;
     if (a_n + b_n == 0) return 0;
     SliceMeta meta{};
@@ -1114,6 +1119,8 @@ extern "C" int pcmx_spmv_sliced_pair(const float* x, int n_cols, int item_mode, 
                                                              0)
     if (item_mode == 4)
         ts ? PCMX_PAIR(4, true) : PCMX_PAIR(4, false);
+    else if (item_mode == 6)
+        ts ? PCMX_PAIR(6, true) : PCMX_PAIR(6, false);
     else if (item_mode == 2)
         ts ? PCMX_PAIR(8, true) : PCMX_PAIR(8, false);
     else

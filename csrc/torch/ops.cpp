@@ -519,7 +519,7 @@ at::Tensor spmv_sliced(const at::Tensor& lrow, const at::Tensor& col, const at::
         }
         TORCH_CHECK((mode & 7) == 0 || (mode & 7) == 2, "spmv_sliced: the packed layout runs the production modes only");
     } else {
-        TORCH_CHECK(!(mode & (1 << 27)), "spmv_sliced: 256-nonzero items need the packed layout");
+        TORCH_CHECK(!(mode & ((1 << 27) | (1 << 28))), "spmv_sliced: 256 / 384-nonzero items need the packed layout");
     }
     TORCH_CHECK(row_mask.numel() >= n_rows && chunk_base.numel() >= ((n_rows + 63) / 64) * S,
                 "spmv_sliced: row_mask / chunk_base shape");

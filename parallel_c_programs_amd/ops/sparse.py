@@ -76,11 +76,11 @@ class SlicedCSR:
 
         if n_slices % 8 or not 8 <= n_slices <= 32:
             raise ValueError("n_slices must be 8, 16, 24 or 32")
-        if item_nnz not in (256, 512, 1024):
-            raise ValueError("item_nnz must be 256, 512 or 1024 (4, 8 or 16 nonzeros per lane)")
+        if item_nnz not in (256, 384, 512, 1024):
+            raise ValueError("item_nnz must be 256, 384, 512 or 1024 (4, 6, 8 or 16 nonzeros per lane)")
         self.item_nnz = item_nnz
-        # kernel layout bits: items of 512 nonzeros (bit 1) or of 256 (bit 27, packed layout only)
-        self.mode = 2 if item_nnz == 512 else (1 << 27) if item_nnz == 256 else 0
+        # kernel layout bits: items of 512 nonzeros (bit 1), of 256 (bit 27) or 384 (bit 28; both packed layout only)
+        self.mode = {512: 2, 256: 1 << 27, 384: 1 << 28}.get(item_nnz, 0)
         dev = m.val.device
         n, S, nnz = m.n_rows, n_slices, m.nnz
         self.n_rows, self.n_cols, self.n_slices, self.nnz = n, m.n_cols, S, nnz
@@ -184,8 +184,8 @@ class SlicedCSR:
         self.ypart = torch.empty(max(1, out0[-1]), dtype=torch.float32, device=dev)
         self.extra = torch.empty(max(1, item0[-1]), dtype=torch.float32, device=dev)
         self._pack(slice_nnz, pack)
-        if item_nnz == 256 and self.cr is None:
-            raise ValueError("item_nnz 256 needs the packed index stream (every slice < 2^21 columns)")
+        if item_nnz in (256, 384) and self.cr is None:
+            raise ValueError(f"item_nnz {item_nnz} needs the packed index stream (every slice < 2^21 columns)")
 
     def _pack(self, slice_nnz: torch.Tensor, pack: bool) -> None:
         """Packed index stream (the kernel's production layout): one int32 per nonzero = column - first tail column
@@ -223,7 +223,7 @@ class SlicedCSR:
                 m._no_lrow = torch.empty(0, dtype=torch.int16, device=m.cr.device)
         if self.mode != other.mode:
             raise ValueError("products_pair: both matrices need the same item size")
-        item_mode = 4 if self.mode & (1 << 27) else self.mode
+        item_mode = 4 if self.mode & (1 << 27) else 6 if self.mode & (1 << 28) else self.mode
         ops().spmv_sliced_pair(x, item_mode, int(mode), self.cr, self.val, self.items, self._meta_packed, self.ypart,
                                self.extra, self.n_slices, int(phases[0]), int(phases[1]), other.cr, other.val,
                                other.items, other._meta_packed, other.ypart, other.extra, other.n_slices,

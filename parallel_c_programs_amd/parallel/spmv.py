@@ -133,7 +133,13 @@ class DistributedSpMV:
         # so 2 chunks balance the exposed last-chunk exchange against the launch overhead; 512-nnz items give the
         # smaller per-rank matrices more waves (2 chunks: 0.134 -> 0.127 ms)
         C = chunks if chunks else (1 if W == 1 else 2)
-        item_nnz = item_nnz or (1024 if W == 1 else 512)
+        # round 5: a rank of <= 16M nonzeros (N = 8 on the 1e8 matrix) takes 384-nnz items (6 per lane): its short
+        # phase launches give each wave only ~2 items, and 384 fills the tail better than 512 (step 0.1163-0.1168 ->
+        # 0.1149 ms with 2 resident blocks per slice in the paired launch; N = 4 indifferent, 256: slower;
+        # profiles/r5_spmv/items_384_ab.txt)
+        auto_items = not item_nnz
+        local_nnz = int(local.row_ptr[-1] - local.row_ptr[0])
+        item_nnz = item_nnz or (1024 if W == 1 else 384 if local_nnz <= 16_000_000 else 512)
         C = max(1, min(int(C), self.block))
         self.chunks = C
         self.L = -(-self.block // C)
@@ -171,15 +177,23 @@ class DistributedSpMV:
             a, b = min(c * self.L, self.rows), min((c + 1) * self.L, self.rows)
             part = m.row_block(a, b)
             if self.sliced:
-                part = SlicedCSR(part, slices, head, balance, item_nnz, col_split=self.col_split)
+                try:
+                    sc = SlicedCSR(part, slices, head, balance, item_nnz, col_split=self.col_split)
+                except ValueError:  # 384-nnz items need the packed index stream: an automatic choice falls back to 512
+                    if not (auto_items and item_nnz == 384):
+                        raise
+                    item_nnz = 512
+                    sc = SlicedCSR(part, slices, head, balance, item_nnz, col_split=self.col_split)
+                part = sc
                 # one rank: the in-library combine + fix-up (two launches, 69 + 5 us on the 1e8-nnz matrix) beats the
                 # fused combine (77 us: its waves holding split rows sum their runs serially); distributed steps fuse
                 # (fewer launches on 1/N of the rows, and the send-buffer pack rides along): profiles/r5_spmv/
                 part.fused_combine = ctx.distributed
                 # the paired phase-0 launch (two matrices, two slices per XCD) of a small rank: 1 resident block per
                 # slice and CU instead of 3 — N = 8 0.1182 -> 0.1161 ms per step, N = 4 0.2026 -> 0.2005, N = 2 0.3932 ->
-                # 0.3951 (kept at 3 there); phase 1 indifferent (profiles/r5_spmv/phase_blocks_sweep.txt)
-                part.phase_blocks = (1, 0) if W >= 4 else (0, 0)
+                # 0.3951 (kept at 3 there); with 384-nnz items 2 (0.1149 against 0.1153-0.1156 at 1); phase 1
+                # indifferent (profiles/r5_spmv/phase_blocks_sweep.txt, items_384_ab.txt)
+                part.phase_blocks = (2, 0) if item_nnz == 384 else (1, 0) if W >= 4 else (0, 0)
             elif self.colsplit:
                 part = ColSplitCSR(part, self.col_split)
             elif dev.type == "cuda":

@@ -4,7 +4,7 @@ and per row chunk either the round-4 combine, fix-up and gather pack (three laun
 the host enqueue time of the production step against its device time. The two exchange calls a real step adds cost
 ~13-19 us of host time each (scripts/host_overhead_lab.py, profiles/r2_bench/host_overhead_lab.txt).
 Run: python scripts/spmv_host_lab.py [world] [reps]
-Env: SPMV_LAB_KINDS=paired (comma list of the A/B kinds; "none": no packs), SPMV_LAB_ITEM, SPMV_LAB_SLICES,
+Env: SPMV_LAB_KINDS=paired (comma list of the A/B kinds; "none": no packs), SPMV_LAB_ITEM (0: the production rule), SPMV_LAB_SLICES,
 SPMV_LAB_PB=2,4 (resident product blocks per CU of the phase-0 / phase-1 launches),
 SPMV_LAB_N1=0 (skip the same-box N = 1 step)."""
 import os
@@ -22,11 +22,11 @@ def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     dev = torch.device("cuda", 0)
-    item = int(os.environ.get("SPMV_LAB_ITEM", "512"))
+    item = int(os.environ.get("SPMV_LAB_ITEM", "0"))  # 0: the production rule
     slices = int(os.environ.get("SPMV_LAB_SLICES", "16"))
     d = DistributedSpMV.powerlaw(Context(rank=0, world=W, device=dev), 10_000_000, 100_000_000, slices=slices, chunks=2,
                                  item_nnz=item, colsplit=True)
-    print(f"item_nnz {item}, slices {slices}", flush=True)
+    print(f"item_nnz {d.parts[0][2].item_nnz}, slices {slices}, phase_blocks {d.parts[0][2].phase_blocks}", flush=True)
     xp = torch.rand(d.n_pad, device=dev)
     out = torch.zeros_like(xp)
     Wd, r = d.ctx.world, d.ctx.rank

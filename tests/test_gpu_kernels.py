@@ -396,7 +396,7 @@ def test_spmv_banded_vs_host(gpu):
     assert (out_csr - ref).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("slices,item", [(16, 512), (24, 1024)])
+@pytest.mark.parametrize("slices,item", [(16, 512), (24, 1024), (16, 384), (16, 256)])
 def test_spmv_fused_combine_bit_identical(gpu, slices, item):
     """The round-5 fused combine (combine + split-row fix-up + send-buffer pack in ONE launch) against the two-launch
     combine + fix-up and a gather of the same send lists: same y bits, same send-buffer bits, on a power-law matrix
@@ -479,6 +479,13 @@ def test_spmv_sliced_powerlaw_vs_fp64(gpu, slices, head):
     # byte-packed-scan combine (production) vs the ballot-rank combine (mode bit 6): same partials, same order
     assert torch.equal(out, s.spmv(x.to(gpu), mode=64).cpu().double())
     assert torch.equal(out, unpacked.spmv(x.to(gpu), mode=64).cpu().double())
+    # the short items of distributed ranks (384 / 256 nonzeros, 6 / 4 per lane; packed layout only): fp64 bound,
+    # reproducible
+    for item in (384, 256):
+        si = ops.SlicedCSR(m.to(gpu), slices, head=head, item_nnz=item)
+        oi = si.spmv(x.to(gpu)).cpu().double()
+        assert torch.equal(oi, si.spmv(x.to(gpu)).cpu().double())
+        assert ((oi - want).abs() / (absrow + 1e-3)).max().item() < 1e-5, item
 
 
 @pytest.mark.parametrize("item_nnz", [512, 1024])
