@@ -15,7 +15,7 @@ Run: python scripts/stencil_rank_lab.py [fuse ...]
 Env: STENCIL_LAB_WORLDS=8 (subset of 1,2,4,8), STENCIL_LAB_RPW=0,18 (rows per wave forced on the non-edge launches
 as an explicit launch shape of each call, ops.stencil.launch_shape; 0 = production rule; one line per value, all in one
 process for an A/B); STENCIL_LAB_DEEP=2,3,4 (halo depths m); STENCIL_LAB_ONLY=full (subset of full, split3, split2, split2c); STENCIL_LAB_AHEAD=3 / 6 / 9 (prefetch ring
-of the forced shapes).
+of the forced shapes); STENCIL_LAB_CPL=4 / 8 (columns per lane of the forced shapes).
 """
 import os
 import sys
@@ -49,7 +49,7 @@ def main():
     worlds = [int(w) for w in os.environ.get("STENCIL_LAB_WORLDS", "1,2,4,8").split(",")]
     rpws = [int(r) for r in os.environ.get("STENCIL_LAB_RPW", "0").split(",")]
     for T, world, rpw in [(T, w, r) for T in fuses for w in worlds for r in rpws]:
-        shape = launch_shape(0, rpw, int(os.environ.get("STENCIL_LAB_AHEAD", "0")))
+        shape = launch_shape(int(os.environ.get("STENCIL_LAB_CPL", "0")), rpw, int(os.environ.get("STENCIL_LAB_AHEAD", "0")))
 
         def step(*a, shape=shape, **kw):  # the non-edge launches take the forced rows per wave
             return ops.stencil5_fused_step_(*a, shape=shape, **kw)
