@@ -254,8 +254,8 @@ __device__ __forceinline__ typename RawT<NP>::type update_pairs(const RowP<NP>& 
 // Row spans of one launch: blocks [0, nby_a) of grid.y cover local rows [a0, a1), the rest [b0, b1) (empty when
 // b0 == b1). A distributed step updates both rank-edge row bands in ONE launch after the halo arrives, and a
 // launch covers only its rows (no grid over the whole slab with idle blocks).
-// rpw: rows per wave, a launch parameter (not a template argument): the host picks it per launch so that the grid
-// fills whole residency rounds of the chip (see pick_rpw).
+// rpw: rows per wave, a launch parameter (not a template argument): the host picks it per launch by the launched row
+// count and fusion depth (the rule in pcmx_stencil5xT_bf16_spans_shape), or an explicit launch shape overrides it.
 struct RowSpans {
     int a0, a1, b0, b1, nby_a, rpw;
 };
