@@ -47,6 +47,7 @@ int pcmx_sgemm_host_arrays(const float* a, const float* b, float* c, int m, int 
 int pcmx_vmul_f32(const float* a, const float* b, float* r, long long n, hipStream_t s);
 int pcmx_vadd_f32(const float* a, const float* b, float* r, long long n, hipStream_t s);
 int pcmx_axpy_f32(float alpha, const float* x, float* y, long long n, hipStream_t s);
+int pcmx_copy_f32(const float* a, float* r, long long n, hipStream_t s);
 // dst[i] = src[idx[i]] (32-bit indices; an index outside [0, n_src) reads 0); idx, dst 16-B aligned
 int pcmx_gather_f32(const float* src, long long n_src, const int* idx, float* dst, long long n, hipStream_t s);
 int pcmx_fill_f32(float* x, float v, long long n, hipStream_t s);

@@ -1,23 +1,144 @@
 // Element-wise streaming kernels (HBM-bound): vmul (ref 6-opencl-region-growing/multiply_opencl.cl:1-4),
-// vadd/axpy (north-star vector-add), fill and on-device uniform random generation.
+// vadd/axpy (north-star vector-add), copy, fill and on-device uniform random generation.
 //
-// MI355X design: 16-B (f32x4) accesses per lane so one wave instruction moves 1 KiB, 4 independent
-// f32x4 per lane per iteration to keep enough bytes in flight, non-temporal hints on streamed-once
-// data, grid capped at 256 CUs x 64 blocks with a grid-stride loop (cdna_hip_programming.md G11/G13; the write side
-// of an HBM stream tops out near 5.5 TB/s on MI355X: vadd 1e9 2.18 ms = 5.5 TB/s, fill 5.6, against 7.1 for a
-// read-only stream, profiles/r4_bench/stream_bw_lab.txt).
+// MI355X design (round 6, scripts/stream_bw_lab.hip, profiles/r6_stream/): TICKET-ORDERED TILES. A persistent grid of
+// one 512-thread block per CU takes 128-KiB tiles (per input) from an atomic ticket, double-buffered: the next tile's
+// loads are issued before the current tile's stores (the streaming structure of scan_parked_kernel, scan.hip). Tiles
+// then enter HBM in time order, so the whole chip streams one compact window of the arrays. Interleaved on one box
+// (1e9 f32, nt loads and stores): copy 5.36-5.44 TB/s grid-stride -> 6.31-6.35 ticket; vadd 5.35-5.48 -> 6.44-6.51;
+// axpy in place 5.27-5.37 -> 6.44-6.50. The same tiles handed out statically (tile = block + k * grid) stream at
+// 5.06-5.13, so the ORDER is what pays, not the tile shape. The grid-stride form is box-dependent (5.4-6.6 TB/s on
+// three boxes) where the ticket form held 6.31-6.38 on all three. (Round 4's "the write side tops out near 5.5 TB/s"
+// was the grid-stride order on that box, not HBM.)
+// The counter pair lives per (device, stream) and RESETS ITSELF: the last block to finish zeroes it, and stream order
+// makes the next launch on that stream see zeros (no memset launch per call). During a hipGraph capture (no counter
+// can be allocated, and a replay on another stream would share it) the launch takes the grid-stride form instead.
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "pcmx_common.h"
 #include "pcmx_hip.h"
 
 namespace {
 using pcmx::kWave;
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;  // grid-stride fallback and the small kernels
 constexpr int kUnroll = 4;
+constexpr int kTileWaves = 8;  // ticket kernels: 512 threads, one block per CU
 
 using pcmx::f32x4;
 using pcmx::ld_nt;
 using pcmx::st_nt;
 
+struct Ticket {
+    unsigned next;  // next tile to hand out
+    unsigned done;  // blocks finished
+};
+
+// R f32x4 rows per lane and input: tile = 8 waves x 64 lanes x R float4s (R = 16: 128 KiB; two inputs take R = 8).
+template <int R, int NIN>
+struct Regs {
+    f32x4 a[NIN >= 1 ? R : 1], b[NIN == 2 ? R : 1];
+};
+
+template <int R>
+__device__ __forceinline__ long long tile_base(long long t) {
+    return t * (kTileWaves * kWave * R) + (long long)(threadIdx.x / kWave) * (kWave * R) + (threadIdx.x & (kWave - 1));
+}
+
+template <int R, int NIN>
+__device__ __forceinline__ void tile_load(const f32x4* a, const f32x4* b, long long n4, long long t, Regs<R, NIN>& v) {
+    const long long base = tile_base<R>(t);
+    const bool full = (t + 1) * (kTileWaves * kWave * R) <= n4;  // block-uniform
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const long long i = base + r * kWave;
+        if constexpr (NIN >= 1) v.a[r] = (full || i < n4) ? ld_nt(a + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NIN == 2) v.b[r] = (full || i < n4) ? ld_nt(b + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+template <int R, int NIN, class F>
+__device__ __forceinline__ void tile_store(f32x4* out, long long n4, long long t, const Regs<R, NIN>& v, F f) {
+    const long long base = tile_base<R>(t);
+    const bool full = (t + 1) * (kTileWaves * kWave * R) <= n4;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const long long i = base + r * kWave;
+        if (!(full || i < n4)) continue;
+        f32x4 o;
+        if constexpr (NIN == 2) {
+            o.x = f(v.a[r].x, v.b[r].x), o.y = f(v.a[r].y, v.b[r].y), o.z = f(v.a[r].z, v.b[r].z), o.w = f(v.a[r].w, v.b[r].w);
+        } else if constexpr (NIN == 1) {
+            o.x = f(v.a[r].x, 0.f), o.y = f(v.a[r].y, 0.f), o.z = f(v.a[r].z, 0.f), o.w = f(v.a[r].w, 0.f);
+        } else {
+            const float c = f(0.f, 0.f);
+            o = f32x4{c, c, c, c};
+        }
+        st_nt(out + i, o);
+    }
+}
+
+// r[i] = f(a[i], b[i]) (NIN = 2), f(a[i], 0) (NIN = 1) or f(0, 0) (NIN = 0) over n floats; a / b / r 16-B aligned, r may
+// alias an input element for element (axpy). Every block reaches the self-reset at the end (block-uniform exits).
+template <int R, int NIN, class F>
+__device__ __forceinline__ void stream_tiles(const float* a, const float* b, float* r, long long n, Ticket* tk, F f) {
+    __shared__ unsigned s_t[2];
+    const f32x4* a4 = reinterpret_cast<const f32x4*>(a);
+    const f32x4* b4 = reinterpret_cast<const f32x4*>(b);
+    f32x4* r4 = reinterpret_cast<f32x4*>(r);
+    const long long n4 = n >> 2, tile4 = kTileWaves * kWave * R, ntiles = (n4 + tile4 - 1) / tile4;
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {  // the scalar tail (n % 4 floats)
+        const long long t = (n4 << 2) + threadIdx.x;
+        r[t] = f(NIN >= 1 ? a[t] : 0.f, NIN == 2 ? b[t] : 0.f);
+    }
+    auto take = [&](int slot) -> long long {
+        if (threadIdx.x == 0) s_t[slot] = atomicAdd(&tk->next, 1u);
+        __syncthreads();
+        return (long long)s_t[slot];
+    };
+    Regs<R, NIN> va, vb;
+    long long ta = take(0);
+    if (ta < ntiles) {
+        tile_load<R, NIN>(a4, b4, n4, ta, va);
+        // unrolled by two so both register buffers are statically named; the next tile's loads go out before the
+        // current tile's stores (vmcnt counts in issue order: the stores then wait only for their own tile)
+        while (true) {
+            const long long tb = take(1);
+            if (tb < ntiles) tile_load<R, NIN>(a4, b4, n4, tb, vb);
+            tile_store<R, NIN>(r4, n4, ta, va, f);
+            if (tb >= ntiles) break;
+            ta = take(0);
+            if (ta < ntiles) tile_load<R, NIN>(a4, b4, n4, ta, va);
+            tile_store<R, NIN>(r4, n4, tb, vb, f);
+            if (ta >= ntiles) break;
+        }
+    }
+    if (threadIdx.x == 0) {  // the last block to finish resets the pair for the next launch on this stream
+        if (atomicAdd(&tk->done, 1u) == gridDim.x - 1) {
+            atomicExch(&tk->next, 0u);
+            atomicExch(&tk->done, 0u);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTileWaves * kWave) void vmul_tiles(const float* a, const float* b, float* r, long long n, Ticket* tk) {
+    stream_tiles<8, 2>(a, b, r, n, tk, [](float x, float y) { return x * y; });
+}
+__global__ __launch_bounds__(kTileWaves * kWave) void vadd_tiles(const float* a, const float* b, float* r, long long n, Ticket* tk) {
+    stream_tiles<8, 2>(a, b, r, n, tk, [](float x, float y) { return x + y; });
+}
+__global__ __launch_bounds__(kTileWaves * kWave) void axpy_tiles(float alpha, const float* x, float* y, long long n, Ticket* tk) {
+    stream_tiles<8, 2>(x, y, y, n, tk, [alpha](float xv, float yv) { return fmaf(alpha, xv, yv); });
+}
+__global__ __launch_bounds__(kTileWaves * kWave) void copy_tiles(const float* a, float* r, long long n, Ticket* tk) {
+    stream_tiles<16, 1>(a, nullptr, r, n, tk, [](float x, float) { return x; });
+}
+__global__ __launch_bounds__(kTileWaves * kWave) void fill_tiles(float* r, float v, long long n, Ticket* tk) {
+    stream_tiles<16, 0>(nullptr, nullptr, r, n, tk, [v](float, float) { return v; });
+}
+
+// ---- grid-stride forms (hipGraph capture, and the reference point of the A/B)
 template <class F>
 __device__ __forceinline__ void stream_binary(const float* a, const float* b, float* r, long long n, F f) {
     const long long n4 = n >> 2;
@@ -56,6 +177,9 @@ __global__ __launch_bounds__(kThreads) void vadd_kernel(const float* a, const fl
 }
 __global__ __launch_bounds__(kThreads) void axpy_kernel(float alpha, const float* x, float* y, long long n) {
     stream_binary(x, y, y, n, [alpha](float xv, float yv) { return fmaf(alpha, xv, yv); });
+}
+__global__ __launch_bounds__(kThreads) void copy_kernel(const float* a, float* r, long long n) {
+    stream_binary(a, a, r, n, [](float x, float) { return x; });
 }
 
 __global__ __launch_bounds__(kThreads) void fill_kernel(float* x, float v, long long n) {
@@ -117,26 +241,76 @@ inline int stream_grid(long long n, int per_thread) {
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 256;
+    return cus > 0 ? cus : 256;
+}
+
+// The self-resetting counter pair of (device, stream), allocated and zeroed on first use (kept for the process);
+// nullptr while `s` is capturing (the caller then launches the grid-stride form).
+Ticket* stream_ticket(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, Ticket*> reg;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (cap != hipStreamCaptureStatusNone) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = reg.find({dev, s});
+    if (it != reg.end()) return it->second;
+    Ticket* t = nullptr;
+    if (hipMalloc(&t, sizeof(Ticket)) != hipSuccess || hipMemset(t, 0, sizeof(Ticket)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    reg[{dev, s}] = t;
+    return t;
+}
+
+template <int R>
+int tile_grid(long long n) {
+    const long long tile = (long long)kTileWaves * kWave * R * 4, tiles = (n + tile - 1) / tile;
+    const int cus = device_cus();
+    return (int)(tiles < cus ? (tiles < 1 ? 1 : tiles) : cus);  // one resident 512-thread block per CU
+}
 }  // namespace
 
 extern "C" int pcmx_vmul_f32(const float* a, const float* b, float* r, long long n, hipStream_t s) {
     if (n <= 0) return 0;
     if (!aligned16(a) || !aligned16(b) || !aligned16(r)) return -1;
-    vmul_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(a, b, r, n);
+    if (Ticket* tk = stream_ticket(s)) vmul_tiles<<<tile_grid<8>(n), kTileWaves * kWave, 0, s>>>(a, b, r, n, tk);
+    else vmul_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(a, b, r, n);
     return (int)hipGetLastError();
 }
 
 extern "C" int pcmx_vadd_f32(const float* a, const float* b, float* r, long long n, hipStream_t s) {
     if (n <= 0) return 0;
     if (!aligned16(a) || !aligned16(b) || !aligned16(r)) return -1;
-    vadd_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(a, b, r, n);
+    if (Ticket* tk = stream_ticket(s)) vadd_tiles<<<tile_grid<8>(n), kTileWaves * kWave, 0, s>>>(a, b, r, n, tk);
+    else vadd_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(a, b, r, n);
     return (int)hipGetLastError();
 }
 
 extern "C" int pcmx_axpy_f32(float alpha, const float* x, float* y, long long n, hipStream_t s) {
     if (n <= 0) return 0;
     if (!aligned16(x) || !aligned16(y)) return -1;
-    axpy_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(alpha, x, y, n);
+    if (Ticket* tk = stream_ticket(s)) axpy_tiles<<<tile_grid<8>(n), kTileWaves * kWave, 0, s>>>(alpha, x, y, n, tk);
+    else axpy_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(alpha, x, y, n);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcmx_copy_f32(const float* a, float* r, long long n, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (!aligned16(a) || !aligned16(r)) return -1;
+    if (Ticket* tk = stream_ticket(s)) copy_tiles<<<tile_grid<16>(n), kTileWaves * kWave, 0, s>>>(a, r, n, tk);
+    else copy_kernel<<<stream_grid(n, kUnroll), kThreads, 0, s>>>(a, r, n);
     return (int)hipGetLastError();
 }
 
@@ -151,7 +325,8 @@ extern "C" int pcmx_gather_f32(const float* src, long long n_src, const int* idx
 extern "C" int pcmx_fill_f32(float* x, float v, long long n, hipStream_t s) {
     if (n <= 0) return 0;
     if (!aligned16(x)) return -1;
-    fill_kernel<<<stream_grid(n, 1), kThreads, 0, s>>>(x, v, n);
+    if (Ticket* tk = stream_ticket(s)) fill_tiles<<<tile_grid<16>(n), kTileWaves * kWave, 0, s>>>(x, v, n, tk);
+    else fill_kernel<<<stream_grid(n, 1), kThreads, 0, s>>>(x, v, n);
     return (int)hipGetLastError();
 }
 

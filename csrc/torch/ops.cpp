@@ -81,6 +81,16 @@ at::Tensor axpy_(at::Tensor y, double alpha, const at::Tensor& x) {
     return y;
 }
 
+at::Tensor copy_(at::Tensor dst, const at::Tensor& src) {
+    check_gpu(dst, "dst", at::kFloat), check_gpu(src, "src", at::kFloat);
+    TORCH_CHECK(dst.is_contiguous() && (reinterpret_cast<uintptr_t>(dst.data_ptr()) & 15u) == 0, "copy_: dst must be contiguous, 16-B aligned");
+    TORCH_CHECK(src.numel() == dst.numel() && src.device() == dst.device(), "copy_: size / device mismatch");
+    const at::DeviceGuard g(dst.device());
+    auto sc = aligned_contig(src);
+    check_rc(pcmx_copy_f32(sc.data_ptr<float>(), dst.data_ptr<float>(), dst.numel(), cur_stream(dst)), "copy_");
+    return dst;
+}
+
 at::Tensor fill_(at::Tensor x, double v) {
     check_gpu(x, "x", at::kFloat);
     TORCH_CHECK(x.is_contiguous() && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15u) == 0, "fill_: contiguous, aligned");
@@ -632,6 +642,9 @@ void spmv_sliced_combine(const at::Tensor& ypart, const at::Tensor& row_mask, co
     const int *sp = nullptr, *ss = nullptr;
     float* sb = nullptr;
     if (send_ptr.has_value()) {
+        // INTERNAL op: the list CONTENTS (send_ptr rising from 0 to send_slot.numel(), every slot inside sendbuf) are
+        // device data; checking them here would sync every call, so SlicedCSR._check_send (the only caller,
+        // ops/sparse.py) validates each set of lists once. Shapes and dtypes are checked here.
         TORCH_CHECK(send_slot.has_value() && sendbuf.has_value(), "spmv_sliced_combine: send_ptr needs send_slot and sendbuf");
         check_gpu(*send_ptr, "send_ptr", at::kInt), check_gpu(*send_slot, "send_slot", at::kInt);
         check_gpu(*sendbuf, "sendbuf", at::kFloat);
@@ -711,6 +724,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("axpy_(Tensor(a!) y, float alpha, Tensor x) -> Tensor(a!)");
     m.def("gather_(Tensor src, Tensor idx, Tensor(a!) out) -> Tensor(a!)");
     m.def("fill_(Tensor(a!) x, float v) -> Tensor(a!)");
+    m.def("copy_(Tensor(a!) dst, Tensor src) -> Tensor(a!)");
     m.def("rand_uniform_(Tensor(a!) x, int seed, float lo, float hi) -> Tensor(a!)");
     m.def("reduce(Tensor x, int op) -> Tensor");
     m.def("dot(Tensor a, Tensor b) -> Tensor");
@@ -749,6 +763,7 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("axpy_", axpy_);
     m.impl("gather_", gather_);
     m.impl("fill_", fill_);
+    m.impl("copy_", copy_);
     m.impl("rand_uniform_", rand_uniform_);
     m.impl("reduce", reduce);
     m.impl("dot", dot);

@@ -55,6 +55,10 @@ class CSR:
         return d
 
 
+class PackedLayoutUnavailable(ValueError):
+    """SlicedCSR: the requested item size needs the packed index stream, which this matrix's slices cannot use."""
+
+
 class SlicedCSR:
     """XCD-sliced CSR for SpMV on MI355X (csrc/kernels/spmv.hip: spmv_sliced_kernel).
 
@@ -109,6 +113,12 @@ class SlicedCSR:
             tgt = torch.arange(1, S, device=dev, dtype=torch.float64) * (float(cum[-1]) / S)
             bounds = torch.searchsorted(cum, tgt, right=True).to(torch.int32)
         self.bounds = bounds.cpu()
+        if item_nnz in (256, 384):  # decided BEFORE the build: these items exist in the packed index stream only
+            b = self.bounds.tolist()
+            widest = max(h - l for l, h in zip([0] + b, b + [m.n_cols]))
+            if not pack or nnz == 0 or H >= 1 << 21 or widest >= 1 << 21:
+                raise PackedLayoutUnavailable(f"item_nnz {item_nnz} needs the packed index stream (every slice < 2^21 "
+                                              f"columns; widest {widest})")
         sid = torch.bucketize(col, bounds, right=True)  # slice of every nonzero (int64)
         deg = (m.row_ptr[1:] - m.row_ptr[:-1]).to(dev)
         rows = torch.repeat_interleave(torch.arange(n, device=dev), deg)
@@ -173,7 +183,10 @@ class SlicedCSR:
         n_ch = (n + 63) // 64
         self.fix_chunk0 = torch.searchsorted(self.fix[:, 1].contiguous().long(),
                                              torch.arange(0, n_ch + 2, device=dev) * 64).to(torch.int32).contiguous()
-        self.fused_combine = True  # combine + fix-up (+ pack) in one launch (False: the in-library two-launch form)
+        # combine + fix-up (+ pack) in ONE launch (True) or the in-library two-launch form (False, the default: faster
+        # for a single matrix, 69 + 5 us against 77 us on the 1e8-nnz product; DistributedSpMV turns it on for its
+        # distributed steps, where the send-buffer pack rides along: profiles/r5_spmv/)
+        self.fused_combine = False
         # resident product blocks per CU of the column-split phase 0 / phase 1 launches (0: the library default, 3;
         # DistributedSpMV sets them by rank size)
         self.phase_blocks = (0, 0)
@@ -184,8 +197,7 @@ class SlicedCSR:
         self.ypart = torch.empty(max(1, out0[-1]), dtype=torch.float32, device=dev)
         self.extra = torch.empty(max(1, item0[-1]), dtype=torch.float32, device=dev)
         self._pack(slice_nnz, pack)
-        if item_nnz in (256, 384) and self.cr is None:
-            raise ValueError(f"item_nnz {item_nnz} needs the packed index stream (every slice < 2^21 columns)")
+        assert item_nnz not in (256, 384) or self.cr is not None  # (decided above)
 
     def _pack(self, slice_nnz: torch.Tensor, pack: bool) -> None:
         """Packed index stream (the kernel's production layout): one int32 per nonzero = column - first tail column
@@ -235,9 +247,29 @@ class SlicedCSR:
         carry it to the peers (the distributed step's pack, fused into the same launch)."""
         meta = self._meta_packed if getattr(self, "_meta_packed", None) is not None else self.meta
         sp, ss, sb = send if send is not None else (None, None, None)
+        if send is not None:
+            self._check_send(sp, ss, sb)
         ops().spmv_sliced_combine(self.ypart, self.row_mask, self.chunk_base, meta, self.n_slices, self.extra,
                                   self.fix, self.fix_chunk0, out, self.n_rows, sp, ss, sb)
         return out
+
+    def _check_send(self, sp: torch.Tensor, ss: torch.Tensor, sb: torch.Tensor) -> None:
+        """The fused pack writes sendbuf[send_slot[k]] for k in [send_ptr[r], send_ptr[r + 1]) of every row r, on the
+        device, unchecked: the lists are validated here once per set (a host sync; the distributed step reuses the
+        same tensors every step). send_ptr: n_rows + 1 non-decreasing entries from 0 to len(send_slot); every slot
+        inside sendbuf."""
+        key = (sp.data_ptr(), ss.data_ptr(), sb.data_ptr(), sp.numel(), ss.numel(), sb.numel())
+        if key in getattr(self, "_send_ok", ()):
+            return
+        if sp.numel() < self.n_rows + 1 or sp.dtype != torch.int32 or ss.dtype != torch.int32:
+            raise ValueError("send: int32 send_ptr of n_rows + 1 entries and int32 send_slot")
+        p = sp[:self.n_rows + 1].long()
+        ok = int(p[0]) == 0 and int(p[-1]) == ss.numel() and bool((p[1:] >= p[:-1]).all())
+        if ss.numel():
+            ok = ok and int(ss.min()) >= 0 and int(ss.max()) < sb.numel()
+        if not ok:
+            raise ValueError("send: send_ptr must rise from 0 to len(send_slot) and every slot must lie in sendbuf")
+        self._send_ok = getattr(self, "_send_ok", set()) | {key}
 
     def spmv(self, x: torch.Tensor, out: torch.Tensor | None = None, mode: int = 0,
              phases: tuple[int, int] | None = None, send: tuple | None = None) -> torch.Tensor:

@@ -62,6 +62,13 @@ def axpy_(y: torch.Tensor, alpha: float, x: torch.Tensor, n_threads: int = 0) ->
     return y
 
 
+def copy_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """dst <- src (f32): the ticket-ordered streaming kernel on the GPU, torch's copy on the host."""
+    if dst.is_cuda:
+        return ops().copy_(dst, src)
+    return dst.copy_(src)
+
+
 def dot(a: torch.Tensor, b: torch.Tensor, n_threads: int = 0) -> torch.Tensor:
     """sum(a*b) as a 0-d float32 tensor (f64 host accumulation / f64 final fold on the GPU)."""
     if a.is_cuda:

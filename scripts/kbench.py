@@ -73,13 +73,19 @@ def bench_stream(n, reps, what):
             med, best = timeit(lambda: torch.cumsum(x, 0), reps)
             emit(kernel="scan", impl="torch", n=n, ms=med, ms_best=best, gbps=8 * n / med / 1e6)
     if "vec" in what:
-        z = torch.empty_like(x)
-        med, best = timeit(lambda: ops.vadd(x, x), reps)
-        emit(kernel="vadd", impl="pcmx", n=n, ms=med, ms_best=best, gbps=12 * n / med / 1e6)
-        med, best = timeit(lambda: torch.add(x, x, out=z), reps)
-        emit(kernel="vadd", impl="torch", n=n, ms=med, ms_best=best, gbps=12 * n / med / 1e6)
-        med, best = timeit(lambda: z.copy_(x), reps)
-        emit(kernel="copy", impl="torch", n=n, ms=med, ms_best=best, gbps=8 * n / med / 1e6)
+        # the production streaming ops (ticket-ordered tiles, vector.hip) against torch, interleaved over 3 rounds
+        w, z = torch.empty_like(x), torch.empty_like(x)
+        ops.rand_uniform_(w, 2, -1, 1)
+        cases = [("vadd", 12, lambda: ops.vadd(x, w), lambda: torch.add(x, w, out=z)),
+                 ("vmul", 12, lambda: ops.vmul(x, w), lambda: torch.mul(x, w, out=z)),
+                 ("axpy", 12, lambda: ops.axpy_(z, 0.5, x), lambda: z.add_(x, alpha=0.5)),
+                 ("copy", 8, lambda: ops.copy_(z, x), lambda: z.copy_(x)),
+                 ("fill", 4, lambda: ops.fill_(z, 1.5), lambda: z.fill_(1.5))]
+        for rnd in range(3):
+            for name, bpe, mine, ref in cases:
+                for impl, fn in (("pcmx", mine), ("torch", ref)):
+                    med, best = timeit(fn, reps)
+                    emit(kernel=name, impl=impl, round=rnd, n=n, ms=med, ms_best=best, gbps=bpe * n / med / 1e6)
 
 
 def main():

@@ -125,6 +125,159 @@ __global__ __launch_bounds__(256) void vadd_chunk_kernel(const f32x4* a, const f
     }
 }
 
+// ROUND 6: the SCAN's streaming structure applied to copy / vadd / axpy. scan_parked_kernel moves 1R + 1W at
+// 6.29 TB/s; these isolate which of its traits matter: W waves x R f32x4 rows per lane (tile = W*R KiB per input),
+// a PERSISTENT grid of `per_cu` blocks per CU, tiles handed out in time order (atomic ticket, TICKET) or statically
+// (tile = block + k * grid), and the next tile's loads issued BEFORE the current tile's stores (double buffer).
+// NIN = 1: copy (r = a); NIN = 2: r = a + b (vadd; axpy is the same traffic with r aliasing b).
+template <int R, int NIN>
+struct TileRegs {
+    f32x4 a[R], b[NIN == 2 ? R : 1];
+};
+
+template <int R, int W, int NIN>
+__device__ __forceinline__ void tl_load(const f32x4* a, const f32x4* b, long long t, TileRegs<R, NIN>& v) {
+    const long long base = t * (W * 64 * R) + (long long)(threadIdx.x / 64) * (64 * R) + (threadIdx.x & 63);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v.a[r] = __builtin_nontemporal_load(a + base + r * 64);
+    if constexpr (NIN == 2) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) v.b[r] = __builtin_nontemporal_load(b + base + r * 64);
+    }
+}
+template <int R, int W, int NIN>
+__device__ __forceinline__ void tl_store(f32x4* out, long long t, const TileRegs<R, NIN>& v) {
+    const long long base = t * (W * 64 * R) + (long long)(threadIdx.x / 64) * (64 * R) + (threadIdx.x & 63);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if constexpr (NIN == 2) __builtin_nontemporal_store(v.a[r] + v.b[r], out + base + r * 64);
+        else __builtin_nontemporal_store(v.a[r], out + base + r * 64);
+    }
+}
+
+template <int R, int W, int NIN, bool TICKET>
+__global__ __launch_bounds__(W * 64) void tiled_kernel(const f32x4* a, const f32x4* b, f32x4* r, long long ntiles,
+                                                       unsigned* ticket) {
+    __shared__ unsigned s_t[2];
+    TileRegs<R, NIN> va, vb;
+    auto next_tile = [&](long long cur, int slot) -> long long {
+        if constexpr (TICKET) {
+            if (threadIdx.x == 0) s_t[slot] = atomicAdd(ticket, 1u);
+            __syncthreads();
+            return (long long)s_t[slot];
+        } else {
+            return cur + gridDim.x;
+        }
+    };
+    long long ta = TICKET ? next_tile(0, 0) : (long long)blockIdx.x;
+    if (ta >= ntiles) return;
+    tl_load<R, W, NIN>(a, b, ta, va);
+    while (true) {
+        const long long tb = next_tile(ta, 1);
+        if (tb < ntiles) tl_load<R, W, NIN>(a, b, tb, vb);
+        tl_store<R, W, NIN>(r, ta, va);
+        if (tb >= ntiles) break;
+        ta = next_tile(tb, 0);
+        if (ta < ntiles) tl_load<R, W, NIN>(a, b, ta, va);
+        tl_store<R, W, NIN>(r, tb, vb);
+        if (ta >= ntiles) break;
+    }
+}
+
+// ONE-SHOT: one tile per block, grid = number of tiles: the hardware dispatcher hands tiles out in launch order (the
+// ticket order, with no counter to reset); no double buffer, several resident blocks per CU overlap instead.
+template <int R, int W, int NIN>
+__global__ __launch_bounds__(W * 64) void oneshot_kernel(const f32x4* a, const f32x4* b, f32x4* r) {
+    TileRegs<R, NIN> v;
+    tl_load<R, W, NIN>(a, b, blockIdx.x, v);
+    tl_store<R, W, NIN>(r, blockIdx.x, v);
+}
+
+// SELF-RESETTING TICKET: as tiled_kernel<TICKET> but the counter needs no memset: the last block to finish zeroes it
+// (ticket[0] = next tile, ticket[1] = finished blocks); stream order makes the next launch see zeros.
+template <int R, int W, int NIN>
+__global__ __launch_bounds__(W * 64) void tiled_selfreset_kernel(const f32x4* a, const f32x4* b, f32x4* r,
+                                                                 long long ntiles, unsigned* ticket) {
+    __shared__ unsigned s_t[2];
+    TileRegs<R, NIN> va, vb;
+    auto take = [&](int slot) -> long long {
+        if (threadIdx.x == 0) s_t[slot] = atomicAdd(ticket, 1u);
+        __syncthreads();
+        return (long long)s_t[slot];
+    };
+    long long ta = take(0);
+    if (ta < ntiles) {
+        tl_load<R, W, NIN>(a, b, ta, va);
+        while (true) {
+            const long long tb = take(1);
+            if (tb < ntiles) tl_load<R, W, NIN>(a, b, tb, vb);
+            tl_store<R, W, NIN>(r, ta, va);
+            if (tb >= ntiles) break;
+            ta = take(0);
+            if (ta < ntiles) tl_load<R, W, NIN>(a, b, ta, va);
+            tl_store<R, W, NIN>(r, tb, vb);
+            if (ta >= ntiles) break;
+        }
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(ticket + 1, 1u) == gridDim.x - 1) {
+            atomicExch(ticket, 0u);
+            atomicExch(ticket + 1, 0u);
+        }
+    }
+}
+
+int tiled_sweep(f32x4* a, f32x4* b, f32x4* r, long long n4, unsigned* ticket, hipEvent_t e0, hipEvent_t e1) {
+    int cus = 256;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const double B = (double)n4 * 16;
+    auto time = [&](const char* name, double bytes, auto fn) {
+        for (int i = 0; i < 2; ++i) fn();
+        hipEventRecord(e0);
+        for (int i = 0; i < 10; ++i) fn();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        ms /= 10;
+        printf("%-36s %.4f ms %7.1f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+    };
+    char nm[96];
+#define TL(R, W, NIN, TK, PERCU)                                                                               \
+    {                                                                                                          \
+        const long long tile4 = (long long)W * 64 * R, nt = n4 / tile4;                                        \
+        const int grid = (int)(nt < (long long)cus * PERCU ? nt : (long long)cus * PERCU);                     \
+        snprintf(nm, sizeof nm, "%s R%d W%d %s x%d", NIN == 1 ? "copy" : "vadd", R, W, TK ? "ticket" : "static", \
+                 PERCU);                                                                                       \
+        time(nm, (NIN + 1) * (double)nt * tile4 * 16, [&] {                                                    \
+            if (TK) hipMemsetAsync(ticket, 0, 4);                                                              \
+            tiled_kernel<R, W, NIN, TK><<<grid, W * 64>>>(a, b, r, nt, ticket);                                \
+        });                                                                                                    \
+    }
+    TL(16, 8, 1, true, 1)
+    TL(16, 8, 1, false, 1)
+    TL(16, 8, 1, true, 2)
+    TL(16, 8, 1, false, 2)
+    TL(8, 8, 1, true, 2)
+    TL(8, 8, 1, false, 2)
+    TL(8, 16, 1, true, 1)
+    TL(8, 4, 1, false, 4)
+    TL(16, 4, 1, false, 2)
+    TL(8, 8, 2, true, 1)
+    TL(8, 8, 2, false, 1)
+    TL(8, 8, 2, true, 2)
+    TL(8, 8, 2, false, 2)
+    TL(16, 8, 2, false, 1)
+    TL(8, 16, 2, true, 1)
+    TL(8, 4, 2, false, 4)
+    TL(4, 8, 2, false, 4)
+#undef TL
+    (void)B;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const long long n = argc > 1 ? (long long)atof(argv[1]) : 1000000000LL;
     const long long n4 = n / 4;
@@ -152,6 +305,76 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const double B = (double)n4 * 16;
+    if (argc > 2 && argv[2][0] == 't') {  // persistent tiled (scan-structure) sweep
+        unsigned* ticket;
+        CK(hipMalloc(&ticket, 16));
+        return tiled_sweep(a, b, r, n4, ticket, e0, e1);
+    }
+    if (argc > 2 && argv[2][0] == 'a') {  // interleaved A/B: grid-stride vs ticket-tiled, 6 alternations
+        unsigned* ticket;
+        CK(hipMalloc(&ticket, 16));
+        int cus = 256;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        const long long ntc = n4 / (8 * 64 * 16), ntv = n4 / (8 * 64 * 8);
+        for (int rep = 0; rep < 6; ++rep) {
+            printf("-- alternation %d\n", rep);
+            time("grid copy U4 nt g16384", 2 * B, [&] { copy_kernel<4, true><<<16384, 256>>>(a, r, n4); });
+            time("tiled copy R16W8 ticket x1", 2 * (double)ntc * 8192 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tiled_kernel<16, 8, 1, true><<<cus, 512>>>(a, b, r, ntc, ticket);
+            });
+            time("grid vadd U4 nt g16384", 3 * B, [&] { vadd_kernel<4, true><<<16384, 256>>>(a, b, r, n4); });
+            time("tiled vadd R8W8 ticket x2", 3 * (double)ntv * 4096 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tiled_kernel<8, 8, 2, true><<<2 * cus, 512>>>(a, b, r, ntv, ticket);
+            });
+            time("grid axpy(in place) U4 nt g16384", 3 * B, [&] { vadd_kernel<4, true><<<16384, 256>>>(a, b, b, n4); });
+            time("tiled axpy(in place) R8W8 ticket x2", 3 * (double)ntv * 4096 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tiled_kernel<8, 8, 2, true><<<2 * cus, 512>>>(a, b, b, ntv, ticket);
+            });
+            time("tiled copy R16W8 static x1", 2 * (double)ntc * 8192 * 16,
+                 [&] { tiled_kernel<16, 8, 1, false><<<cus, 512>>>(a, b, r, ntc, ticket); });
+        }
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 'o') {  // one-shot + self-resetting ticket vs the memset ticket, 4 alternations
+        unsigned* ticket;
+        CK(hipMalloc(&ticket, 16));
+        CK(hipMemset(ticket, 0, 16));
+        int cus = 256;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        char nm[96];
+#define OS(R, W, NIN)                                                                                         \
+    {                                                                                                         \
+        const long long tile4 = (long long)W * 64 * R, nt = n4 / tile4;                                      \
+        snprintf(nm, sizeof nm, "oneshot %s R%d W%d", NIN == 1 ? "copy" : "vadd", R, W);                     \
+        time(nm, (NIN + 1) * (double)nt * tile4 * 16, [&] { oneshot_kernel<R, W, NIN><<<(int)nt, W * 64>>>(a, b, r); }); \
+    }
+#define SR(R, W, NIN, PERCU)                                                                                  \
+    {                                                                                                         \
+        const long long tile4 = (long long)W * 64 * R, nt = n4 / tile4;                                      \
+        snprintf(nm, sizeof nm, "selfreset %s R%d W%d x%d", NIN == 1 ? "copy" : "vadd", R, W, PERCU);        \
+        time(nm, (NIN + 1) * (double)nt * tile4 * 16,                                                        \
+             [&] { tiled_selfreset_kernel<R, W, NIN><<<cus * PERCU, W * 64>>>(a, b, r, nt, ticket); });      \
+    }
+        for (int rep = 0; rep < 4; ++rep) {
+            printf("-- alternation %d\n", rep);
+            OS(4, 4, 1) OS(8, 4, 1) OS(16, 4, 1) OS(8, 8, 1) OS(16, 8, 1)
+            OS(4, 4, 2) OS(8, 4, 2) OS(4, 8, 2) OS(8, 8, 2)
+            SR(16, 8, 1, 1) SR(16, 8, 1, 2) SR(8, 8, 2, 1) SR(8, 8, 2, 2) SR(8, 4, 2, 4)
+            const long long ntc = n4 / (8 * 64 * 16);
+            time("tiled copy R16W8 ticket x1", 2 * (double)ntc * 8192 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tiled_kernel<16, 8, 1, true><<<cus, 512>>>(a, b, r, ntc, ticket);
+            });
+            hipMemsetAsync(ticket, 0, 16);
+            time("grid copy U4 nt g16384", 2 * B, [&] { copy_kernel<4, true><<<16384, 256>>>(a, r, n4); });
+        }
+#undef OS
+#undef SR
+        return 0;
+    }
     if (argc > 2) {  // chunked-only sweep: grid sizes x chunked kernels
         for (int grid : {1024, 2048, 4096, 8192, 16384, 32768}) {
             const long long chunk = (n4 + grid - 1) / grid;

@@ -26,6 +26,52 @@ def test_vmul_vadd_axpy(gpu, n):
     torch.testing.assert_close(y, 2.5 * a + b)
 
 
+@pytest.mark.parametrize("n", [1, 5, 16384, 16387, 32768 * 3 + 4, (1 << 24) + 3, 256 * 32768 * 2 + 7])
+def test_ticket_streams_copy_fill_exact(gpu, n):
+    """The ticket-ordered streaming kernels (vector.hip): copy and fill bit-exact, vadd / vmul bit-exact against
+    torch (one fp32 op per element), across single-tile, partial-tile, scalar-tail and more-tiles-than-CUs sizes;
+    the self-resetting counter is exercised by back-to-back launches on one stream."""
+    a = torch.rand(n, device=gpu)
+    b = torch.rand(n, device=gpu)
+    for _ in range(3):
+        d = torch.full_like(a, float("nan"))
+        ops.copy_(d, a)
+        assert torch.equal(d, a)
+        assert torch.equal(ops.vadd(a, b), a + b) and torch.equal(ops.vmul(a, b), a * b)
+        ops.fill_(d, 1.25)
+        assert bool((d == 1.25).all())
+
+
+def test_ticket_streams_per_stream_counters_and_capture(gpu):
+    """Launches on two streams at once (each stream has its own counter pair) and inside a hipGraph capture (the
+    grid-stride form: no counter is allocated while capturing) all give exact results."""
+    n = (1 << 23) + 1
+    a, b = torch.rand(n, device=gpu), torch.rand(n, device=gpu)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1.wait_stream(torch.cuda.current_stream())
+    s2.wait_stream(torch.cuda.current_stream())
+    outs = []
+    for s in (s1, s2, s1, s2):
+        with torch.cuda.stream(s):
+            outs.append(ops.vadd(a, b) if s is s1 else ops.vmul(a, b))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], a + b) and torch.equal(outs[2], a + b)
+    assert torch.equal(outs[1], a * b) and torch.equal(outs[3], a * b)
+    y = b.clone()
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream()
+    with torch.cuda.stream(cs):
+        dst = torch.empty_like(a)
+        with torch.cuda.graph(g, stream=cs):
+            ops.copy_(dst, a)
+            ops.axpy_(y, 2.0, a)
+    y.copy_(b)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(dst, a)
+    torch.testing.assert_close(y, 2.0 * a + b)
+
+
 def test_vmul_reference_demo(gpu):
     # ref multiply_opencl.c:47-50: a[i] = i+1, b[i] = 1/(i+1) -> every product is 1.0
     i = torch.arange(1024, device=gpu, dtype=torch.float32)
