@@ -42,7 +42,13 @@ collective decision on a separate CPU process group at the end of each section: 
 pair with a data collective another rank waits in; a rank that fails before a timed region stops the others at the
 next decision point, Runner), and the run exits 1. `--inject-fault SECTION:RANK:KIND` (KIND perturb = corrupt that
 rank's timed output after timing, raise = raise in its check, raise-early = raise right after its set-up, before the
-timed region) is the test hook.
+timed region, selftest = report the stencil / SpMV N > 1 self-test as failed) is the test hook.
+
+At N > 1 every distributed section (reduce, scan, stencil, spmv) also times its COMPUTE-ONLY twin in the same job
+(the same kernels on the same data, the exchange skipped) and reports <section>_compute_only_ms,
+<section>_comm_exposed_ms, the per-rank spread of its median device step time and the bytes each rank exchanges per
+step (attribute_comm), plus the process group's backend and size (comm_backend, comm_world_size): a first
+multi-GPU run then says whether a miss is exposed communication, imbalance between ranks or compute.
 
 rank 0 prints ONE JSON line; `value` = whole-job SGEMM TFLOPS (sum over GPUs), the other configs are extra fields
 of the same line. `--small` shrinks every size (CPU/gloo rehearsal of the multi-rank path, tests).
@@ -206,6 +212,7 @@ class Checks:
         self.items[key] = (bool(ok), "all", None)
 
     def info(self, key, value, agg="max"):
+        """agg over ranks: "max", "min" or "sum"."""
         self.items[key] = (value, agg, None)
 
 
@@ -232,8 +239,8 @@ class Runner:
         self.fault = None
         if fault:
             sec, rank, kind = fault.split(":")
-            if kind not in ("perturb", "raise", "raise-early"):
-                raise ValueError("--inject-fault SECTION:RANK:perturb|raise|raise-early")
+            if kind not in ("perturb", "raise", "raise-early", "selftest"):
+                raise ValueError("--inject-fault SECTION:RANK:perturb|raise|raise-early|selftest")
             self.fault = (sec, int(rank), kind)
 
     def injected(self, section: str, kind: str) -> bool:
@@ -274,10 +281,11 @@ class Runner:
                     merged[k] = (v, agg, limit)
                     continue
                 pv = merged[k][0]
-                merged[k] = ((pv and v) if agg == "all" else max(pv, v) if agg == "max" else min(pv, v), agg, limit)
+                merged[k] = ((pv and v) if agg == "all" else max(pv, v) if agg == "max" else pv + v if agg == "sum"
+                             else min(pv, v), agg, limit)
         bad = []
         for k, (v, agg, limit) in merged.items():
-            self.out[k] = _r(v, 4) if agg in ("max", "min") and limit is None else v
+            self.out[k] = _r(v, 4) if agg in ("max", "min", "sum") and limit is None else v
             if (agg == "all" and not v) or (limit is not None and not v <= limit):
                 bad.append(k)
         if bad:
@@ -296,6 +304,40 @@ def device_times(chk: Checks, prefix: str, ms: list, hms: list | None = None) ->
         chk.info(f"{prefix}_device_ms_{k}", v, "max")
     if hms:
         chk.info(f"{prefix}_host_ms_max", max(hms), "max")
+
+
+def attribute_comm(ctx, chk: Checks, out: dict, prefix: str, full_ms: float, dev_ms: list, w, steps: int,
+                   warmup: int, settle_ms: float) -> None:
+    """N > 1: what a step's time is made of, measured in the same job (so a first multi-GPU run explains itself):
+      <prefix>_compute_only_ms      the same kernels on the same data with every exchange skipped (w.compute_only_step),
+                                    timed exactly like the full step (W warm-ups, K steps between barrier + sync, max
+                                    over ranks);
+      <prefix>_comm_exposed_ms      full step minus compute-only: the communication the schedule did not hide;
+      <prefix>_rank_step_ms_min/max the per-rank median device step time, lowest and highest rank (imbalance), for
+                                    the full step and (…_compute_only_rank_ms_min/max) the compute-only twin;
+      <prefix>_bytes_exchanged_per_step          the most one rank sends per step (payload bytes);
+      <prefix>_bytes_exchanged_per_step_total    summed over ranks.
+    Runs AFTER the section's checks: the twin leaves the data unchecked (stale halos / ghosts)."""
+    import statistics
+
+    from parallel_c_programs_amd.utils.harness import timed
+
+    ms_c = []
+    t = timed(ctx, w.compute_only_step, steps, warmup, ms_c, settle_ms=settle_ms)
+    comp = 1e3 * t / steps
+    out[f"{prefix}_compute_only_ms"] = _r(comp)
+    out[f"{prefix}_comm_exposed_ms"] = _r(full_ms - comp)
+    if dev_ms:
+        med = statistics.median(dev_ms)
+        chk.info(f"{prefix}_rank_step_ms_min", med, "min")
+        chk.info(f"{prefix}_rank_step_ms_max", med, "max")
+    if ms_c:
+        med = statistics.median(ms_c)
+        chk.info(f"{prefix}_compute_only_rank_ms_min", med, "min")
+        chk.info(f"{prefix}_compute_only_rank_ms_max", med, "max")
+    b = float(w.bytes_exchanged_per_step())
+    chk.info(f"{prefix}_bytes_exchanged_per_step", b, "max")
+    chk.info(f"{prefix}_bytes_exchanged_per_step_total", b, "sum")
 
 
 def main(argv=None):
@@ -431,6 +473,9 @@ def main(argv=None):
                 chk.flag(f"scan_{mode}_lookback_ok", c["lookback_ok"])
                 prev = chk.items.get("scan_full_max_rel_err_vs_fp64", (0.0,))[0]
                 chk.error("scan_full_max_rel_err_vs_fp64", max(prev, c["rel_err_vs_fp64"]), LIM)
+            if ctx.distributed:  # the compute-only twin, after the check (it overwrites the checked output)
+                yield
+                attribute_comm(ctx, chk, out, f"{name}_{mode}", rep["ms_per_step"], ms, w, K, Wm, SETTLE)
             del w
             if dev.type == "cuda":
                 torch.cuda.empty_cache()
@@ -461,8 +506,14 @@ def main(argv=None):
         chk.flag("stencil_timed_grid_bit_exact", c["timed_grid_bit_exact"])
         chk.flag("stencil_bit_exact", c["bit_exact_vs_single_step_oracle"])
         chk.flag("stencil_finite", c["finite"])
-        if c["halo_selftest"] is not None:  # the deep halo proven on this backend before timing (N > 1)
-            out["stencil_halo_selftest_bit_exact"] = c["halo_selftest"]
+        if runner.injected("stencil", "selftest"):  # test hook: a deep-halo self-test that failed on this backend
+            c["halo_selftest"] = False
+        if c["halo_selftest"] is not None:  # the deep halo proven on this backend before timing (N > 1): a failed
+            # self-test falls back to m = 1 for the timing but still fails the section (a broken schedule is a bug)
+            chk.flag("stencil_halo_selftest_bit_exact", c["halo_selftest"])
+        if ctx.distributed:
+            yield
+            attribute_comm(ctx, chk, out, "stencil", rep["ms_per_step"], ms, s, K, Wm, SETTLE)
         del s
         log(f"stencil {out['stencil_glups']} GLUP/s")
 
@@ -504,9 +555,16 @@ def main(argv=None):
         # chained steps x <- A x (the power-iteration pattern, exchanges deferred across step boundaries) vs fp64
         chk.error("spmv_iterated_max_rel_err_vs_fp64", c["iterated_max_rel_err_vs_fp64"], LIM)
         out["spmv_iterated_steps"], out["spmv_deferred_exchange"] = c["iterated_steps"], c["deferred"]
-        if c["pipeline_selftest"] is not None:  # deferred vs finished-in-step chained steps, bit for bit (N > 1)
-            out["spmv_pipeline_selftest_bit_identical"] = c["pipeline_selftest"]
+        if runner.injected("spmv", "selftest"):  # test hook: a deferred-pipeline self-test that failed
+            c["pipeline_selftest"] = False
+        if c["pipeline_selftest"] is not None:  # deferred vs finished-in-step chained steps, bit for bit (N > 1);
+            # the timed steps stop deferring on a mismatch, and the section fails
+            chk.flag("spmv_pipeline_selftest_bit_identical", c["pipeline_selftest"])
         runner.maybe_raise("spmv")
+        if ctx.distributed:
+            yield
+            attribute_comm(ctx, chk, out, "spmv", rep["ms_per_step"], ms, sp, K, Wm, SETTLE)
+            sp.d.finish()
         rows = (sp.d.row0, sp.d.row1)
         del sp
         log(f"spmv {out['spmv_gflops']} GFLOP/s")
@@ -531,6 +589,10 @@ def main(argv=None):
 
     if ctx.distributed and dev.type == "cuda" and ctx.backend == "nccl":
         runner.run("allreduce", allreduce)
+    if ctx.distributed:
+        import torch.distributed as dist
+
+        out["comm_backend"], out["comm_world_size"] = ctx.backend, dist.get_world_size()
 
     rc = 1 if runner.failed else 0
     if rank == 0:

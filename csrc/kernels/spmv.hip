@@ -1219,7 +1219,11 @@ const pcmx::i32x4* banded_lut_table(const BandGeo& g, hipStream_t s) {
     }
     auto& ent = cache[key];
     ent.second = std::move(tab);
-    if (hipMemcpyAsync(d, ent.second.data(), ent.second.size() * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess) {
+    // the upload completes before the pointer is cached and returned (once per geometry; never inside a capture,
+    // see above): a later caller on ANOTHER stream finds the cached table and must not read it before the copy on s
+    // has landed
+    if (hipMemcpyAsync(d, ent.second.data(), ent.second.size() * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
         cache.erase(key);
         (void)hipFree(d);
         (void)hipGetLastError();

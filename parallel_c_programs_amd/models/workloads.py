@@ -44,6 +44,16 @@ class Workload:
         so a local failure cannot leave another rank waiting in a data collective."""
         return {"check_passed": True}
 
+    def compute_only_step(self) -> None:
+        """The same kernels on the same data as step(), with every inter-rank exchange skipped (N > 1 attribution:
+        full step minus this = the exposed communication; ref 2-mpi-region-growing/region.c:497-532 separates the
+        exchange from the compute the same way). Leaves the workload's state unchecked: run it after check()."""
+        self.step()
+
+    def bytes_exchanged_per_step(self) -> float:
+        """Payload bytes this rank SENDS to other ranks per step (averaged over a deep-halo period)."""
+        return 0.0
+
 
 class Sgemm(Workload):
     """C = A @ B, fp32 exact (MFMA v_mfma_f32_32x32x2_f32), per-rank operands (data-parallel, weak)."""
@@ -100,6 +110,12 @@ class Reduce(Workload):
         self.ctx.all_reduce_(s)
         self.total.copy_(s.reshape(()))
 
+    def compute_only_step(self):
+        self.total.copy_(ops.reduce(self.x, "sum").reshape(()).float())
+
+    def bytes_exchanged_per_step(self):
+        return 4.0 if self.ctx.distributed else 0.0  # one f32 into the all-reduce
+
     def work_per_step(self):
         return 4.0 * self.x.numel()
 
@@ -124,6 +140,12 @@ class Scan(Workload):
 
     def step(self):
         self.y = global_scan(self.x, self.ctx)
+
+    def compute_only_step(self):
+        self.y = global_scan(self.x, self.ctx, comm=False)
+
+    def bytes_exchanged_per_step(self):
+        return 4.0 if self.ctx.distributed else 0.0  # this rank's total into the all-gather
 
     def work_per_step(self):
         # effective bandwidth: the 8 B/element a scan must move (read + write); with several ranks the extra
@@ -195,6 +217,12 @@ class Stencil(Workload):
             self.slab.run(self.graph_steps, self.overlap, graph=True)
         else:
             self.slab.step(self.overlap)
+
+    def compute_only_step(self):
+        self.slab.step(self.overlap, comm=False)
+
+    def bytes_exchanged_per_step(self):
+        return self.slab.halo_bytes_per_step()
 
     def work_per_step(self):
         return float(self.cells_local) * (self.graph_steps or self.slab.fuse)
@@ -297,6 +325,16 @@ class SpMV(Workload):
         return {"max_rel_err_vs_fp64": e, "iterated_max_rel_err_vs_fp64": ei, "iterated_steps": self.ITERATE_STEPS,
                 "pipeline_selftest": self.selftest, "deferred": self.defer and self.d.colsplit,
                 "check_passed": e <= REL_ERR_LIMIT and ei <= REL_ERR_LIMIT}
+
+    def compute_only_step(self):
+        self.d.comm = False
+        try:
+            self.y = self.d.step_padded(self.xp, defer_exchange=self.defer)
+        finally:
+            self.d.comm = True
+
+    def bytes_exchanged_per_step(self):
+        return self.d.bytes_sent_per_step()
 
     def work_per_step(self):
         return 2.0 * self.d.local_nnz

@@ -30,17 +30,22 @@ def global_reduce(x: torch.Tensor, ctx: Context, op: str = "sum") -> torch.Tenso
     return t.reshape(())
 
 
-def global_scan(x: torch.Tensor, ctx: Context, exclusive: bool = False) -> torch.Tensor:
+def global_scan(x: torch.Tensor, ctx: Context, exclusive: bool = False, comm: bool = True) -> torch.Tensor:
     """Prefix sum of the rank-ordered concatenation of every rank's x; returns this rank's slice.
 
     One rank: the single-pass look-back scan alone (8 B/element of HBM traffic). Several ranks: a local
     HBM-bound reduce (4 B/element), an all-gather of the per-rank totals over RCCL, and the scan seeded
-    with the sum of the lower ranks' totals (12 B/element, no second fix-up pass over the output)."""
+    with the sum of the lower ranks' totals (12 B/element, no second fix-up pass over the output).
+    comm=False (bench attribution only): the same kernels with the all-gather skipped (every rank's offset then
+    comes from its own total alone: NOT the global scan)."""
     if not ctx.distributed:
         return ops.scan(x, exclusive=exclusive)
     total = ops.reduce(x, "sum").reshape(1).float()
     totals = torch.empty(ctx.world, dtype=torch.float32, device=x.device)
-    dist.all_gather_into_tensor(totals, total)  # one collective into one tensor, no per-rank list
+    if comm:
+        dist.all_gather_into_tensor(totals, total)  # one collective into one tensor, no per-rank list
+    else:
+        totals.copy_(total.expand(ctx.world))
     before = totals[:ctx.rank].sum().reshape(1) if ctx.rank else torch.zeros(1, dtype=torch.float32, device=x.device)
     return ops.scan(x, exclusive=exclusive, init=before)
 

@@ -30,7 +30,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ..ops.sparse import CSR, SlicedCSR, powerlaw_csr_rows, powerlaw_row_ptr, spmv
+from ..ops.sparse import CSR, PackedLayoutUnavailable, SlicedCSR, powerlaw_csr_rows, powerlaw_row_ptr, spmv
 from ..ops.vector import gather_
 from .dist import Context
 
@@ -179,8 +179,8 @@ class DistributedSpMV:
             if self.sliced:
                 try:
                     sc = SlicedCSR(part, slices, head, balance, item_nnz, col_split=self.col_split)
-                except ValueError:  # 384-nnz items need the packed index stream: an automatic choice falls back to 512
-                    if not (auto_items and item_nnz == 384):
+                except PackedLayoutUnavailable:  # 384-nnz items need the packed index stream: an automatic choice
+                    if not (auto_items and item_nnz == 384):  # falls back to 512
                         raise
                     item_nnz = 512
                     sc = SlicedCSR(part, slices, head, balance, item_nnz, col_split=self.col_split)
@@ -200,6 +200,7 @@ class DistributedSpMV:
                 part = part.plan()
             self.parts.append((a, b, part))
         self._pending = [[], []]  # column split: the exchange works of the previous step's chunks 0 and 1
+        self.comm = True  # False (bench attribution only): every exchange skipped, the same kernels run
         # the send-buffer pack in the sliced product's combine epilogue (False: a separate gather pass, the round-4 form)
         self.fuse_pack = True
         # the two chunk-0-column product launches of a column-split step as ONE paired launch (False: two launches)
@@ -389,6 +390,8 @@ class DistributedSpMV:
         W, r = self.ctx.world, self.ctx.rank
         if self.send_idx[c].numel() and not packed:
             gather_(out, self.send_idx[c], self.sendbuf[c])
+        if not self.comm:
+            return []
         ins, outs, so = [], [], 0
         for q in range(W):
             ns = 0 if q == r else self.send_counts[c][q]
@@ -470,12 +473,24 @@ class DistributedSpMV:
             if not self.ctx.distributed:
                 continue
             if self.exchange == "allgather":
-                works.append(dist.all_gather_into_tensor(out[c * W * L:(c + 1) * W * L], self.send[c], async_op=True))
+                if self.comm:
+                    works.append(dist.all_gather_into_tensor(out[c * W * L:(c + 1) * W * L], self.send[c],
+                                                             async_op=True))
             else:
                 works += self._post_chunk(out, c, packed=send is not None)
         for w in works:
             w.wait()
         return out
+
+    def bytes_sent_per_step(self) -> float:
+        """Payload bytes this rank sends per step: its ghost entries for every peer (ghost), or its padded chunk to
+        every peer (allgather)."""
+        W, r = self.ctx.world, self.ctx.rank
+        if not self.ctx.distributed:
+            return 0.0
+        if self.exchange == "allgather":
+            return 4.0 * self.chunks * self.L * (W - 1)
+        return 4.0 * sum(cnt[q] for cnt in self.send_counts for q in range(W) if q != r)
 
     def step(self, x: torch.Tensor) -> torch.Tensor:
         """x (full, natural order, replicated) -> A x (full, natural order, replicated)."""

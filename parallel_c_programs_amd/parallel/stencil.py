@@ -125,22 +125,23 @@ class StencilSlab:
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(0, T))
             stencil5_step_(u, v, self.row0, self.n, self.k, row_range=(rows - T, rows))
 
-    def step(self, overlap: bool = True) -> None:
+    def step(self, overlap: bool = True, comm: bool = True) -> None:
         """Advances `fuse` time steps: at phase 0 one halo exchange overlapped with the interior launch, then the
-        edge launch; at later phases of a deep halo, one launch and no exchange."""
+        edge launch; at later phases of a deep halo, one launch and no exchange. comm=False (bench attribution only):
+        the same launches with the exchange skipped (the halo rows go stale: the grid is no longer checkable)."""
         ctx, rows, T = self.ctx, self.rows, self.fuse  # rows within T of a rank edge read the halo
         if not ctx.distributed:
             self._update(self.u, self.v)
         elif self.phase == 0:
             lo, hi = self._extent(0)
             if overlap and rows > 2 * T:
-                reqs = self._post_exchange()
+                reqs = self._post_exchange() if comm else []
                 self._update(self.u, self.v, (T, rows - T))
                 for r in reqs:
                     r.wait()
                 self._update_edges(self.u, self.v, lo, hi)
             else:
-                for r in self._post_exchange():
+                for r in (self._post_exchange() if comm else []):
                     r.wait()
                 self._update(self.u, self.v, (lo, hi))
         else:
@@ -148,6 +149,13 @@ class StencilSlab:
         self.u, self.v = self.v, self.u
         self.steps_done += T
         self.phase = (self.phase + 1) % self.m
+
+    def halo_bytes_per_step(self) -> float:
+        """Bytes this rank sends per step: `halo` rows of `cols` bf16 to each neighbour every m steps."""
+        if not self.ctx.distributed:
+            return 0.0
+        nbrs = (self.north >= 0) + (self.south >= 0)
+        return nbrs * self.halo * self.cols * self.u.element_size() / self.m
 
     # ---- checkpoint / resume (SURVEY §5.4): each rank writes its own slab; tensors only (weights_only load)
     def checkpoint(self, prefix: str) -> str:

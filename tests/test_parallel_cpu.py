@@ -474,6 +474,41 @@ def test_bench_gpus_2_launches_two_ranks_itself():
         assert out[f"{k}_device_ms_median"] > 0, k
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_n_gt_1_line_explains_itself(world):
+    """At N > 1 every distributed section also times its compute-only twin in the same job: the
+    line carries compute-only and exposed-communication ms, the per-rank spread of the median step time, the bytes
+    exchanged per step (per rank and in total) and the process group's size, with every check passing."""
+    r, out, nlines = _bench_cpu("--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-x6")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert nlines == 1 and out["checks_passed"] is True
+    assert out["comm_world_size"] == world and out["comm_backend"] == "gloo"
+    for sec in ("reduce_weak", "reduce_strong", "scan_weak", "scan_strong", "stencil", "spmv"):
+        assert out[f"{sec}_compute_only_ms"] > 0, sec
+        full = out[f"{sec}_ms_per_step"]
+        assert out[f"{sec}_comm_exposed_ms"] == pytest.approx(full - out[f"{sec}_compute_only_ms"], abs=2e-3), sec
+        assert 0 < out[f"{sec}_rank_step_ms_min"] <= out[f"{sec}_rank_step_ms_max"], sec
+        assert 0 < out[f"{sec}_compute_only_rank_ms_min"] <= out[f"{sec}_compute_only_rank_ms_max"], sec
+        per, tot = out[f"{sec}_bytes_exchanged_per_step"], out[f"{sec}_bytes_exchanged_per_step_total"]
+        assert 0 < per <= tot <= world * per, sec
+    assert out["reduce_weak_bytes_exchanged_per_step_total"] == 4.0 * world
+    # stencil: the interior ranks send `halo` bf16 rows of 256 columns to each of two neighbours every m steps
+    m, T = out["stencil_halo_mult"], out["stencil_updates_per_step"]
+    assert out["stencil_bytes_exchanged_per_step"] == (2 if world > 2 else 1) * m * T * 256 * 2 / m
+
+
+@pytest.mark.parametrize("section,key", [("stencil", "stencil_halo_selftest_bit_exact"),
+                                         ("spmv", "spmv_pipeline_selftest_bit_identical")])
+def test_bench_failed_selftest_fails_the_section(section, key):
+    """An N > 1 self-test that fails (deep halo / deferred SpMV pipeline) is a failed check of its section, not only
+    a field of the line: the run exits 1 with the key in "<section>_check_failed"."""
+    r, out, nlines = _bench_cpu("--gpus", "2", "--steps", "1", "--warmup", "0", "--sections", section,
+                                "--inject-fault", f"{section}:1:selftest")
+    assert r.returncode == 1, r.stderr[-3000:]
+    assert nlines == 1 and out["checks_passed"] is False and out[key] is False
+    assert out[f"{section}_check_failed"] == [key]
+
+
 def test_bench_world_size_mismatch_is_an_error():
     import subprocess
     import sys
