@@ -143,6 +143,10 @@ int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, 
 int pcmx_raycast_global_variant(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
                                 int image_dim, const float* cam12, float pixel_width, float step, int max_steps,
                                 int f64_color, int variant, hipStream_t s);
+long long pcmx_raycast_dr16_bytes(int dim);
+int pcmx_raycast_dr16_pack(const unsigned char* data, const unsigned char* region, int dim, void* dr, hipStream_t s);
+int pcmx_raycast_global_dr(const void* dr, int dim, unsigned char* image, int image_dim, const float* cam12,
+                           float pixel_width, float step, int max_steps, int f64_color, int variant, hipStream_t s);
 /* texture path: tex holds dim^3 * 16 + 16 bytes: per-voxel texels with the 2x2x2 footprint of data and region
  * (8-byte texels when every data value < 128, else 16-byte; the format flag is stored behind the texels),
  * dim <= 2048 */
@@ -228,6 +232,18 @@ int pcmx_unpack_halo(void* tile, int elem_bytes, int H, int W, int ld, const voi
 /* as pcmx_unpack_halo, and *changed (device int) is set to 1 when any halo cell takes a new value */
 int pcmx_unpack_halo_changed(void* tile, int elem_bytes, int H, int W, int ld, const void* buf, int mask, int* changed,
                              hipStream_t s);
+
+/* ---------------------------------------------------------------- grouped exchange on a dedicated RCCL communicator
+ * (comm/exchange_rccl.hip): per-peer float segments send[soff[q] .. + scnt[q]) -> peer q, recv[roff[q] .. + rcnt[q])
+ * <- peer q, on the communicator's stream, ordered after `compute` (event) and waited for by pcmx_xcomm_wait. */
+int pcmx_xcomm_id_bytes(void);
+int pcmx_xcomm_unique_id(void* out);
+int pcmx_xcomm_create(const void* id, int world, int rank, int device, void** out);
+int pcmx_xcomm_exchange(void* handle, int slot, const float* send, const long long* soff, const long long* scnt,
+                        float* recv, const long long* roff, const long long* rcnt, hipStream_t compute);
+int pcmx_xcomm_wait(void* handle, int slot, hipStream_t compute);
+int pcmx_xcomm_async_error(void* handle);
+int pcmx_xcomm_destroy(void* handle);
 
 #ifdef __cplusplus
 }

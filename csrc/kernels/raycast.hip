@@ -256,6 +256,318 @@ __global__ __launch_bounds__(64) void raycast_ref_batch_kernel(const unsigned ch
     image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
 }
 
+// ---- round 6: PAIR taps and GROUP-PER-RAY marching.
+// Pair taps: the two x taps of a row (x and xu = x or x + 1) come from ONE 8-byte buffer load at the 4-byte-aligned
+// address below x (bytes x and x + 1 both lie inside it); the descriptor spans the volume, so a load running past its
+// end reads 0 instead of faulting. 8 load instructions per sample (4 rows x 2 volumes) instead of 16 byte loads.
+struct Taps2 {
+    float rx, ry, rz;
+    unsigned char t[8];
+    bool ok;
+};
+__device__ __forceinline__ void taps_load2(float px, float py, float pz, __amdgpu_buffer_rsrc_t rs, int dim, Taps2& T) {
+    T.ok = px >= 0 && px < dim - 1 && py >= 0 && py < dim - 1 && pz >= 0 && pz < dim - 1;
+    if (!T.ok) return;
+    const int x = (int)floorf(px), y = (int)floorf(py), z = (int)floorf(pz);
+    const int xu = (int)ceilf(px), yu = (int)ceilf(py), zu = (int)ceilf(pz);
+    T.rx = px - x, T.ry = py - y, T.rz = pz - z;
+    const unsigned P = (unsigned)dim * (unsigned)dim;
+    const unsigned rows[4] = {(unsigned)z * P + (unsigned)y * dim, (unsigned)z * P + (unsigned)yu * dim,
+                              (unsigned)zu * P + (unsigned)y * dim, (unsigned)zu * P + (unsigned)yu * dim};
+    const unsigned sh = (unsigned)(x & 3) * 8u, dx = (unsigned)(xu - x) * 8u;
+    unsigned long long w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        w[k] = __builtin_bit_cast(unsigned long long,
+                                  __builtin_amdgcn_raw_buffer_load_b64(rs, rows[k] + (unsigned)(x & ~3), 0, 0));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        T.t[2 * k] = (unsigned char)(w[k] >> sh);
+        T.t[2 * k + 1] = (unsigned char)(w[k] >> (sh + dx));
+    }
+}
+__device__ __forceinline__ float taps2_value(const Taps2& T) {  // value_at_ref's arithmetic, operation for operation
+    if (!T.ok) return 0.f;
+    const float rx = T.rx, ry = T.ry, rz = T.rz;
+    const float a0 = rx * T.t[0] + (1 - rx) * T.t[1];
+    const float a1 = rx * T.t[2] + (1 - rx) * T.t[3];
+    const float a2 = rx * T.t[4] + (1 - rx) * T.t[5];
+    const float a3 = rx * T.t[6] + (1 - rx) * T.t[7];
+    const float b0 = ry * a0 + (1 - ry) * a1;
+    const float b1 = ry * a2 + (1 - ry) * a3;
+    return rz * b0 + (1 - rz) * b1;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t volume_rsrc(const unsigned char* d, int dim) {
+    const long long bytes = (long long)dim * dim * dim;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(d), (short)0,
+                                             (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+
+// The reference's ray set-up for pixel (px, py), operation for operation (raycast.cu:352-357).
+__device__ __forceinline__ void ray_setup(const Cam& c, int px, int py, int image_dim, float (&pos)[3], float& sx,
+                                          float& sy, float& sz) {
+    const int half = image_dim / 2;
+    const int x = px - half, y = py - half;
+    float ray[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float sc = c.cam[k] + c.fwd[k];
+        const float t = (sc + c.right[k] * (x * c.pw)) + c.up[k] * (y * c.pw);
+        ray[k] = t + c.cam[k] * -1;
+        pos[k] = c.cam[k];
+    }
+    const float l = (float)sqrt((double)(ray[0] * ray[0] + ray[1] * ray[1] + ray[2] * ray[2]));
+    ray[0] /= l, ray[1] /= l, ray[2] /= l;
+    sx = ray[0] * c.step, sy = ray[1] * c.step, sz = ray[2] * c.step;
+}
+
+// The batch caster with pair taps (variant 4): otherwise raycast_ref_batch_kernel.
+template <bool F64COLOR, int B>
+__global__ __launch_bounds__(64) void raycast_ref_batch2_kernel(const unsigned char* __restrict__ data,
+                                                                const unsigned char* __restrict__ region, int dim,
+                                                                unsigned char* __restrict__ image, int image_dim, Cam c) {
+    const int px = blockIdx.x * 8 + (threadIdx.x & 7);
+    const int py = blockIdx.y * 8 + (threadIdx.x >> 3);
+    if (px >= image_dim || py >= image_dim) return;
+    const auto rd = volume_rsrc(data, dim), rr = volume_rsrc(region, dim);
+    float pos[3], sx, sy, sz;
+    ray_setup(c, px, py, image_dim, pos, sx, sy, sz);
+    const float hi = (float)(dim - 1);
+    int i = 0;
+    float color = 0.f;
+    while (i < c.max_steps) {
+        const float nx = pos[0] + sx, ny = pos[1] + sy, nz = pos[2] + sz;
+        if (in_box(nx, ny, nz, hi)) break;
+        ++i;
+        pos[0] = nx, pos[1] = ny, pos[2] = nz;
+    }
+    bool done = i >= c.max_steps;
+    while (!done) {
+        float q[B][3];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            pos[0] = pos[0] + sx, pos[1] = pos[1] + sy, pos[2] = pos[2] + sz;
+            q[b][0] = pos[0], q[b][1] = pos[1], q[b][2] = pos[2];
+        }
+        Taps2 R[B], D[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            taps_load2(q[b][0], q[b][1], q[b][2], rr, dim, R[b]);
+            taps_load2(q[b][0], q[b][1], q[b][2], rd, dim, D[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (!done) {
+                if (!(color < 255 && i < c.max_steps)) {
+                    done = true;
+                } else {
+                    ++i;
+                    if (!in_box(q[b][0], q[b][1], q[b][2], hi)) {
+                        done = true;
+                    } else {
+                        const int r = (int)taps2_value(R[b]);
+                        const float v = taps2_value(D[b]);
+                        if constexpr (F64COLOR)
+                            color = (float)((double)color + (double)v * (0.01 + r));
+                        else
+                            color += v * (0.01f + r);
+                    }
+                }
+            }
+        }
+    }
+    image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
+}
+
+// DR16 layout: data and region interleaved per voxel (u16 = data | region << 8, dr16_pack_kernel), so ONE 8-byte load
+// at the 4-byte-aligned address below voxel x of a row holds voxels x and x + 1 of BOTH volumes: 4 load instructions
+// per sample. The same bytes, so the same arithmetic and bit-identical images.
+__global__ __launch_bounds__(256) void dr16_pack_kernel(const unsigned char* __restrict__ data,
+                                                        const unsigned char* __restrict__ region,
+                                                        unsigned* __restrict__ out, long long n4) {
+    // 4 voxels per thread: one u32 of each volume in, two u32 of interleaved pairs out
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+        const unsigned d = __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(data) + i);
+        const unsigned r = __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(region) + i);
+        const unsigned lo = (d & 0xffu) | ((r & 0xffu) << 8) | ((d & 0xff00u) << 8) | ((r & 0xff00u) << 16);
+        const unsigned hi = ((d >> 16) & 0xffu) | (((r >> 16) & 0xffu) << 8) | ((d >> 24) << 16) | ((r >> 24) << 24);
+        reinterpret_cast<uint2*>(out)[i] = make_uint2(lo, hi);
+    }
+}
+
+__device__ __forceinline__ void taps_load_dr(float px, float py, float pz, __amdgpu_buffer_rsrc_t rs, int dim,
+                                             Taps2& R, Taps2& D) {
+    D.ok = px >= 0 && px < dim - 1 && py >= 0 && py < dim - 1 && pz >= 0 && pz < dim - 1;
+    R.ok = D.ok;
+    if (!D.ok) return;
+    const int x = (int)floorf(px), y = (int)floorf(py), z = (int)floorf(pz);
+    const int xu = (int)ceilf(px), yu = (int)ceilf(py), zu = (int)ceilf(pz);
+    D.rx = R.rx = px - x, D.ry = R.ry = py - y, D.rz = R.rz = pz - z;
+    const unsigned P = (unsigned)dim * (unsigned)dim;
+    const unsigned rows[4] = {(unsigned)z * P + (unsigned)y * dim, (unsigned)z * P + (unsigned)yu * dim,
+                              (unsigned)zu * P + (unsigned)y * dim, (unsigned)zu * P + (unsigned)yu * dim};
+    // byte offset of voxel x = 2x; the 4-aligned 8-byte window below it holds voxels x and x + 1
+    const unsigned sh = (unsigned)(x & 1) * 16u, dx = (unsigned)(xu - x) * 16u;
+    unsigned long long w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        w[k] = __builtin_bit_cast(unsigned long long,
+                                  __builtin_amdgcn_raw_buffer_load_b64(rs, 2u * (rows[k] + (unsigned)(x & ~1)), 0, 0));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const unsigned a = (unsigned)(w[k] >> sh), b = (unsigned)(w[k] >> (sh + dx));
+        D.t[2 * k] = (unsigned char)a, R.t[2 * k] = (unsigned char)(a >> 8);
+        D.t[2 * k + 1] = (unsigned char)b, R.t[2 * k + 1] = (unsigned char)(b >> 8);
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dr16_rsrc(const unsigned short* d, int dim) {
+    const long long bytes = 2LL * dim * dim * dim;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(d), (short)0,
+                                             (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+
+// The batch caster on the DR16 layout (variant 9): per-lane rays, B steps' samples in flight.
+template <bool F64COLOR, int B>
+__global__ __launch_bounds__(64) void raycast_dr_batch_kernel(const unsigned short* __restrict__ dr, int dim,
+                                                              unsigned char* __restrict__ image, int image_dim, Cam c) {
+    const int px = blockIdx.x * 8 + (threadIdx.x & 7);
+    const int py = blockIdx.y * 8 + (threadIdx.x >> 3);
+    if (px >= image_dim || py >= image_dim) return;
+    const auto rs = dr16_rsrc(dr, dim);
+    float pos[3], sx, sy, sz;
+    ray_setup(c, px, py, image_dim, pos, sx, sy, sz);
+    const float hi = (float)(dim - 1);
+    int i = 0;
+    float color = 0.f;
+    while (i < c.max_steps) {
+        const float nx = pos[0] + sx, ny = pos[1] + sy, nz = pos[2] + sz;
+        if (in_box(nx, ny, nz, hi)) break;
+        ++i;
+        pos[0] = nx, pos[1] = ny, pos[2] = nz;
+    }
+    bool done = i >= c.max_steps;
+    while (!done) {
+        float q[B][3];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            pos[0] = pos[0] + sx, pos[1] = pos[1] + sy, pos[2] = pos[2] + sz;
+            q[b][0] = pos[0], q[b][1] = pos[1], q[b][2] = pos[2];
+        }
+        Taps2 R[B], D[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) taps_load_dr(q[b][0], q[b][1], q[b][2], rs, dim, R[b], D[b]);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (!done) {
+                if (!(color < 255 && i < c.max_steps)) {
+                    done = true;
+                } else {
+                    ++i;
+                    if (!in_box(q[b][0], q[b][1], q[b][2], hi)) {
+                        done = true;
+                    } else {
+                        const int r = (int)taps2_value(R[b]);
+                        const float v = taps2_value(D[b]);
+                        if constexpr (F64COLOR)
+                            color = (float)((double)color + (double)v * (0.01 + r));
+                        else
+                            color += v * (0.01f + r);
+                    }
+                }
+            }
+        }
+    }
+    image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
+}
+
+// GROUP-PER-RAY caster (variants 5-7): G consecutive lanes march ONE ray, G steps at a time. Every lane of the group
+// replays the ray's f32 position adds (the same sequence as the serial caster, so positions stay bit-exact) and keeps
+// the position of ITS step: lane j of the group samples steps k + j + 1 of each round of G. Each lane computes its
+// step's term (v * (0.01 + r), in f32 or f64 as the colour mode wants) in parallel; the terms go through LDS and every
+// lane of the group adds them to the colour in step order, so the colour's roundings are exactly the serial
+// caster's. The loop stops after a round in which the colour reached 255 (later terms are >= 0, and the output clamps
+// to 255 either way) or the ray left the volume's box (later samples read 0; adding 0 leaves the colour unchanged).
+// A small image then fills the chip: 64^2 rays at G = 64 are 4096 waves instead of 64.
+template <bool F64COLOR, int G, bool DR>
+__global__ __launch_bounds__(256) void raycast_ref_group_kernel(const unsigned char* __restrict__ data,
+                                                                const unsigned char* __restrict__ region,
+                                                                const unsigned short* __restrict__ dr, int dim,
+                                                                unsigned char* __restrict__ image, int image_dim, Cam c) {
+    using Term = typename std::conditional<F64COLOR, double, float>::type;
+    __shared__ Term s_term[256];
+    const int lane = threadIdx.x & 63, sub = lane & (G - 1);
+    const int ray = (int)((blockIdx.x * 256u + threadIdx.x) / G);
+    const int n_rays = image_dim * image_dim;
+    bool done = ray >= n_rays;  // group-uniform, as everything below that decides control flow
+    const int px = done ? 0 : ray % image_dim, py = done ? 0 : ray / image_dim;
+    const auto rd = volume_rsrc(data, dim), rr = volume_rsrc(region, dim);
+    const auto rs = dr16_rsrc(dr, dim);
+    float pos[3], sx, sy, sz;
+    ray_setup(c, px, py, image_dim, pos, sx, sy, sz);
+    const float hi = (float)(dim - 1);
+    int i = 0;
+    if (!done) {
+        while (i < c.max_steps) {  // outside the box a sample adds exactly 0: adds only up to the first sample inside
+            const float nx = pos[0] + sx, ny = pos[1] + sy, nz = pos[2] + sz;
+            if (in_box(nx, ny, nz, hi)) break;
+            ++i;
+            pos[0] = nx, pos[1] = ny, pos[2] = nz;
+        }
+        done = i >= c.max_steps;
+    }
+    float color = 0.f;
+    const int g0 = threadIdx.x & ~(G - 1);  // the group's first slot in s_term
+    const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (lane & ~(G - 1));
+    while (__ballot(!done) != 0ull) {
+        if (!done) {
+            float q0 = 0.f, q1 = 0.f, q2 = 0.f;
+#pragma unroll 8
+            for (int b = 0; b < G; ++b) {
+                pos[0] = pos[0] + sx, pos[1] = pos[1] + sy, pos[2] = pos[2] + sz;
+                if (sub == b) q0 = pos[0], q1 = pos[1], q2 = pos[2];
+            }
+            const bool valid = i + sub + 1 <= c.max_steps;
+            Taps2 R, D;
+            if (valid) {
+                if constexpr (DR) {
+                    taps_load_dr(q0, q1, q2, rs, dim, R, D);
+                } else {
+                    taps_load2(q0, q1, q2, rr, dim, R);
+                    taps_load2(q0, q1, q2, rd, dim, D);
+                }
+            }
+            Term t = 0;
+            if (valid && D.ok) {
+                const int r = (int)taps2_value(R);
+                const float v = taps2_value(D);
+                if constexpr (F64COLOR)
+                    t = (double)v * (0.01 + r);
+                else
+                    t = v * (0.01f + r);
+            }
+            s_term[threadIdx.x] = t;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 8
+            for (int b = 0; b < G; ++b) {
+                if constexpr (F64COLOR)
+                    color = (float)((double)color + s_term[g0 + b]);
+                else
+                    color = color + s_term[g0 + b];
+            }
+            __builtin_amdgcn_wave_barrier();  // the slots are rewritten next round
+            const bool left = valid && !in_box(q0, q1, q2, hi);
+            i += G;
+            done = color >= 255 || i >= c.max_steps || (__ballot(left) & gmask) != 0ull;
+        }
+    }
+    if (ray < n_rays && sub == 0) image[py * image_dim + px] = (unsigned char)(color > 255 ? 255.f : color);
+}
+
 // value_at_ref on a z-slab buffer whose plane 0 is global plane zoff (identical arithmetic)
 __device__ __forceinline__ float value_at_slab(float px, float py, float pz, const unsigned char* __restrict__ d, int dim,
                                               int zoff) {
@@ -858,6 +1170,8 @@ __global__ __launch_bounds__(256) void raycast_tex_kernel(const void* __restrict
         raycast_tex_march<D, false, SEG>(tex, dim, image, image_dim, c, s_part);
 }
 
+constexpr long long kRaycastSmallRays = 1LL << 16;  // production rule of pcmx_raycast_global
+
 Cam make_cam(const float* cam12, float pw, float step, int max_steps) {
     Cam c;
     for (int k = 0; k < 3; ++k) {
@@ -880,22 +1194,80 @@ extern "C" int pcmx_volume_gen_u8(unsigned char* data, int dim, unsigned seed, h
 }
 
 // cam12 = camera[3], forward[3], right[3], up[3] (host array; already normalised, see pcmx_default_camera)
+// Production global caster (round 6): images of up to 2^16 rays march one ray per 16-lane group (variant 6: a 64^2
+// image is 1024 waves instead of 64); larger images interleave data and region into the DR16 layout first (one 8-byte
+// load per row and sample for both volumes) and march one ray per 4-lane group (variant 11). Measured on one MI355X
+// (scripts/raycast_global_lab.py, profiles/r6_raycast/; every image bit-identical to the serial caster's): 64^2
+// 1.98 -> 0.47 ms, 512^2 5.2 -> 2.5 ms (pack included). The DR16 buffer comes from the stream-ordered allocator here
+// (the torch op passes its own, pcmx_raycast_global_dr); a failed allocation falls back to variant 4.
 extern "C" int pcmx_raycast_global(const unsigned char* data, const unsigned char* region, int dim, unsigned char* image,
                                    int image_dim, const float* cam12, float pixel_width, float step, int max_steps,
                                    int f64_color, hipStream_t s) {
     if (dim <= 1 || image_dim <= 0) return -1;
+    const long long n_rays = (long long)image_dim * image_dim;
+    if (n_rays > kRaycastSmallRays && dim % 4 == 0) {
+        static bool pool_kept = false;  // keep freed async allocations in the pool (no OS round trip per frame)
+        int dev = 0;
+        if (!pool_kept && hipGetDevice(&dev) == hipSuccess) {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                unsigned long long keep = ~0ull;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            }
+            pool_kept = true;
+        }
+        void* dr = nullptr;
+        if (hipMallocAsync(&dr, (size_t)pcmx_raycast_dr16_bytes(dim), s) == hipSuccess) {
+            int rc = pcmx_raycast_dr16_pack(data, region, dim, dr, s);
+            if (rc == 0)
+                rc = pcmx_raycast_global_dr(dr, dim, image, image_dim, cam12, pixel_width, step, max_steps, f64_color, 11, s);
+            const hipError_t fe = hipFreeAsync(dr, s);
+            return rc ? rc : (int)fe;
+        }
+        (void)hipGetLastError();
+        return pcmx_raycast_global_variant(data, region, dim, image, image_dim, cam12, pixel_width, step, max_steps,
+                                           f64_color, 4, s);
+    }
     return pcmx_raycast_global_variant(data, region, dim, image, image_dim, cam12, pixel_width, step, max_steps,
-                                       f64_color, 0, s);
+                                       f64_color, 6, s);
 }
 
-// variant 0 (production): 8x8-pixel one-wave tiles, the samples of 8 steps in flight (raycast_ref_batch_kernel; 16 on
-// images of more than 2^16 rays); 1: the round-4 caster (16x16 tiles, one step in flight); 2 / 3: batch kernel with 4 /
-// 16 steps in flight (lab). Identical images.
+// variant 0: the round-5 caster, 8x8-pixel one-wave tiles, the samples of 8 steps in flight (raycast_ref_batch_kernel; 16
+// on images of more than 2^16 rays); 1: the round-4 caster (16x16 tiles, one step in flight); 2 / 3: batch kernel with
+// 4 / 16 steps in flight; 4: variant 0 with pair taps; 5 / 6 / 7 / 8: one ray per 64 / 16 / 8 / 4-lane group; 9 / 10 /
+// 11: DR16 layout (pcmx_raycast_global_dr). Identical images. The production choice is pcmx_raycast_global's.
 extern "C" int pcmx_raycast_global_variant(const unsigned char* data, const unsigned char* region, int dim,
                                            unsigned char* image, int image_dim, const float* cam12, float pixel_width,
                                            float step, int max_steps, int f64_color, int variant, hipStream_t s) {
-    if (dim <= 1 || image_dim <= 0 || variant < 0 || variant > 3) return -1;
+    if (dim <= 1 || image_dim <= 0 || variant < 0 || variant > 11) return -1;
     const Cam c = make_cam(cam12, pixel_width, step, max_steps);
+    const long long n_rays = (long long)image_dim * image_dim;
+    if (variant >= 5 && variant <= 8) {  // group-per-ray: G lanes per ray, 256 / G rays per block
+        const int G = variant == 5 ? 64 : variant == 6 ? 16 : variant == 7 ? 8 : 4;
+        const unsigned blocks = (unsigned)((n_rays * G + 255) / 256);
+#define PCMX_RAYCAST_G(GG)                                                                                                   \
+    (f64_color ? raycast_ref_group_kernel<true, GG, false><<<blocks, 256, 0, s>>>(data, region, nullptr, dim, image,         \
+                                                                                 image_dim, c)                             \
+               : raycast_ref_group_kernel<false, GG, false><<<blocks, 256, 0, s>>>(data, region, nullptr, dim, image,        \
+                                                                                  image_dim, c))
+        if (G == 64) PCMX_RAYCAST_G(64);
+        else if (G == 16) PCMX_RAYCAST_G(16);
+        else if (G == 8) PCMX_RAYCAST_G(8);
+        else PCMX_RAYCAST_G(4);
+#undef PCMX_RAYCAST_G
+        return (int)hipGetLastError();
+    }
+    if (variant >= 9) return PCMX_ERR_ARG;  // DR16 variants: pcmx_raycast_global_dr
+    if (variant == 4) {  // batch caster with pair taps
+        const dim3 grid((image_dim + 7) / 8, (image_dim + 7) / 8);
+        if (n_rays > (1 << 16))
+            f64_color ? raycast_ref_batch2_kernel<true, 16><<<grid, 64, 0, s>>>(data, region, dim, image, image_dim, c)
+                      : raycast_ref_batch2_kernel<false, 16><<<grid, 64, 0, s>>>(data, region, dim, image, image_dim, c);
+        else
+            f64_color ? raycast_ref_batch2_kernel<true, 8><<<grid, 64, 0, s>>>(data, region, dim, image, image_dim, c)
+                      : raycast_ref_batch2_kernel<false, 8><<<grid, 64, 0, s>>>(data, region, dim, image, image_dim, c);
+        return (int)hipGetLastError();
+    }
     if (variant == 1) {
         const dim3 grid((image_dim + 15) / 16, (image_dim + 15) / 16);
         if (f64_color)
@@ -915,6 +1287,49 @@ extern "C" int pcmx_raycast_global_variant(const unsigned char* data, const unsi
     else if (b == 8) PCMX_RAYCAST_B(8);
     else PCMX_RAYCAST_B(16);
 #undef PCMX_RAYCAST_B
+    return (int)hipGetLastError();
+}
+
+extern "C" long long pcmx_raycast_dr16_bytes(int dim) { return dim > 1 ? 2LL * dim * dim * dim : 0; }
+
+// Interleaves data and region into the DR16 layout (dim^3 u16; dim % 4 == 0 and 4-B aligned volumes).
+extern "C" int pcmx_raycast_dr16_pack(const unsigned char* data, const unsigned char* region, int dim, void* dr,
+                                      hipStream_t s) {
+    if (dim <= 1 || dim % 4 || !dr || ((uintptr_t)data & 3u) || ((uintptr_t)region & 3u) || ((uintptr_t)dr & 7u))
+        return PCMX_ERR_ARG;
+    const long long n4 = (long long)dim * dim * dim / 4;
+    const long long blocks = (n4 + 255) / 256 < 16384 ? (n4 + 255) / 256 : 16384;
+    dr16_pack_kernel<<<(int)blocks, 256, 0, s>>>(data, region, reinterpret_cast<unsigned*>(dr), n4);
+    return (int)hipGetLastError();
+}
+
+// Global caster on a DR16 volume (pcmx_raycast_dr16_pack): variant 9 = per-lane rays (batch), 10 / 11 = group per ray
+// with 16 / 4 lanes. Bit-identical to pcmx_raycast_global_variant.
+extern "C" int pcmx_raycast_global_dr(const void* dr, int dim, unsigned char* image, int image_dim, const float* cam12,
+                                      float pixel_width, float step, int max_steps, int f64_color, int variant,
+                                      hipStream_t s) {
+    if (dim <= 1 || image_dim <= 0 || !dr || variant < 9 || variant > 11) return PCMX_ERR_ARG;
+    const Cam c = make_cam(cam12, pixel_width, step, max_steps);
+    const unsigned short* d16 = reinterpret_cast<const unsigned short*>(dr);
+    const long long n_rays = (long long)image_dim * image_dim;
+    if (variant == 9) {
+        const dim3 grid((image_dim + 7) / 8, (image_dim + 7) / 8);
+        if (n_rays > (1 << 16))
+            f64_color ? raycast_dr_batch_kernel<true, 16><<<grid, 64, 0, s>>>(d16, dim, image, image_dim, c)
+                      : raycast_dr_batch_kernel<false, 16><<<grid, 64, 0, s>>>(d16, dim, image, image_dim, c);
+        else
+            f64_color ? raycast_dr_batch_kernel<true, 8><<<grid, 64, 0, s>>>(d16, dim, image, image_dim, c)
+                      : raycast_dr_batch_kernel<false, 8><<<grid, 64, 0, s>>>(d16, dim, image, image_dim, c);
+        return (int)hipGetLastError();
+    }
+    const int G = variant == 10 ? 16 : 4;
+    const unsigned blocks = (unsigned)((n_rays * G + 255) / 256);
+    if (G == 16)
+        f64_color ? raycast_ref_group_kernel<true, 16, true><<<blocks, 256, 0, s>>>(nullptr, nullptr, d16, dim, image, image_dim, c)
+                  : raycast_ref_group_kernel<false, 16, true><<<blocks, 256, 0, s>>>(nullptr, nullptr, d16, dim, image, image_dim, c);
+    else
+        f64_color ? raycast_ref_group_kernel<true, 4, true><<<blocks, 256, 0, s>>>(nullptr, nullptr, d16, dim, image, image_dim, c)
+                  : raycast_ref_group_kernel<false, 4, true><<<blocks, 256, 0, s>>>(nullptr, nullptr, d16, dim, image, image_dim, c);
     return (int)hipGetLastError();
 }
 

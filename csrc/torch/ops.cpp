@@ -387,6 +387,22 @@ at::Tensor raycast_global(const at::Tensor& data, const at::Tensor& region, int6
     const at::DeviceGuard g(data.device());
     auto img = at::empty({image_dim, image_dim}, data.options());
     auto c = cam_vec(cam12);
+    if (variant < 0) {  // the production rule (pcmx_raycast_global): 16-lane groups, DR16 + 4-lane groups above 2^16 rays
+        variant = (image_dim * image_dim > (1 << 16) && data.size(0) % 4 == 0) ? 11 : 6;
+    }
+    if (variant >= 9) {  // the DR16 layout (data and region interleaved per voxel), packed on this call
+        const int dim = (int)data.size(0);
+        TORCH_CHECK(dim % 4 == 0, "raycast_global: DR16 variants need dim % 4 == 0");
+        auto dr = at::empty({pcmx_raycast_dr16_bytes(dim)}, data.options());
+        check_rc(pcmx_raycast_dr16_pack(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), dim, dr.data_ptr(),
+                                        cur_stream(data)),
+                 "raycast_dr16_pack");
+        check_rc(pcmx_raycast_global_dr(dr.data_ptr(), dim, img.data_ptr<uint8_t>(), (int)image_dim, c.data(),
+                                        (float)pixel_width, (float)step, (int)max_steps, f64_color ? 1 : 0, (int)variant,
+                                        cur_stream(data)),
+                 "raycast_global_dr");
+        return img;
+    }
     check_rc(pcmx_raycast_global_variant(data.data_ptr<uint8_t>(), region.data_ptr<uint8_t>(), (int)data.size(0),
                                          img.data_ptr<uint8_t>(), (int)image_dim, c.data(), (float)pixel_width, (float)step,
                                          (int)max_steps, f64_color ? 1 : 0, (int)variant, cur_stream(data)),
@@ -742,7 +758,7 @@ TORCH_LIBRARY(pcmx, m) {
     m.def("volume_gen_(Tensor(a!) data, int seed) -> Tensor(a!)");
     m.def("volume_gen_slab_(Tensor(a!) data, int z_first, int seed) -> Tensor(a!)");
     m.def("raycast_slab_(Tensor data, Tensor region, int z0, Tensor(a!) state, bool init, bool bottom, int image_dim, float[] cam12, float pixel_width, float step, int max_steps) -> Tensor");
-    m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True, int variant=0) -> Tensor");
+    m.def("raycast_global(Tensor data, Tensor region, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, bool f64_color=True, int variant=-1) -> Tensor");
     m.def("brick_pack(Tensor data, Tensor region) -> Tensor");
     m.def("raycast_bricked(Tensor tex, int image_dim, float[] cam12, float pixel_width, float step, int max_steps, int batch=0, int segments=0) -> Tensor");
     m.def("stencil5_(Tensor u, Tensor(a!) out, int r0, int r1, int global_row0, int global_rows, float k) -> ()");
@@ -794,9 +810,54 @@ TORCH_LIBRARY_IMPL(pcmx, CUDA, m) {
     m.impl("unpack_halo_", unpack_halo_);
 }
 
+// ---------------------------------------------------------------- grouped exchange (dedicated RCCL communicator)
+// Plain pybind functions (no torch dispatcher on the per-step path): parallel/dist.py NativeExchange.
+pybind11::bytes xcomm_unique_id() {
+    std::string id((size_t)pcmx_xcomm_id_bytes(), '\0');
+    check_rc(pcmx_xcomm_unique_id(id.data()), "xcomm_unique_id");
+    return pybind11::bytes(id);
+}
+
+int64_t xcomm_create(const std::string& id, int64_t world, int64_t rank, int64_t device) {
+    TORCH_CHECK((int)id.size() == pcmx_xcomm_id_bytes(), "xcomm_create: unique id of ", pcmx_xcomm_id_bytes(), " bytes");
+    void* h = nullptr;
+    check_rc(pcmx_xcomm_create(id.data(), (int)world, (int)rank, (int)device, &h), "xcomm_create");
+    return reinterpret_cast<int64_t>(h);
+}
+
+void xcomm_exchange(int64_t h, int64_t slot, const at::Tensor& send, const std::vector<int64_t>& soff,
+                    const std::vector<int64_t>& scnt, at::Tensor recv, const std::vector<int64_t>& roff,
+                    const std::vector<int64_t>& rcnt) {
+    check_gpu(send, "send", at::kFloat), check_gpu(recv, "recv", at::kFloat);
+    TORCH_CHECK(send.is_contiguous() && recv.is_contiguous() && send.device() == recv.device(), "xcomm_exchange: buffers");
+    const size_t W = soff.size();
+    TORCH_CHECK(W > 0 && scnt.size() == W && roff.size() == W && rcnt.size() == W, "xcomm_exchange: one entry per rank");
+    for (size_t q = 0; q < W; ++q) {  // every segment inside its buffer (host-side, no device data involved)
+        TORCH_CHECK(scnt[q] >= 0 && soff[q] >= 0 && soff[q] + scnt[q] <= send.numel(), "xcomm_exchange: send segment ", q);
+        TORCH_CHECK(rcnt[q] >= 0 && roff[q] >= 0 && roff[q] + rcnt[q] <= recv.numel(), "xcomm_exchange: recv segment ", q);
+    }
+    check_rc(pcmx_xcomm_exchange(reinterpret_cast<void*>(h), (int)slot, send.data_ptr<float>(),
+                                 reinterpret_cast<const long long*>(soff.data()), reinterpret_cast<const long long*>(scnt.data()),
+                                 recv.data_ptr<float>(), reinterpret_cast<const long long*>(roff.data()),
+                                 reinterpret_cast<const long long*>(rcnt.data()), cur_stream(recv)),
+             "xcomm_exchange");
+}
+
+void xcomm_wait(int64_t h, int64_t slot, int64_t device) {
+    check_rc(pcmx_xcomm_wait(reinterpret_cast<void*>(h), (int)slot, c10::hip::getCurrentHIPStream((int)device).stream()),
+             "xcomm_wait");
+}
+
 PYBIND11_MODULE(_C, mod) {
     mod.doc() = "pcmx MI355X kernels (ops live under torch.ops.pcmx)";
     mod.def("device_count", []() { return pcmx_device_count(); });
     mod.def("spmv_csr_plan", &spmv_csr_plan, "CSR-adaptive work items from a CPU int64 row_ptr",
             pybind11::arg("row_ptr"), pybind11::arg("item_nnz") = 1024);
+    mod.def("xcomm_unique_id", &xcomm_unique_id, "ncclUniqueId of a new dedicated RCCL communicator (rank 0)");
+    mod.def("xcomm_create", &xcomm_create, "join the dedicated RCCL communicator: handle");
+    mod.def("xcomm_exchange", &xcomm_exchange, "grouped per-peer send/recv of float segments, ordered after the "
+            "current stream (slot: one exchange in flight)");
+    mod.def("xcomm_wait", &xcomm_wait, "the current stream of `device` waits for the slot's exchange");
+    mod.def("xcomm_async_error", [](int64_t h) { return pcmx_xcomm_async_error(reinterpret_cast<void*>(h)); });
+    mod.def("xcomm_destroy", [](int64_t h) { return pcmx_xcomm_destroy(reinterpret_cast<void*>(h)); });
 }

@@ -182,7 +182,7 @@ def default_camera(image_dim: int) -> Camera:
 
 
 def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, method: str = "global",
-            cam: Camera | None = None, batch: int = 0, segments: int = 0, variant: int = 0) -> torch.Tensor:
+            cam: Camera | None = None, batch: int = 0, segments: int = 0, variant: int = -1) -> torch.Tensor:
     """Render the volume (ray marching, trilinear sampling of data and region).
 
     method: "global" — bit-compatible with the reference's serial/global-memory caster (f64 colour update);
@@ -191,8 +191,10 @@ def raycast(data: torch.Tensor, region: torch.Tensor, image_dim: int = 512, meth
             `batch` = its march steps per prefetch batch (1, 4, 8, 16: same image; 0 = 16, the fastest);
             `segments` = waves sharing one ray patch, each marching a contiguous share of the steps (1, 2, 4;
             0 = the fastest; partial colours are composed in ray order, so images agree up to f32 rounding);
-            `variant` (global methods) = caster variant: 0 the production caster (8 steps' samples in flight), 1 the
-            one-step-in-flight form, 2 / 3 4 / 16 steps in flight (lab; identical images).
+            `variant` (global methods) = caster variant: -1 the production rule (one ray per 16-lane group up to 2^16
+            rays, else the DR16 interleaved volume with one ray per 4-lane group), 0 the round-5 caster (8 steps'
+            samples in flight per lane), 1 the one-step-in-flight form, 2 / 3 4 / 16 steps in flight, 4 pair taps,
+            5-8 one ray per 64 / 16 / 8 / 4 lanes, 9-11 DR16 layout (lab; identical images).
     """
     cam = cam or default_camera(image_dim)
     if not data.is_cuda:

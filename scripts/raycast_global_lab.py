@@ -13,6 +13,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from parallel_c_programs_amd import ops  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+# round 6: 4 = batch caster with pair taps, 5 / 6 / 7 / 8 = group-per-ray caster with 64 / 16 / 8 / 4 lanes per ray
+VARIANTS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 0, 2, 3, 1, 0]
+GROW = len(sys.argv) <= 3 or sys.argv[3] != "nogrow"
 dev = torch.device("cuda", 0)
 
 
@@ -29,15 +32,20 @@ def timed(fn, n=reps):
 
 
 vol = ops.create_volume(512, device=dev, seed=0)
-for method in ("naive", "tiled", "naive", "tiled"):
+for method in (("naive", "tiled", "naive", "tiled") if GROW else ("tiled",)):
     ms, (reg, launches) = timed(lambda: ops.region3d(vol, threshold=1, method=method))
     print(f"grow {method:5s} {ms:8.3f} ms per grow ({launches} launches)  voxels {int((reg != 0).sum())}", flush=True)
 region = (reg != 0).to(torch.uint8)
 for image_dim in (64, 512):
     ref = ops.raycast(vol, region, image_dim, method="global", variant=1)
-    for v in (1, 0, 2, 3, 1, 0):
+    for v in VARIANTS:
         ms, img = timed(lambda: ops.raycast(vol, region, image_dim, method="global", variant=v))
         print(f"raycast global {image_dim:3d}^2 variant {v}: {ms:8.3f} ms  sum {int(img.long().sum())}"
               f"{'' if torch.equal(img, ref) else '  MISMATCH'}", flush=True)
+    ref32 = ops.raycast(vol, region, image_dim, method="global_f32", variant=1)
+    for v in sorted(set(VARIANTS)):
+        ms, img = timed(lambda: ops.raycast(vol, region, image_dim, method="global_f32", variant=v))
+        print(f"raycast global_f32 {image_dim:3d}^2 variant {v}: {ms:8.3f} ms  sum {int(img.long().sum())}"
+              f"{'' if torch.equal(img, ref32) else '  MISMATCH'}", flush=True)
     ms, img = timed(lambda: ops.raycast(vol, region, image_dim, method="texture"))
     print(f"raycast texture {image_dim:3d}^2: {ms:8.3f} ms (pack + march)", flush=True)

@@ -113,6 +113,22 @@ def test_raycast_global_bit_exact(gpu, image_dim):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("image_dim", [64, 288])
+def test_raycast_global_variants_bit_identical(gpu, image_dim):
+    """Every global-caster variant (round 6: pair taps, one ray per 64 / 16 / 8 / 4-lane group, the DR16 interleaved
+    volume) and the production rule give the one-step caster's image bit for bit, in both colour modes, on both sides
+    of the 2^16-ray switch (288^2 = 82944 rays)."""
+    vol = ops.create_volume(512, device=gpu, seed=0)
+    reg, _ = ops.region3d(vol, threshold=1, method="tiled")
+    reg = (reg != 0).to(torch.uint8)
+    for method in ("global", "global_f32"):
+        ref = ops.raycast(vol, reg, image_dim, method=method, variant=1)
+        assert int(ref.long().sum()) > 0
+        for v in [-1, 0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]:
+            out = ops.raycast(vol, reg, image_dim, method=method, variant=v)
+            assert torch.equal(out, ref), (method, v)
+
+
 def test_raycast_reference_data_golden(gpu):
     # T5: glibc-rand reference volume, 64x64 image sum = 127180 with 100 saturated pixels
     vol = ops.create_volume(512, background="rand")
