@@ -101,6 +101,23 @@ class Context:
             x.wait()
         return []
 
+    def exchange_segments(self, slot: int, send: torch.Tensor, soff: list, scnt: list, recv: torch.Tensor, roff: list,
+                          rcnt: list) -> list:
+        """Asynchronous exchange of contiguous segments: send[soff[q] : soff[q] + scnt[q]] goes to rank q and
+        recv[roff[q] : roff[q] + rcnt[q]] is received from rank q (one entry per rank, zero counts move nothing).
+        Returns the works to wait on. On RCCL with float32 GPU buffers it takes the NATIVE path (NativeExchange: a
+        dedicated RCCL communicator driven from C++, ~an order of magnitude less host time than a torch all_to_all;
+        `slot` names the exchange in flight, one per concurrently pending exchange); otherwise the same segments
+        as views through exchange() (gloo, LazyContext, CPU tensors)."""
+        if not self.distributed:
+            return []
+        nx = native_exchange(self) if send.is_cuda and send.dtype == torch.float32 else None
+        if nx is not None:
+            return nx.post(slot, send, soff, scnt, recv, roff, rcnt)
+        ins = [send[o:o + n] for o, n in zip(soff, scnt)]
+        outs = [recv[o:o + n] for o, n in zip(roff, rcnt)]
+        return self.exchange(outs, ins, async_op=True)
+
     def neighbour_exchange(self, pairs, async_op: bool = False) -> list:
         """Sends / receives with a few peers: pairs = [(peer, send tensor, recv tensor)], each peer at most once,
         tensors contiguous (possibly no pairs: the rank still takes part in the collective)."""
@@ -138,6 +155,57 @@ class Context:
         t = self.scalar(float(v))
         self.all_reduce_(t, "max")
         return float(t.item())
+
+
+class _NativeWork:
+    def __init__(self, nx, slot):
+        self.nx, self.slot = nx, slot
+
+    def wait(self):
+        self.nx.C.xcomm_wait(self.nx.handle, self.slot, self.nx.device)
+
+
+class NativeExchange:
+    """A dedicated RCCL communicator for per-step exchanges (csrc/comm/exchange_rccl.hip): rank 0's ncclUniqueId is
+    broadcast over the job's process group once, then every exchange is ONE C++ call (grouped ncclSend / ncclRecv per
+    peer on the communicator's stream, ordered after the caller's stream by an event) and its wait another (the
+    caller's stream waits for the slot's done event). Created on first use by Context.exchange_segments, on every
+    rank at the same program point (the exchange calls themselves are collective). PCMX_NATIVE_EXCHANGE=0 turns it
+    off (torch all_to_all instead)."""
+
+    def __init__(self, ctx: Context):
+        from .. import _C
+
+        self.C, self.device = _C, ctx.device.index
+        obj = [_C.xcomm_unique_id() if ctx.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        self.handle = _C.xcomm_create(obj[0], ctx.world, ctx.rank, self.device)
+
+    def post(self, slot, send, soff, scnt, recv, roff, rcnt) -> list:
+        self.C.xcomm_exchange(self.handle, int(slot), send, soff, scnt, recv, roff, rcnt)
+        return [_NativeWork(self, int(slot))]
+
+    def healthy(self) -> bool:
+        return self.C.xcomm_async_error(self.handle) == 0
+
+    def close(self) -> None:
+        if self.handle:
+            self.C.xcomm_destroy(self.handle)
+            self.handle = 0
+
+
+_NATIVE = {}
+
+
+def native_exchange(ctx: Context) -> NativeExchange | None:
+    """The job's NativeExchange (created on first call), or None when the backend is not RCCL, the context is a test
+    transport (LazyContext) or PCMX_NATIVE_EXCHANGE=0."""
+    if ctx.backend != "nccl" or type(ctx) is not Context or os.environ.get("PCMX_NATIVE_EXCHANGE", "1") == "0":
+        return None
+    nx = _NATIVE.get(ctx.device.index)
+    if nx is None:
+        nx = _NATIVE[ctx.device.index] = NativeExchange(ctx)
+    return nx
 
 
 class _DeferredWork:
@@ -225,6 +293,11 @@ def finalize(ctx: Context | None = None) -> None:
         try:
             if ctx is not None:
                 ctx.barrier()
+            if ctx is not None and ctx.device.type == "cuda":
+                torch.cuda.synchronize(ctx.device)
+            for nx in _NATIVE.values():
+                nx.close()
+            _NATIVE.clear()
         finally:
             dist.destroy_process_group()
 

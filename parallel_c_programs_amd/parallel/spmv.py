@@ -119,7 +119,8 @@ SlicedCSR.product_phase = _sliced_product_phase
 class DistributedSpMV:
     def __init__(self, ctx: Context, row_ptr: torch.Tensor, local: CSR, cuts: list[int], slices: int = 0,
                  head: float = 0.0625, balance: float = 0.0, chunks: int | None = None, item_nnz: int = 0,
-                 exchange: str = "ghost", keep_plain: bool = False, colsplit: bool | None = None):
+                 exchange: str = "ghost", keep_plain: bool = False, colsplit: bool | None = None,
+                 chunk0_frac: float | None = None):
         W, dev = ctx.world, ctx.device
         if exchange not in ("ghost", "allgather"):
             raise ValueError("exchange: 'ghost' or 'allgather'")
@@ -143,6 +144,22 @@ class DistributedSpMV:
         C = max(1, min(int(C), self.block))
         self.chunks = C
         self.L = -(-self.block // C)
+        # row chunk boundaries in local-row space, the same on every rank (cb[c] <= local row < cb[c + 1]: chunk c).
+        # Uniform (c * L) except the 2-chunk ghost layout of a distributed GPU step, whose chunk 0 takes a fraction
+        # chunk0_frac of the rows (round 6, default CHUNK0_FRAC): the column-split step posts chunk 0's exchange after
+        # chunk 0's combine and needs it at the top of the next step, so its window is chunk 1's phase-1 products +
+        # combine, while chunk 1's window is the fixed paired phase-0 launch. A smaller chunk 0 both shrinks chunk 0's
+        # exchange and widens its window (docs/ARCHITECTURE.md, SpMV exchange model; profiles/r6_spmv/).
+        if chunk0_frac is None:
+            chunk0_frac = self.CHUNK0_FRAC if (C == 2 and self.exchange == "ghost" and ctx.distributed and slices
+                                               and dev.type == "cuda" and colsplit is not False) else 0.5
+        if C == 2 and self.exchange == "ghost" and chunk0_frac != 0.5:
+            L0 = max(1, min(self.block - 1, int(round(float(chunk0_frac) * self.block))))
+            self.cb = [0, L0, max(self.block, L0)]
+        else:
+            self.cb = [c * self.L for c in range(C + 1)]
+        self.cb[-1] = max(self.cb[-1], self.block)
+        self.chunk0_frac = self.cb[1] / max(1, self.block) if C > 1 else 1.0
         col = local.col.to(dev)
         if self.exchange == "allgather":
             self.n_pad = C * W * self.L
@@ -174,7 +191,7 @@ class DistributedSpMV:
         self.sliced = bool(slices) and dev.type == "cuda"
         self.parts = []  # (first local row, last local row + 1, CSR, SlicedCSR or ColSplitCSR)
         for c in range(C):
-            a, b = min(c * self.L, self.rows), min((c + 1) * self.L, self.rows)
+            a, b = self.chunk_rows(c)
             part = m.row_block(a, b)
             if self.sliced:
                 try:
@@ -201,6 +218,7 @@ class DistributedSpMV:
             self.parts.append((a, b, part))
         self._pending = [[], []]  # column split: the exchange works of the previous step's chunks 0 and 1
         self.comm = True  # False (bench attribution only): every exchange skipped, the same kernels run
+        self._segs = [None] * C  # per chunk: the exchange's (send offsets, counts, recv offsets, counts), built once
         # the send-buffer pack in the sliced product's combine epilogue (False: a separate gather pass, the round-4 form)
         self.fuse_pack = True
         # the two chunk-0-column product launches of a column-split step as ONE paired launch (False: two launches)
@@ -212,6 +230,17 @@ class DistributedSpMV:
             self.send = torch.zeros(C, self.L, dtype=torch.float32, device=dev)  # tails of short chunks stay 0
         self.bufs = [torch.zeros(self.n_pad, dtype=torch.float32, device=dev) for _ in range(2)]
 
+    CHUNK0_FRAC = 0.5
+
+    def chunk_rows(self, c: int) -> tuple[int, int]:
+        """Local rows [a, b) of row chunk c on this rank."""
+        return min(self.cb[c], self.rows), min(self.cb[c + 1], self.rows)
+
+    def _chunk_of(self, lr: torch.Tensor) -> torch.Tensor:
+        """Row chunk of local rows lr (any rank's: the boundaries are the same on every rank)."""
+        inner = torch.tensor(self.cb[1:-1], dtype=lr.dtype, device=lr.device)
+        return torch.searchsorted(inner, lr, right=True)
+
     # ---- ghost layout (set-up: one exchange of the index lists)
     def _ghost_layout(self, col: torch.Tensor) -> torch.Tensor:
         """Builds the compact chunk-major / owner-minor layout, the per-(chunk, peer) send and receive lists, and
@@ -221,10 +250,10 @@ class DistributedSpMV:
         need = torch.unique(col.long())  # ascending global ids = owner-major
         owner = torch.searchsorted(cuts_t[1:], need, right=True)
         need, owner = need[owner != r], owner[owner != r]  # ghosts (own rows are all kept)
-        chunk = (need - cuts_t[owner]) // L
+        chunk = self._chunk_of(need - cuts_t[owner])
         # receive side: ghost (chunk c, owner q) counts; own segment of chunk c = own rows of chunk c
         cnt = torch.bincount(chunk * W + owner, minlength=C * W).view(C, W).cpu()
-        own = [max(0, min((c + 1) * L, self.rows) - min(c * L, self.rows)) for c in range(C)]
+        own = [b - a for a, b in (self.chunk_rows(c) for c in range(C))]
         for c in range(C):
             cnt[c, r] = own[c]
         # chunk c = [ghosts of every peer q != r, in rank order | own rows of chunk c]: the ghost part is ONE
@@ -249,8 +278,10 @@ class DistributedSpMV:
         # renumber the local columns: own rows -> own segment of their chunk, ghosts -> pos
         g = col.long()
         mine = (g >= self.row0) & (g < self.row1)
-        lo = g - self.row0
-        own_pos = seg_dev[(lo // L).clamp(0, C - 1) * W + r] + lo % L
+        lo = (g - self.row0).clamp(0, max(0, self.rows - 1))  # (only own columns use own_pos)
+        lch = self._chunk_of(lo)
+        cb_dev = torch.tensor(self.cb, dtype=torch.int64, device=dev)
+        own_pos = seg_dev[lch * W + r] + (lo - cb_dev[lch])
         gpos = pos[torch.searchsorted(need, g).clamp(max=max(0, need.numel() - 1))] if need.numel() else g
         out = torch.where(mine, own_pos, gpos).to(torch.int32)
         self.ghost_ids, self.ghost_pos = need, pos
@@ -267,19 +298,20 @@ class DistributedSpMV:
             dist.all_to_all_single(got, need.to(dev_c), got_counts.tolist(), req_counts.tolist())
             got = got.to(dev) - self.row0  # local rows peer q needs, ascending per peer
             peer = torch.repeat_interleave(torch.arange(W, device=dev), got_counts.to(dev))
-            gchunk = got // L
+            gchunk = self._chunk_of(got)
             self.send_idx, self.send_counts = [], []
             for c in range(C):
                 sel = gchunk == c  # owner-major order kept: peers in rank order, rows ascending
                 # layout positions, int32: the pack kernel reads 4 B of index per entry (ops.gather_)
-                self.send_idx.append((got[sel] - c * L + self.seg[c * W + r]).to(torch.int32).contiguous())
+                self.send_idx.append((got[sel] - self.cb[c] + self.seg[c * W + r]).to(torch.int32).contiguous())
                 self.send_counts.append(torch.bincount(peer[sel], minlength=W).tolist())
             self.sendbuf = [torch.empty(ix.numel(), dtype=torch.float32, device=dev) for ix in self.send_idx]
             # the same send lists inverted per own row (send_ptr: CSR over the chunk's rows, send_slot: slots in
             # sendbuf[c]): the sliced product's fused combine writes each row's value into its slots itself
             self.send_csr = []
             for c in range(C):
-                rows_c = max(0, min((c + 1) * L, self.rows) - min(c * L, self.rows))
+                a_c, b_c = self.chunk_rows(c)
+                rows_c = b_c - a_c
                 lr = (self.send_idx[c].long() - self.seg[c * W + r])
                 order = torch.sort(lr, stable=True).indices
                 ptr = torch.zeros(rows_c + 1, dtype=torch.int64, device=dev)
@@ -293,12 +325,13 @@ class DistributedSpMV:
     def powerlaw(ctx: Context, n_rows: int, nnz: int, alpha: float = 2.5, seed: int = 1,
                  slices: int = 0, head: float = 0.0625, balance: float = 0.0,
                  chunks: int | None = None, item_nnz: int = 0, exchange: str = "ghost",
-                 keep_plain: bool = False, colsplit: bool | None = None) -> DistributedSpMV:
+                 keep_plain: bool = False, colsplit: bool | None = None,
+                 chunk0_frac: float | None = None) -> DistributedSpMV:
         rp = powerlaw_row_ptr(n_rows, nnz, alpha, seed)
         cuts = nnz_balanced_cuts(rp, ctx.world)
         local = powerlaw_csr_rows(rp, cuts[ctx.rank], cuts[ctx.rank + 1], n_rows, seed)
         return DistributedSpMV(ctx, rp, local, cuts, slices, head, balance, chunks, item_nnz, exchange, keep_plain,
-                               colsplit)
+                               colsplit, chunk0_frac)
 
     def vendor_matrix(self) -> torch.Tensor:
         """This rank's rows as a torch sparse CSR tensor (layout columns): `torch.mv(A, xp)` runs hipSPARSE."""
@@ -355,7 +388,7 @@ class DistributedSpMV:
         return torch.cat([p[:self.cuts[q + 1] - self.cuts[q]] for q, p in enumerate(parts)])
 
     def local_positions_chunk(self, c: int) -> torch.Tensor:
-        a, b = min(c * self.L, self.rows), min((c + 1) * self.L, self.rows)
+        a, b = self.chunk_rows(c)
         s0 = self.seg[c * self.ctx.world + self.ctx.rank]
         return torch.arange(s0, s0 + (b - a), device=self.ctx.device)
 
@@ -392,14 +425,16 @@ class DistributedSpMV:
             gather_(out, self.send_idx[c], self.sendbuf[c])
         if not self.comm:
             return []
-        ins, outs, so = [], [], 0
-        for q in range(W):
-            ns = 0 if q == r else self.send_counts[c][q]
-            ins.append(self.sendbuf[c][so:so + ns])
-            so += ns
-            s0 = self.seg[c * W + q]
-            outs.append(out[s0:s0 + (0 if q == r else self.recv_counts[c][q])])
-        return self.ctx.exchange(outs, ins, async_op=True)
+        if self._segs[c] is None:  # per-peer segments of the send buffer and of the chunk's ghost region (fixed)
+            soff, scnt, roff, rcnt, so = [], [], [], [], 0
+            for q in range(W):
+                ns = 0 if q == r else self.send_counts[c][q]
+                soff.append(so), scnt.append(ns)
+                so += ns
+                roff.append(self.seg[c * W + q]), rcnt.append(0 if q == r else self.recv_counts[c][q])
+            self._segs[c] = (soff, scnt, roff, rcnt)
+        soff, scnt, roff, rcnt = self._segs[c]
+        return self.ctx.exchange_segments(c, self.sendbuf[c], soff, scnt, out, roff, rcnt)
 
     def _wait(self, k: int) -> None:
         for w in self._pending[k]:

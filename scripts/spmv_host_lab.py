@@ -6,7 +6,8 @@ the host enqueue time of the production step against its device time. The two ex
 Run: python scripts/spmv_host_lab.py [world] [reps]
 Env: SPMV_LAB_KINDS=paired (comma list of the A/B kinds; "none": no packs), SPMV_LAB_ITEM (0: the production rule), SPMV_LAB_SLICES,
 SPMV_LAB_PB=2,4 (resident product blocks per CU of the phase-0 / phase-1 launches),
-SPMV_LAB_N1=0 (skip the same-box N = 1 step)."""
+SPMV_LAB_N1=0 (skip the same-box N = 1 step), SPMV_LAB_FRAC=0.4 (row chunk 0's share), SPMV_LAB_RCCL=1 (the step with both exchanges on a world-1 RCCL
+communicator, round 6)."""
 import os
 import sys
 import time
@@ -24,9 +25,11 @@ def main():
     dev = torch.device("cuda", 0)
     item = int(os.environ.get("SPMV_LAB_ITEM", "0"))  # 0: the production rule
     slices = int(os.environ.get("SPMV_LAB_SLICES", "16"))
+    frac = float(os.environ.get("SPMV_LAB_FRAC", "0.5"))  # row chunk 0's share (round 6: uneven chunks)
     d = DistributedSpMV.powerlaw(Context(rank=0, world=W, device=dev), 10_000_000, 100_000_000, slices=slices, chunks=2,
-                                 item_nnz=item, colsplit=True)
-    print(f"item_nnz {d.parts[0][2].item_nnz}, slices {slices}, phase_blocks {d.parts[0][2].phase_blocks}", flush=True)
+                                 item_nnz=item, colsplit=True, chunk0_frac=frac)
+    print(f"item_nnz {d.parts[0][2].item_nnz}, slices {slices}, phase_blocks {d.parts[0][2].phase_blocks}, "
+          f"chunk0_frac {d.chunk0_frac:.3f} (rows {[d.chunk_rows(c) for c in range(2)]})", flush=True)
     xp = torch.rand(d.n_pad, device=dev)
     out = torch.zeros_like(xp)
     Wd, r = d.ctx.world, d.ctx.rank
@@ -132,6 +135,83 @@ def main():
     print(f"N={W} rank 0 column-split step (production): host enqueue {host:.4f} ms/step, device {devt:.4f} ms/step "
           f"({'launch-bound' if host > devt else 'device-bound'}; + ~0.03 ms of host time for the 2 exchange calls)",
           flush=True)
+    if os.environ.get("SPMV_LAB_RCCL") == "1":
+        # Round 6: the production step WITH its two exchanges on a world-1 RCCL communicator: each
+        # chunk's real send bytes go through an RCCL all_to_all_single to self, posted where _post_chunk posts it (right
+        # after that chunk's fused combine + pack) and waited where _step_colsplit waits (chunk 0's at the top of the
+        # next step, chunk 1's after the paired phase-0 launch), on RCCL's own stream, concurrently with the products.
+        # That prices RCCL's host launch, its kernel's CUs and its HBM / L2 traffic against the L2-bound products; only
+        # the xGMI transfer itself is not modelled (the self-exchange is a local copy).
+        import torch.distributed as dist
+        from parallel_c_programs_amd.parallel.dist import free_port
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        sendb = [sc[2] for sc in send_csr]
+        recvb = [torch.empty_like(b) for b in sendb]
+        print(f"exchange bytes per chunk: {[4 * b.numel() for b in sendb]}", flush=True)
+        pend = [None, None]
+        (_, _, q0), (_, _, q1) = d.parts
+        from parallel_c_programs_amd.parallel.dist import NativeExchange
+
+        nx = NativeExchange(Context(0, 1, 0, dev, "nccl"))  # the production native path (C++ grouped send/recv)
+
+        def post(c, native):
+            if native:
+                n = sendb[c].numel()
+                return nx.post(c, sendb[c], [0], [n], recvb[c], [0], [n])[0]
+            return dist.all_to_all_single(recvb[c], sendb[c], async_op=True)
+
+        def xstep(comm=True, native=False):
+            if pend[0] is not None:
+                pend[0].wait()
+                pend[0] = None
+            q0.products_pair(q1, xp, (0, q0.n_slices // 16), (0, q1.n_slices // 16), mode=q0.phase_blocks[0] << 8)
+            if pend[1] is not None:
+                pend[1].wait()
+                pend[1] = None
+            for c, (a, b, part) in enumerate(d.parts):
+                s0 = d.seg[c * Wd + r]
+                part.fused_combine = True
+                part.product_phase(xp, 1, c, out[s0:s0 + (b - a)], send=send_csr[c])
+                if comm:
+                    pend[c] = post(c, native)
+
+        def flush():
+            for k in range(2):
+                if pend[k] is not None:
+                    pend[k].wait()
+                    pend[k] = None
+
+        def xchg_only(native):
+            for c in range(2):
+                post(c, native).wait()
+
+        for rnd in range(4):
+            t_plain = dev_ms(lambda: xstep(False))
+            flush()
+            t_comm = dev_ms(lambda: xstep(True))
+            flush()
+            t_nat = dev_ms(lambda: xstep(True, native=True))
+            flush()
+            t_x = dev_ms(lambda: xchg_only(False))
+            t_xn = dev_ms(lambda: xchg_only(True))
+            print(f"round {rnd} N={W} rank step: no exchange {t_plain:.4f} ms; both RCCL self-exchanges in flight via "
+                  f"torch all_to_all_single {t_comm:.4f} ms (+{1e3 * (t_comm - t_plain):.1f} us), via the native "
+                  f"exchange {t_nat:.4f} ms (+{1e3 * (t_nat - t_plain):.1f} us); the two exchanges alone, back to back: "
+                  f"torch {t_x:.4f} ms, native {t_xn:.4f} ms", flush=True)
+        for native in (False, True):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                xstep(True, native)
+            t1 = time.perf_counter()
+            flush()
+            torch.cuda.synchronize()
+            print(f"host enqueue with the exchanges ({'native' if native else 'torch all_to_all_single'}): "
+                  f"{(t1 - t0) / reps * 1e3:.4f} ms/step", flush=True)
+        nx.close()
+        dist.destroy_process_group()
     if os.environ.get("SPMV_LAB_N1", "1") == "1":
         # the same-box N = 1 step (the bench's single-GPU section: 1e8 nnz, one sliced product) for the efficiency model
         del d, out, bufs, send_csr, packs, packs32

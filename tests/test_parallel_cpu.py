@@ -250,8 +250,9 @@ def test_stencil_checkpoint_resume_world2(tmp_path):
     assert np.array_equal(fa, reference_run(40, 7, 24).view(torch.int16).numpy())
 
 
-def _spmv(ctx, q, n, nnz, chunks, exchange, colsplit=None):
-    d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1, chunks=chunks, exchange=exchange, colsplit=colsplit)
+def _spmv(ctx, q, n, nnz, chunks, exchange, colsplit=None, chunk0_frac=None):
+    d = DistributedSpMV.powerlaw(ctx, n, nnz, seed=1, chunks=chunks, exchange=exchange, colsplit=colsplit,
+                                 chunk0_frac=chunk0_frac)
     x = torch.linspace(0, 1, n)
     y = d.step(x)
     y2 = d.step(y / y.abs().max())
@@ -302,6 +303,46 @@ def test_distributed_spmv_colsplit_plain_csr(world):
         assert torch.allclose(torch.from_numpy(res[r][0]), y, rtol=1e-5, atol=1e-5)
         ids, yp2 = torch.from_numpy(res[r][4]), torch.from_numpy(res[r][5])
         assert torch.allclose(yp2[ids >= 0], y2[ids[ids >= 0]], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("world,colsplit,frac", [(2, False, 0.3), (4, True, 0.35), (4, False, 0.7)])
+def test_distributed_spmv_uneven_row_chunks(world, colsplit, frac):
+    """Uneven row chunks (round 6: chunk 0 takes `frac` of each rank's rows, so the column-split step posts chunk 0's
+    smaller exchange earlier): the same rows through the same kernel give the serial product bit for bit, and every
+    layout entry (own rows and the ghosts the uneven exchanges delivered) holds its row's value."""
+    n, nnz = 3000, 40000
+    res = _collect(world, _spmv, n, nnz, 2, "ghost", colsplit, frac)
+    m = ops.powerlaw_csr(n, nnz, seed=1)
+    x = torch.linspace(0, 1, n)
+    y = ops.spmv(m, x)
+    y2 = ops.spmv(m, y / y.abs().max())
+    for r in range(world):
+        assert res[r][6] == colsplit
+        if colsplit:
+            assert torch.allclose(torch.from_numpy(res[r][0]), y, rtol=1e-5, atol=1e-5)
+        else:
+            assert torch.equal(torch.from_numpy(res[r][0]), y)
+        ids, yp2 = torch.from_numpy(res[r][4]), torch.from_numpy(res[r][5])
+        assert torch.allclose(yp2[ids >= 0], y2[ids[ids >= 0]], rtol=1e-5, atol=1e-5)
+
+
+def _spmv_chunk_bounds(ctx, q, frac):
+    d = DistributedSpMV.powerlaw(ctx, 3000, 40000, seed=1, chunks=2, chunk0_frac=frac)
+    q.put((ctx.rank, (d.cb, [d.chunk_rows(c) for c in range(2)], d.rows, d.block)))
+
+
+def test_spmv_chunk0_frac_bounds_are_global():
+    """The chunk boundaries are the same on every rank (fractions of the LARGEST block), so a ghost's chunk is known
+    to its receiver without asking its owner."""
+    res = _collect(3, _spmv_chunk_bounds, 0.3)
+    cbs = {tuple(res[r][0]) for r in range(3)}
+    assert len(cbs) == 1
+    cb = cbs.pop()
+    block = res[0][3]
+    assert cb[0] == 0 and cb[1] == round(0.3 * block) and cb[2] >= block
+    for r in range(3):
+        (a0, b0), (a1, b1) = res[r][1]
+        assert a0 == 0 and b0 == a1 and b1 == res[r][2]
 
 
 def _late_wait_colsplit(self, xp, out):
