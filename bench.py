@@ -21,6 +21,9 @@ max) and its longest host enqueue:
   scan     global inclusive prefix sum over the rank-ordered concatenation (reduce-then-scan): weak and
            strong like reduce; fp64 check of EVERY output of every rank incl. its rank offset, and the stream's
            look-back error word
+  axpy     y <- alpha x + y, 1e9 f32 per GPU (12 B/element), weak scaling, no communication; every element of the
+           timed output checked against fp64 (data chosen so that every step is exact in fp32); torch's
+           y.add_(x, alpha=a) timed alongside
   stencil  16384^2 bf16 5-point stencil (random grid), strong scaling: row slabs, T fused updates per kernel (T by
            slab height: 8 / 8 / 6 / 6 at N = 1 / 2 / 4 / 8), a deep halo at N = 4 / 8 (5T rows exchanged every 5th
            step, overlapped with the interior update; self-tested on the job's backend first); bit-exact checks: the timed grid itself (all warm-up + timed updates) against a
@@ -66,7 +69,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "TFLOPS SGEMM 8192^2 + GB/s reduce 1e9 f32, at 1/2/4/8 MI355X"
-SECTIONS = ("sgemm", "reduce", "scan", "stencil", "spmv")
+SECTIONS = ("sgemm", "reduce", "scan", "axpy", "stencil", "spmv")
 
 
 def parse(argv=None):
@@ -486,6 +489,32 @@ def main(argv=None):
         if name in sections:
             runner.run(name, lambda chk, name=name, cls=cls: reduce_scan(name, cls, chk))
 
+    # ---- AXPY 1e9 f32 per GPU (the streaming hot loop; weak scaling, no exchange)
+    def axpy(chk):
+        w = W.Axpy(ctx, n=rn)
+        yield
+        ms, hms = [], []
+        t = timed(ctx, w.step, K, Wm, ms, hms, settle_ms=SETTLE)
+        rep = w.report(t, K)
+        out["axpy_gbps"], out["axpy_ms_per_step"] = _r(rep["value"], 1), _r(rep["ms_per_step"])
+        device_times(chk, "axpy", ms, hms)
+        if not args.no_ref and dev.type == "cuda":
+            yield
+            t_ref = timed(ctx, w.torch_step, K, Wm, settle_ms=SETTLE)
+            out["torch_axpy_gbps"] = _r(world * w.work_per_step() * K / t_ref / 1e9, 1)
+        if runner.injected("axpy", "perturb"):
+            w.y[w.y.numel() // 7] += 1.0
+        yield
+        c = w.check(reduce=False)
+        runner.maybe_raise("axpy")
+        chk.error("axpy_rel_err_vs_fp64", c["rel_err_vs_fp64"], LIM)
+        out["axpy_steps_checked"] = c["steps_applied"]
+        del w
+        log(f"axpy {out['axpy_gbps']} GB/s")
+
+    if "axpy" in sections:
+        runner.run("axpy", axpy)
+
     # ---- stencil 16384^2 bf16, strong scaling over row slabs with the overlapped fused halo exchange
     def stencil(chk):
         s = W.Stencil(ctx, n=args.stencil_n, fuse=args.stencil_fuse, halo_mult=args.stencil_halo_mult)
@@ -592,7 +621,11 @@ def main(argv=None):
     if ctx.distributed:
         import torch.distributed as dist
 
+        from parallel_c_programs_amd.parallel.dist import native_exchange_active
+
         out["comm_backend"], out["comm_world_size"] = ctx.backend, dist.get_world_size()
+        # the per-step exchanges ran on the native RCCL communicator (C++ grouped send / recv), not torch's all_to_all
+        out["comm_native_exchange"] = native_exchange_active(ctx)
 
     rc = 1 if runner.failed else 0
     if rank == 0:

@@ -19,6 +19,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 
 #include "pcmx_common.h"
 #include "pcmx_errors.h"
@@ -75,21 +76,22 @@ extern "C" int pcmx_xcomm_create(const void* id, int world, int rank, int device
     return 0;
 }
 
-// send / recv: float buffers; soff / scnt / roff / rcnt: world entries each (floats). Peers with a zero count move
+// send / recv: device buffers; soff / scnt / roff / rcnt: world entries each, in BYTES. Peers with a zero count move
 // nothing; the self entry (q == rank) is a copy through RCCL like any other peer (a world-1 communicator exchanges
 // with itself: the lab's stand-in for xGMI).
-extern "C" int pcmx_xcomm_exchange(void* handle, int slot, const float* send, const long long* soff,
-                                   const long long* scnt, float* recv, const long long* roff, const long long* rcnt,
+extern "C" int pcmx_xcomm_exchange(void* handle, int slot, const void* send, const long long* soff,
+                                   const long long* scnt, void* recv, const long long* roff, const long long* rcnt,
                                    hipStream_t compute) {
+    const char* sb = static_cast<const char*>(send);
+    char* rb = static_cast<char*>(recv);
     XComm* x = static_cast<XComm*>(handle);
-    if (!x || slot < 0 || slot >= kSlots) return PCMX_ERR_ARG;
+    if (!x || !x->comm || slot < 0 || slot >= kSlots) return PCMX_ERR_ARG;
     PCMX_HIP_RET(hipEventRecord(x->ready[slot], compute));
     PCMX_HIP_RET(hipStreamWaitEvent(x->stream, x->ready[slot], 0));
     int rc = rc_nccl(ncclGroupStart());
     for (int q = 0; rc == 0 && q < x->world; ++q) {
-        if (scnt[q] > 0) rc = rc_nccl(ncclSend(send + soff[q], (size_t)scnt[q], ncclFloat32, q, x->comm, x->stream));
-        if (rc == 0 && rcnt[q] > 0)
-            rc = rc_nccl(ncclRecv(recv + roff[q], (size_t)rcnt[q], ncclFloat32, q, x->comm, x->stream));
+        if (scnt[q] > 0) rc = rc_nccl(ncclSend(sb + soff[q], (size_t)scnt[q], ncclUint8, q, x->comm, x->stream));
+        if (rc == 0 && rcnt[q] > 0) rc = rc_nccl(ncclRecv(rb + roff[q], (size_t)rcnt[q], ncclUint8, q, x->comm, x->stream));
     }
     const int rc_end = rc_nccl(ncclGroupEnd());  // (always closes the group it opened)
     if (rc == 0) rc = rc_end;
@@ -105,10 +107,63 @@ extern "C" int pcmx_xcomm_wait(void* handle, int slot, hipStream_t compute) {
     return 0;
 }
 
+// Start-up probe: one float to and from every peer (value 1000 * sender + receiver) through the same grouped path,
+// waited for on the host for at most timeout_ms (hipEventQuery polling), then checked. A probe that times out or
+// fails ABORTS the communicator (ncclCommAbort ends its pending operations, so nothing is left spinning on the GPU)
+// and returns PCMX_ERR_TIMEOUT / PCMX_ERR_COMM: the caller falls back to torch.distributed. Collective.
+extern "C" int pcmx_xcomm_probe(void* handle, int timeout_ms) {
+    XComm* x = static_cast<XComm*>(handle);
+    if (!x || !x->comm) return PCMX_ERR_ARG;
+    const int W = x->world;
+    float *dev = nullptr;
+    if (hipMalloc(&dev, 2 * (size_t)W * sizeof(float)) != hipSuccess) return PCMX_ERR_ALLOC;
+    float* host = new float[2 * (size_t)W];
+    for (int q = 0; q < W; ++q) host[q] = (float)(1000 * x->rank + q), host[W + q] = -1.f;
+    long long* offs = new long long[4 * (size_t)W];
+    for (int q = 0; q < W; ++q) offs[q] = 4 * q, offs[W + q] = 4, offs[2 * W + q] = 4 * q, offs[3 * W + q] = 4;
+    int rc = hipMemcpy(dev, host, 2 * (size_t)W * sizeof(float), hipMemcpyHostToDevice) == hipSuccess ? 0 : PCMX_ERR_COMM;
+    if (rc == 0)
+        rc = pcmx_xcomm_exchange(x, kSlots - 1, dev, offs, offs + W, dev + W, offs + 2 * W, offs + 3 * W, x->stream);
+    if (rc == 0) {
+        const timespec nap{0, 200000};  // 0.2 ms
+        for (long waited_us = 0;; waited_us += 200) {
+            const hipError_t q = hipEventQuery(x->done[kSlots - 1]);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) {
+                rc = PCMX_ERR_COMM;
+                break;
+            }
+            ncclResult_t ae = ncclSuccess;
+            if (ncclCommGetAsyncError(x->comm, &ae) != ncclSuccess || ae != ncclSuccess) {
+                rc = PCMX_ERR_COMM;
+                break;
+            }
+            if (waited_us / 1000 >= timeout_ms) {
+                rc = PCMX_ERR_TIMEOUT;
+                break;
+            }
+            nanosleep(&nap, nullptr);
+        }
+    }
+    if (rc == 0 && hipMemcpy(host + W, dev + W, (size_t)W * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = PCMX_ERR_COMM;
+    for (int q = 0; rc == 0 && q < W; ++q)
+        if (host[W + q] != (float)(1000 * q + x->rank)) rc = PCMX_ERR_COMM;
+    if (rc != 0) {
+        ncclCommAbort(x->comm);
+        x->comm = nullptr;
+    }
+    (void)hipStreamSynchronize(x->stream);
+    (void)hipFree(dev);
+    delete[] host;
+    delete[] offs;
+    return rc;
+}
+
 // Asynchronous RCCL errors of the communicator (a peer that died, a transport failure): 0 when healthy.
 extern "C" int pcmx_xcomm_async_error(void* handle) {
     XComm* x = static_cast<XComm*>(handle);
-    if (!x) return PCMX_ERR_ARG;
+    if (!x || !x->comm) return PCMX_ERR_ARG;
     ncclResult_t e = ncclSuccess;
     const int rc = rc_nccl(ncclCommGetAsyncError(x->comm, &e));
     return rc ? rc : rc_nccl(e);
@@ -118,7 +173,7 @@ extern "C" int pcmx_xcomm_destroy(void* handle) {
     XComm* x = static_cast<XComm*>(handle);
     if (!x) return 0;
     (void)hipStreamSynchronize(x->stream);
-    const int rc = rc_nccl(ncclCommDestroy(x->comm));
+    const int rc = x->comm ? rc_nccl(ncclCommDestroy(x->comm)) : 0;  // (an aborted communicator is gone already)
     for (int s = 0; s < kSlots; ++s) {
         if (x->ready[s]) (void)hipEventDestroy(x->ready[s]);
         if (x->done[s]) (void)hipEventDestroy(x->done[s]);

@@ -234,14 +234,15 @@ int pcmx_unpack_halo_changed(void* tile, int elem_bytes, int H, int W, int ld, c
                              hipStream_t s);
 
 /* ---------------------------------------------------------------- grouped exchange on a dedicated RCCL communicator
- * (comm/exchange_rccl.hip): per-peer float segments send[soff[q] .. + scnt[q]) -> peer q, recv[roff[q] .. + rcnt[q])
+ * (comm/exchange_rccl.hip): per-peer byte segments send[soff[q] .. + scnt[q]) -> peer q, recv[roff[q] .. + rcnt[q])
  * <- peer q, on the communicator's stream, ordered after `compute` (event) and waited for by pcmx_xcomm_wait. */
 int pcmx_xcomm_id_bytes(void);
 int pcmx_xcomm_unique_id(void* out);
 int pcmx_xcomm_create(const void* id, int world, int rank, int device, void** out);
-int pcmx_xcomm_exchange(void* handle, int slot, const float* send, const long long* soff, const long long* scnt,
-                        float* recv, const long long* roff, const long long* rcnt, hipStream_t compute);
+int pcmx_xcomm_exchange(void* handle, int slot, const void* send, const long long* soff, const long long* scnt,
+                        void* recv, const long long* roff, const long long* rcnt, hipStream_t compute);
 int pcmx_xcomm_wait(void* handle, int slot, hipStream_t compute);
+int pcmx_xcomm_probe(void* handle, int timeout_ms);
 int pcmx_xcomm_async_error(void* handle);
 int pcmx_xcomm_destroy(void* handle);
 

@@ -828,18 +828,21 @@ int64_t xcomm_create(const std::string& id, int64_t world, int64_t rank, int64_t
 void xcomm_exchange(int64_t h, int64_t slot, const at::Tensor& send, const std::vector<int64_t>& soff,
                     const std::vector<int64_t>& scnt, at::Tensor recv, const std::vector<int64_t>& roff,
                     const std::vector<int64_t>& rcnt) {
-    check_gpu(send, "send", at::kFloat), check_gpu(recv, "recv", at::kFloat);
-    TORCH_CHECK(send.is_contiguous() && recv.is_contiguous() && send.device() == recv.device(), "xcomm_exchange: buffers");
+    TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.device() == recv.device(), "xcomm_exchange: GPU buffers, one device");
+    TORCH_CHECK(send.is_contiguous() && recv.is_contiguous() && send.scalar_type() == recv.scalar_type(),
+                "xcomm_exchange: contiguous buffers of one dtype");
     const size_t W = soff.size();
     TORCH_CHECK(W > 0 && scnt.size() == W && roff.size() == W && rcnt.size() == W, "xcomm_exchange: one entry per rank");
+    const int64_t es = send.element_size();
+    std::vector<int64_t> b(4 * W);  // the segments in bytes
     for (size_t q = 0; q < W; ++q) {  // every segment inside its buffer (host-side, no device data involved)
         TORCH_CHECK(scnt[q] >= 0 && soff[q] >= 0 && soff[q] + scnt[q] <= send.numel(), "xcomm_exchange: send segment ", q);
         TORCH_CHECK(rcnt[q] >= 0 && roff[q] >= 0 && roff[q] + rcnt[q] <= recv.numel(), "xcomm_exchange: recv segment ", q);
+        b[q] = soff[q] * es, b[W + q] = scnt[q] * es, b[2 * W + q] = roff[q] * es, b[3 * W + q] = rcnt[q] * es;
     }
-    check_rc(pcmx_xcomm_exchange(reinterpret_cast<void*>(h), (int)slot, send.data_ptr<float>(),
-                                 reinterpret_cast<const long long*>(soff.data()), reinterpret_cast<const long long*>(scnt.data()),
-                                 recv.data_ptr<float>(), reinterpret_cast<const long long*>(roff.data()),
-                                 reinterpret_cast<const long long*>(rcnt.data()), cur_stream(recv)),
+    const auto* bl = reinterpret_cast<const long long*>(b.data());
+    check_rc(pcmx_xcomm_exchange(reinterpret_cast<void*>(h), (int)slot, send.data_ptr(), bl, bl + W, recv.data_ptr(),
+                                 bl + 2 * W, bl + 3 * W, cur_stream(recv)),
              "xcomm_exchange");
 }
 
@@ -858,6 +861,10 @@ PYBIND11_MODULE(_C, mod) {
     mod.def("xcomm_exchange", &xcomm_exchange, "grouped per-peer send/recv of float segments, ordered after the "
             "current stream (slot: one exchange in flight)");
     mod.def("xcomm_wait", &xcomm_wait, "the current stream of `device` waits for the slot's exchange");
+    mod.def("xcomm_probe", [](int64_t h, int64_t timeout_ms) {
+        pybind11::gil_scoped_release nogil;
+        return pcmx_xcomm_probe(reinterpret_cast<void*>(h), (int)timeout_ms);
+    }, "one float to / from every peer, host-waited with a timeout; aborts the communicator on failure (0: ok)");
     mod.def("xcomm_async_error", [](int64_t h) { return pcmx_xcomm_async_error(reinterpret_cast<void*>(h)); });
     mod.def("xcomm_destroy", [](int64_t h) { return pcmx_xcomm_destroy(reinterpret_cast<void*>(h)); });
 }

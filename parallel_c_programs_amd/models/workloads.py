@@ -128,6 +128,56 @@ class Reduce(Workload):
         return {"rel_err_vs_fp64": e, "check_passed": e <= REL_ERR_LIMIT}
 
 
+class Axpy(Workload):
+    """y <- alpha x + y over n f32 per GPU (the north star's AXPY hot loop; ref 6-opencl-region-growing/
+    multiply_opencl.cl:1-4 is its element-wise ancestor): 12 B/element of HBM traffic per step, weak scaling, no
+    communication. The ticket-ordered streaming kernel (csrc/kernels/vector.hip).
+
+    The data make every step EXACT in fp32, so the timed output itself is checkable bit for bit after any number of
+    steps: x = k / 2^11 (k < 2^11), y0 on the 2^-23 grid in [0, 1), alpha = 2^-12; every increment alpha x is then a
+    multiple of 2^-23 and y stays below 2 (where that grid is representable) for fewer than 4096 steps."""
+
+    ALPHA = 2.0 ** -12
+
+    def __init__(self, ctx, n=10**9, **_):
+        super().__init__(ctx, {"n": n, "alpha": self.ALPHA}, "axpy", "GB/s")
+        self.x = torch.empty(int(n), device=ctx.device)
+        self.y = torch.empty(int(n), device=ctx.device)
+        ops.rand_uniform_(self.x, 5000 + ctx.rank, 0.0, 1.0)
+        ops.rand_uniform_(self.y, 6000 + ctx.rank, 0.0, 1.0)
+        self.x.mul_(2048.0).floor_().div_(2048.0)
+        self.y.mul_(2.0 ** 23).floor_().div_(2.0 ** 23)
+        self.y0 = self.y.clone()
+        self.alpha, self.steps = self.ALPHA, 0
+
+    def step(self):
+        ops.axpy_(self.y, self.alpha, self.x)
+        self.steps += 1
+
+    def torch_step(self):
+        """The same update through torch (the vendor bar); counted like a step."""
+        self.y.add_(self.x, alpha=self.alpha)
+        self.steps += 1
+
+    def work_per_step(self):
+        return 12.0 * self.x.numel()
+
+    def check(self, reduce: bool = True, chunk: int = 1 << 26):
+        """EVERY element of the timed output against fp64 y0 + steps * alpha * x (exact while steps < 4096), relative
+        to max |y|. Local only."""
+        err = torch.zeros((), dtype=torch.float64, device=self.x.device)
+        big = torch.zeros((), dtype=torch.float64, device=self.x.device)
+        n, a = self.x.numel(), self.steps * self.alpha
+        for s0 in range(0, n, chunk):
+            ref = self.y0[s0:s0 + chunk].double() + a * self.x[s0:s0 + chunk].double()
+            err = torch.maximum(err, (self.y[s0:s0 + chunk].double() - ref).abs().max())
+            big = torch.maximum(big, ref.abs().max())
+        e = (err / big.clamp_min(1e-300)).item()
+        if reduce:
+            e = self.ctx.max_over_ranks(e)
+        return {"rel_err_vs_fp64": e, "steps_applied": self.steps, "check_passed": e <= REL_ERR_LIMIT}
+
+
 class Scan(Workload):
     """Inclusive prefix sum across ranks: local totals all-gathered, rank offset fed to the single-pass
     decoupled look-back scan as its initial value."""

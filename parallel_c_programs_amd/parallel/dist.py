@@ -105,13 +105,13 @@ class Context:
                           rcnt: list) -> list:
         """Asynchronous exchange of contiguous segments: send[soff[q] : soff[q] + scnt[q]] goes to rank q and
         recv[roff[q] : roff[q] + rcnt[q]] is received from rank q (one entry per rank, zero counts move nothing).
-        Returns the works to wait on. On RCCL with float32 GPU buffers it takes the NATIVE path (NativeExchange: a
+        Returns the works to wait on. On RCCL with GPU buffers of one dtype it takes the NATIVE path (NativeExchange: a
         dedicated RCCL communicator driven from C++, ~an order of magnitude less host time than a torch all_to_all;
         `slot` names the exchange in flight, one per concurrently pending exchange); otherwise the same segments
         as views through exchange() (gloo, LazyContext, CPU tensors)."""
         if not self.distributed:
             return []
-        nx = native_exchange(self) if send.is_cuda and send.dtype == torch.float32 else None
+        nx = native_exchange(self) if send.is_cuda and send.dtype == recv.dtype else None
         if nx is not None:
             return nx.post(slot, send, soff, scnt, recv, roff, rcnt)
         ins = [send[o:o + n] for o, n in zip(soff, scnt)]
@@ -180,6 +180,12 @@ class NativeExchange:
         obj = [_C.xcomm_unique_id() if ctx.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         self.handle = _C.xcomm_create(obj[0], ctx.world, ctx.rank, self.device)
+        # proven before first use: one float to / from every peer, host-waited with a timeout (a hung or failed probe
+        # aborts the communicator), then agreed over the job's own process group; any failure -> the torch path
+        rc = _C.xcomm_probe(self.handle, int(float(os.environ.get("PCMX_XCOMM_PROBE_S", "60")) * 1000))
+        if ctx.max_over_ranks(0.0 if rc == 0 else 1.0) != 0.0:
+            self.close()
+            raise RuntimeError(f"native exchange probe failed (rank {ctx.rank}: rc {rc})")
 
     def post(self, slot, send, soff, scnt, recv, roff, rcnt) -> list:
         self.C.xcomm_exchange(self.handle, int(slot), send, soff, scnt, recv, roff, rcnt)
@@ -200,12 +206,23 @@ _NATIVE = {}
 def native_exchange(ctx: Context) -> NativeExchange | None:
     """The job's NativeExchange (created on first call), or None when the backend is not RCCL, the context is a test
     transport (LazyContext) or PCMX_NATIVE_EXCHANGE=0."""
-    if ctx.backend != "nccl" or type(ctx) is not Context or os.environ.get("PCMX_NATIVE_EXCHANGE", "1") == "0":
+    if ctx.backend != "nccl" or isinstance(ctx, LazyContext) or os.environ.get("PCMX_NATIVE_EXCHANGE", "1") == "0":
         return None
-    nx = _NATIVE.get(ctx.device.index)
-    if nx is None:
-        nx = _NATIVE[ctx.device.index] = NativeExchange(ctx)
-    return nx
+    key = ctx.device.index
+    if key not in _NATIVE:
+        try:
+            _NATIVE[key] = NativeExchange(ctx)
+        except RuntimeError as e:  # (the same outcome on every rank: the probe's result is agreed)
+            import sys
+
+            print(f"[dist] {e}: exchanges go through torch.distributed", file=sys.stderr, flush=True)
+            _NATIVE[key] = None
+    return _NATIVE[key]
+
+
+def native_exchange_active(ctx: Context) -> bool:
+    """True when this job's exchanges run on the native RCCL communicator (reported in the bench line)."""
+    return _NATIVE.get(ctx.device.index) is not None
 
 
 class _DeferredWork:
@@ -296,7 +313,8 @@ def finalize(ctx: Context | None = None) -> None:
             if ctx is not None and ctx.device.type == "cuda":
                 torch.cuda.synchronize(ctx.device)
             for nx in _NATIVE.values():
-                nx.close()
+                if nx is not None:
+                    nx.close()
             _NATIVE.clear()
         finally:
             dist.destroy_process_group()

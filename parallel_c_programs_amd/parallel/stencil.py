@@ -94,12 +94,17 @@ class StencilSlab:
         """One grouped exchange of `halo` contiguous boundary rows per neighbour (Context.neighbour_exchange: ONE
         list all_to_all on RCCL, ~19 us of host time against ~60 us for a batch of four P2P ops, which would make a
         2048-row slab's step, ~45 us of GPU time at N = 8, launch-bound)."""
-        u, h, rows, pairs = self.u, self.halo, self.rows, []
+        u, h, rows, W, cols = self.u, self.halo, self.rows, self.ctx.world, self.cols
+        # as segments of the flat slab (Context.exchange_segments: the native RCCL path on a GPU job, else the same
+        # views through one list all-to-all); slot 4 (the SpMV chunks use 0 and 1)
+        soff, scnt, roff, rcnt = [0] * W, [0] * W, [0] * W, [0] * W
         if self.north >= 0:
-            pairs.append((self.north, u[h:2 * h], u[0:h]))
+            soff[self.north], scnt[self.north], roff[self.north], rcnt[self.north] = h * cols, h * cols, 0, h * cols
         if self.south >= 0:
-            pairs.append((self.south, u[rows:rows + h], u[rows + h:rows + 2 * h]))
-        return self.ctx.neighbour_exchange(pairs, async_op=True)
+            q = self.south
+            soff[q], scnt[q], roff[q], rcnt[q] = rows * cols, h * cols, (rows + h) * cols, h * cols
+        flat = u.view(-1)
+        return self.ctx.exchange_segments(4, flat, soff, scnt, flat, roff, rcnt)
 
     def _extent(self, phase: int) -> tuple[int, int]:
         """Local rows the step at `phase` updates: its own rows plus (m-1-phase)T halo rows on each side with a

@@ -156,10 +156,27 @@ def main():
 
         nx = NativeExchange(Context(0, 1, 0, dev, "nccl"))  # the production native path (C++ grouped send/recv)
 
+        side = torch.cuda.Stream(dev)
+        evs = [torch.cuda.Event(), torch.cuda.Event()]
+
+        class _Ev:
+            def __init__(self, c):
+                self.c = c
+
+            def wait(self):
+                torch.cuda.current_stream(dev).wait_event(evs[self.c])
+
         def post(c, native):
+            if native == "copy":  # the same event structure, the exchange replaced by torch's copy on a side stream
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    recvb[c].copy_(sendb[c])
+                    evs[c].record(side)
+                return _Ev(c)
             if native:
                 n = sendb[c].numel()
-                return nx.post(c, sendb[c], [0], [n], recvb[c], [0], [n])[0]
+                w = nx.post(c, sendb[c], [0], [n], recvb[c], [0], [n])[0]
+                return w if native != "nowait" else None
             return dist.all_to_all_single(recvb[c], sendb[c], async_op=True)
 
         def xstep(comm=True, native=False):
@@ -194,12 +211,18 @@ def main():
             flush()
             t_nat = dev_ms(lambda: xstep(True, native=True))
             flush()
+            t_nw = dev_ms(lambda: xstep(True, native="nowait"))
+            flush()
+            torch.cuda.synchronize()
+            t_cp = dev_ms(lambda: xstep(True, native="copy"))
+            flush()
             t_x = dev_ms(lambda: xchg_only(False))
             t_xn = dev_ms(lambda: xchg_only(True))
             print(f"round {rnd} N={W} rank step: no exchange {t_plain:.4f} ms; both RCCL self-exchanges in flight via "
                   f"torch all_to_all_single {t_comm:.4f} ms (+{1e3 * (t_comm - t_plain):.1f} us), via the native "
                   f"exchange {t_nat:.4f} ms (+{1e3 * (t_nat - t_plain):.1f} us); the two exchanges alone, back to back: "
-                  f"torch {t_x:.4f} ms, native {t_xn:.4f} ms", flush=True)
+                  f"torch {t_x:.4f} ms, native {t_xn:.4f} ms; native posted but never waited {t_nw:.4f} ms; a side-stream "
+                  f"copy with the same waits {t_cp:.4f} ms", flush=True)
         for native in (False, True):
             torch.cuda.synchronize()
             t0 = time.perf_counter()

@@ -326,6 +326,24 @@ c.exchange([out[2:5]], [src[0:3]])
 torch.cuda.synchronize()
 assert torch.equal(out[2:5], src[0:3]) and float(out[0:2].sum()) == 0 and float(out[5]) == 0
 print("rccl call shapes ok")
+# the native grouped exchange (dedicated RCCL communicator, csrc/comm/exchange_rccl.hip): probed at creation, then
+# segments to / from every rank (here: itself) through Context.exchange_segments, an out-of-bounds segment refused
+from parallel_c_programs_amd.parallel.dist import native_exchange, native_exchange_active
+nx = native_exchange(c)
+assert nx is not None and native_exchange_active(c)
+snd = torch.arange(10, dtype=torch.float32, device=dev) + 1
+rcv = torch.zeros(16, device=dev)
+for w in c.exchange_segments(3, snd, [2], [5], rcv, [9], [5]):
+    w.wait()
+torch.cuda.synchronize()
+assert torch.equal(rcv[9:14], snd[2:7]) and float(rcv[:9].sum()) == 0 and float(rcv[14:].sum()) == 0, rcv
+try:
+    c.exchange_segments(3, snd, [8], [5], rcv, [0], [5])
+    raise SystemExit("out-of-bounds send segment accepted")
+except RuntimeError:
+    pass
+assert nx.healthy()
+print("native exchange ok")
 # ... and the distributed SpMV step (ghost layout set-up exchange, _post_chunk per chunk, step_padded) and the
 # seeded global scan, through a context that takes the N > 1 branches
 from parallel_c_programs_amd.parallel.spmv import DistributedSpMV

@@ -568,6 +568,7 @@ def test_bench_world_size_mismatch_is_an_error():
 @pytest.mark.parametrize("fault,section,failed_key", [
     ("sgemm:1:perturb", "sgemm", "sgemm_max_rel_err_vs_fp64"),
     ("scan:0:perturb", "scan", "scan_weak_rel_err_vs_fp64"),
+    ("axpy:1:perturb", "axpy", "axpy_rel_err_vs_fp64"),
     ("stencil:1:perturb", "stencil", "stencil_timed_grid_bit_exact"),
     ("spmv:1:perturb", "spmv", "spmv_max_rel_err_vs_fp64"),
 ])
