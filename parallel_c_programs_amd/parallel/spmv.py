@@ -230,7 +230,7 @@ class DistributedSpMV:
             self.send = torch.zeros(C, self.L, dtype=torch.float32, device=dev)  # tails of short chunks stay 0
         self.bufs = [torch.zeros(self.n_pad, dtype=torch.float32, device=dev) for _ in range(2)]
 
-    CHUNK0_FRAC = 0.5
+    CHUNK0_FRAC = 0.4
 
     def chunk_rows(self, c: int) -> tuple[int, int]:
         """Local rows [a, b) of row chunk c on this rank."""
