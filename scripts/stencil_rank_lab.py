@@ -15,7 +15,10 @@ Run: python scripts/stencil_rank_lab.py [fuse ...]
 Env: STENCIL_LAB_WORLDS=8 (subset of 1,2,4,8), STENCIL_LAB_RPW=0,18 (rows per wave forced on the non-edge launches
 as an explicit launch shape of each call, ops.stencil.launch_shape; 0 = production rule; one line per value, all in one
 process for an A/B); STENCIL_LAB_DEEP=2,3,4 (halo depths m); STENCIL_LAB_ONLY=full (subset of full, split3, split2, split2c); STENCIL_LAB_AHEAD=3 / 6 / 9 (prefetch ring
-of the forced shapes); STENCIL_LAB_CPL=4 / 8 (columns per lane of the forced shapes).
+of the forced shapes); STENCIL_LAB_CPL=4 / 8 (columns per lane of the forced shapes); STENCIL_LAB_RCCL=1 (round 6:
+each deep-halo variant also runs WITH its exchange: the real halo bytes, 2 x mT rows, through the native exchange on a
+world-1 RCCL communicator, posted before the interior launch and waited before the edge launch as StencilSlab.step
+does; printed as deepM+x).
 """
 import os
 import sys
@@ -45,6 +48,15 @@ def timed(fn, reps=50):
 def main():
     fuses = [int(a) for a in sys.argv[1:]] or [4, 6, 8]
     dev = torch.device("cuda", 0)
+    nx = None
+    if os.environ.get("STENCIL_LAB_RCCL") == "1":
+        import torch.distributed as dist
+
+        from parallel_c_programs_amd.parallel.dist import Context, NativeExchange, free_port
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        nx = NativeExchange(Context(0, 1, 0, dev, "nccl"))
     g = torch.Generator(device=dev).manual_seed(1)
     worlds = [int(w) for w in os.environ.get("STENCIL_LAB_WORLDS", "1,2,4,8").split(",")]
     rpws = [int(r) for r in os.environ.get("STENCIL_LAB_RPW", "0").split(",")]
@@ -91,9 +103,17 @@ def main():
                 b4 = [u4.clone() for _ in range(M + 1)]
                 c4 = [u4.clone() for _ in range(M + 1)]
 
-                def deep(M=M, b4=b4):
+                rbuf = torch.empty(2 * M * T * N, dtype=torch.bfloat16, device=dev)
+
+                def deep(M=M, b4=b4, comm=False, rbuf=rbuf):
                     e0 = (M - 1) * T
+                    works = []
+                    if comm:  # both neighbours' halo payload (2 x mT rows) through RCCL, to itself
+                        flat = b4[0].view(-1)
+                        works = nx.post(4, flat, [M * T * N], [2 * M * T * N], rbuf, [0], [2 * M * T * N])
                     step(b4[0], b4[1], row0, N, halo=M * T, steps=T, row_range=(T, rows - T))
+                    for w in works:
+                        w.wait()
                     ops.stencil5_fused_spans_(b4[0], b4[1], ((-e0, T), (rows - T, rows + e0)), row0, N,
                                               halo=M * T, steps=T)
                     for ph in range(1, M):
@@ -104,6 +124,8 @@ def main():
                     e = (M - 1 - ph) * T
                     step(c4[ph], c4[ph + 1], row0, N, halo=M * T, steps=T, row_range=(-e, rows + e))
                 deeps[f"deep{M}"] = (M, deep, b4, c4)
+                if nx is not None:
+                    deeps[f"deep{M}+x"] = (M, lambda deep=deep: deep(comm=True), b4, c4)
                 del u4
 
             full()

@@ -228,6 +228,37 @@ __global__ __launch_bounds__(W * 64) void tiled_selfreset_kernel(const f32x4* a,
     }
 }
 
+// Ticket-ordered READ-ONLY stream (the reduce's traffic): persistent, next tile's loads in flight while the current
+// tile is summed; per-lane partial kept (written once so the loads stay live).
+template <int R, int W>
+__global__ __launch_bounds__(W * 64) void tsum_kernel(const f32x4* a, long long ntiles, unsigned* ticket, float* out) {
+    __shared__ unsigned s_t[2];
+    TileRegs<R, 1> va, vb;
+    f32x4 acc = {0, 0, 0, 0};
+    auto take = [&](int slot) -> long long {
+        if (threadIdx.x == 0) s_t[slot] = atomicAdd(ticket, 1u);
+        __syncthreads();
+        return (long long)s_t[slot];
+    };
+    long long ta = take(0);
+    if (ta < ntiles) {
+        tl_load<R, W, 1>(a, a, ta, va);
+        while (true) {
+            const long long tb = take(1);
+            if (tb < ntiles) tl_load<R, W, 1>(a, a, tb, vb);
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc += va.a[r];
+            if (tb >= ntiles) break;
+            ta = take(0);
+            if (ta < ntiles) tl_load<R, W, 1>(a, a, ta, va);
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc += vb.a[r];
+            if (ta >= ntiles) break;
+        }
+    }
+    if (acc.x + acc.y + acc.z + acc.w == 12345.f) out[0] = 1.f;
+}
+
 int tiled_sweep(f32x4* a, f32x4* b, f32x4* r, long long n4, unsigned* ticket, hipEvent_t e0, hipEvent_t e1) {
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -335,6 +366,34 @@ int main(int argc, char** argv) {
             });
             time("tiled copy R16W8 static x1", 2 * (double)ntc * 8192 * 16,
                  [&] { tiled_kernel<16, 8, 1, false><<<cus, 512>>>(a, b, r, ntc, ticket); });
+        }
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == 's') {  // read-only: grid-stride sum vs ticket-ordered tiles, 5 alternations
+        unsigned* ticket;
+        CK(hipMalloc(&ticket, 16));
+        int cus = 256;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        for (int rep = 0; rep < 5; ++rep) {
+            printf("-- alternation %d\n", rep);
+            time("grid sum U4 g16384", B, [&] { sum_kernel<4><<<16384, 256>>>(a, n4, out); });
+            const long long nt16 = n4 / (8 * 64 * 16), nt8 = n4 / (8 * 64 * 8);
+            time("ticket sum R16W8 x1", (double)nt16 * 8192 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tsum_kernel<16, 8><<<cus, 512>>>(a, nt16, ticket, out);
+            });
+            time("ticket sum R16W8 x2", (double)nt16 * 8192 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tsum_kernel<16, 8><<<2 * cus, 512>>>(a, nt16, ticket, out);
+            });
+            time("ticket sum R8W8 x2", (double)nt8 * 4096 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tsum_kernel<8, 8><<<2 * cus, 512>>>(a, nt8, ticket, out);
+            });
+            time("ticket sum R8W8 x4", (double)nt8 * 4096 * 16, [&] {
+                hipMemsetAsync(ticket, 0, 4);
+                tsum_kernel<8, 8><<<4 * cus, 512>>>(a, nt8, ticket, out);
+            });
         }
         return 0;
     }
