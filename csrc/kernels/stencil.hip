@@ -476,6 +476,85 @@ __device__ __forceinline__ void pipeline_v2(const __amdgpu_buffer_rsrc_t ru, con
     }
 }
 
+// ---- PAIRED waves (round 6): two vertically adjacent waves of a workgroup share their common trapezoid.
+// An unpaired wave of rows [rs, re) also computes the level rows its T-step cone reaches beyond both ends: T(T-1)
+// level rows per wave (28% extra work at 18 rows per wave, T = 6: the short slab of an N = 8 rank). In a pair the
+// upper wave marches DOWN its rows [rs, R) and the lower one UP its rows [R, re), so both reach the common boundary R
+// at the END of their march, at the same time. There the T - 1 "drain" steps trade one boundary row per level
+// through LDS instead of recomputing the other's rows: at drain step d (d = 1 .. T-1) each wave takes the partner's
+// level-d row next to R (computed at the partner's step d - 1) and publishes its own level-(d+1) row; a barrier closes
+// every drain step but the last. The outer ends keep their trapezoids (they border other workgroups). Same arithmetic
+// from the same inputs (the update is symmetric in north / south), so bit-identical. Every wave of a paired block
+// executes exactly T - 1 barriers (unpaired and empty waves execute them idly).
+template <int NP>
+struct PairXch {
+    RowP<NP> v[2][2][2][64];  // [pair][writer: 0 down, 1 up][parity of the level written][lane]
+};
+
+template <int T, int kAhead, int NP, bool UP>
+__device__ __forceinline__ void pipeline_v2_pair(const __amdgpu_buffer_rsrc_t ru, const __amdgpu_buffer_rsrc_t ro,
+                                                 unsigned vld, unsigned vst, int sr0, int pitch, int slab_rows, int halo,
+                                                 int rs, int re, float k, RowP<NP> (*mine)[64],
+                                                 const RowP<NP> (*other)[64]) {
+    using W = typename RawT<NP>::type;
+    const int lane = threadIdx.x & 63;
+    // DOWN: own rows [rs, R = re), input rows i0 = rs - T ascending to R + T - 1 (steps past R are the drain);
+    // UP:   own rows [R = rs, re), input rows i0 = re - 1 + T descending to R - T
+    const int R = UP ? rs : re;
+    const int i0 = UP ? re - 1 + T : rs - T;
+    const int nsteps = (re - rs) + 2 * T;
+    const int ilast = UP ? R - 1 : R;  // the last real input row (drain step 0)
+    auto fetch = [&](int r) __attribute__((always_inline)) {
+        const int sr = min(max(r + halo, 0), slab_rows - 1);
+        return buffer_load_row<NP>(ru, vld, (sr - sr0) * pitch);
+    };
+    RowP<NP> ring[T][3];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int p = 0; p < NP; ++p) ring[t][q].p[p] = f2{0.f, 0.f};
+    W pre[kAhead];
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) pre[j] = fetch(UP ? max(i0 - j, ilast) : min(i0 + j, ilast));
+    for (int sb = 0; sb < nsteps; sb += kAhead) {
+#pragma unroll
+        for (int j = 0; j < kAhead; ++j) {
+            const int s = sb + j;  // step index: slots are (s % 3), compile-time within the unrolled body
+            if (s < nsteps) {
+                const int i = UP ? i0 - s : i0 + s;
+                const int d = UP ? (R - 1) - i : i - R;  // drain step (>= 0)
+                const int m0 = j % 3, m1 = (j + 2) % 3, m2 = (j + 1) % 3;  // slots of the steps s, s-1, s-2
+                if (d <= 0) {
+                    ring[0][m0] = unpack_pairs<NP>(pre[j]);
+                    pre[j] = fetch(UP ? max(i - kAhead, ilast) : min(i + kAhead, ilast));
+                }
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const int r = UP ? i + t + 1 : i - t - 1;  // the level t+1 row of this step
+                    if (t + 1 < T) {
+                        if (s <= 2 * t + 1) continue;  // outside the wave's outer trapezoid
+                        if (UP ? r < R : r >= R) {     // the partner's row: its value arrives through LDS
+                            if (t == d - 1) ring[t + 1][m0] = other[d & 1][lane];
+                            continue;
+                        }
+                        W unused;
+                        level_pairs<false, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k, ring[t + 1][m0], unused);
+                        if (d >= 0 && t == d) mine[(d + 1) & 1][lane] = ring[t + 1][m0];  // own row next to R
+                    } else if (UP ? r < re : r >= rs) {
+                        W pk;
+                        RowP<NP> unused;
+                        level_pairs<true, NP>(ring[t][m2], ring[t][m1], ring[t][m0], k, unused, pk);
+                        buffer_store_row<NP>(pk, ro, vst, (r + halo - sr0) * pitch);
+                    }
+                }
+                if (d >= 0 && d <= T - 2) __syncthreads();
+            }
+        }
+    }
+}
+
 // MINW: minimum waves per SIMD the register allocation must allow (__launch_bounds__'s second argument): a short
 // slab has few waves, so fitting one more per SIMD (T=4: 138 -> <= 128 VGPRs, 3 -> 4 waves) can matter more than
 // the few rematerialised values it costs.
@@ -514,6 +593,93 @@ __global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2_kernel(const un
     else
         pipeline_v2<T, kAhead, G::NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, i0, i1, k);
 }
+
+// The block's rows [brs, bre) (all waves of a block lie in one span).
+__device__ __forceinline__ void block_rows(const RowSpans& sp, int& brs, int& bre) {
+    int by = (int)blockIdx.y, base = sp.a0, lim = sp.a1;
+    if (by >= sp.nby_a) by -= sp.nby_a, base = sp.b0, lim = sp.b1;
+    brs = base + by * (kWaves * sp.rpw);
+    bre = min(lim, brs + kWaves * sp.rpw);
+}
+
+// The paired form of stencil5xT2_kernel (see pipeline_v2_pair): waves 2p / 2p+1 march down / up and meet. A block
+// that holds a Dirichlet row or column anywhere in reach runs the unpaired per-wave paths (no barriers at all);
+// otherwise every wave executes exactly T - 1 barriers.
+template <int T, int kAhead, int MINW = 1, int CPL = 8>
+__global__ __launch_bounds__(kWaves * 64, MINW) void stencil5xT2p_kernel(const unsigned short* __restrict__ u,
+                                                                   unsigned short* __restrict__ out, int rows, int cols,
+                                                                   int ld, int halo, RowSpans sp, long long grow0,
+                                                                   long long grows, float k) {
+    using G = Geo<CPL, T>;
+    constexpr int NP = G::NP;
+    static_assert(kAhead % 3 == 0, "ring slots must be compile-time");
+    __shared__ PairXch<NP> xch;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int c0 = G::c0(lane);
+    int rs, re, brs, bre;
+    wave_rows(sp, wave, rs, re);
+    block_rows(sp, brs, bre);
+    const bool in_grid = c0 + CPL <= cols;
+    const bool store_lane = G::store_lane(lane, cols, in_grid);
+    const bool fix0 = c0 == 0, fixl = c0 + CPL == cols;
+    const int slab_rows = rows + 2 * halo;
+    const int pitch = ld * 2;
+    const unsigned vld = in_grid ? (unsigned)c0 * 2 : 0x80000000u;
+    const unsigned vst = store_lane ? (unsigned)c0 * 2 : 0x80000000u;
+    // block-uniform: the strip's columns are the same for every wave, the row test covers the block's whole reach
+    const long long g0 = grow0 + brs - 2 * T, g1 = grow0 + bre + 2 * T;
+    const bool block_slow = (g0 <= 0 && 0 <= g1) || (g0 <= grows - 1 && grows - 1 <= g1) ||
+                            __builtin_amdgcn_ballot_w64(fix0 || fixl) != 0;
+    auto descriptors = [&](int lo, int hi, __amdgpu_buffer_rsrc_t& ru, __amdgpu_buffer_rsrc_t& ro, int& sr0) {
+        sr0 = min(max(lo + halo, 0), slab_rows - 1);
+        const int sr1 = min(max(hi + halo, 0), slab_rows - 1) + 1;
+        const unsigned bytes = (unsigned)((size_t)(sr1 - sr0) * (size_t)pitch);
+        ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(u) + (size_t)sr0 * ld, (short)0, (int)bytes,
+                                               0x00020000);
+        ro = __builtin_amdgcn_make_buffer_rsrc(out + (size_t)sr0 * ld, (short)0, (int)bytes, 0x00020000);
+    };
+    if (block_slow) {  // exactly the unpaired kernel's per-wave paths
+        if (rs >= re) return;
+        const long long w0 = grow0 + rs - 2 * T, w1 = grow0 + re + T - 2;
+        const bool edge_rows = (w0 <= 0 && 0 <= w1) || (w0 <= grows - 1 && grows - 1 <= w1);
+        if (edge_rows || __builtin_amdgcn_ballot_w64(fix0 || fixl) != 0) {
+            stencil5xT_body<T, kAhead, CPL>(u, out, rows, cols, ld, halo, rs, re, grow0, grows, k);
+        } else {
+            __amdgpu_buffer_rsrc_t ru, ro;
+            int sr0;
+            descriptors(rs - T, re + T - 1, ru, ro, sr0);
+            pipeline_v2<T, kAhead, NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, rs - T, re + T, k);
+        }
+        return;
+    }
+    const int pair = wave >> 1;
+    const bool up = (wave & 1) != 0;
+    int prs, pre;  // the partner's rows
+    wave_rows(sp, wave ^ 1, prs, pre);
+    const bool paired = up ? rs < re : prs < pre;  // the pair exists iff its lower (up) wave has rows
+    if (!paired) {
+        if (rs < re) {  // an upper wave whose partner is empty: the unpaired pipeline (both trapezoids)
+            __amdgpu_buffer_rsrc_t ru, ro;
+            int sr0;
+            descriptors(rs - T, re + T - 1, ru, ro, sr0);
+            pipeline_v2<T, kAhead, NP>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, rs - T, re + T, k);
+        }
+        for (int b = 0; b < T - 1; ++b) __syncthreads();  // the paired waves' drain barriers
+        return;
+    }
+    __amdgpu_buffer_rsrc_t ru, ro;
+    int sr0;
+    if (up) {
+        descriptors(rs - 1, re - 1 + T, ru, ro, sr0);
+        pipeline_v2_pair<T, kAhead, NP, true>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, re, k, xch.v[pair][1],
+                                              xch.v[pair][0]);
+    } else {
+        descriptors(rs - T, re, ru, ro, sr0);
+        pipeline_v2_pair<T, kAhead, NP, false>(ru, ro, vld, vst, sr0, pitch, slab_rows, halo, rs, re, k,
+                                               xch.v[pair][0], xch.v[pair][1]);
+    }
+}
 #pragma clang fp contract(on)
 }  // namespace
 
@@ -532,6 +698,12 @@ extern "C" int pcmx_stencil5_bf16(const void* u, void* out, int rows, int cols, 
 }
 
 namespace {
+// The production choice of paired waves (stencil5xT2p_kernel) for a launch: see pcmx_stencil5xT_bf16_spans_shape.
+bool PairedDefault(int steps, bool edge, int rpw) {
+    (void)steps, (void)edge, (void)rpw;
+    return false;  // measured, not adopted (see the launch rule)
+}
+
 // strips covering `cols` columns (see Geo): the first strip whose loaded range [x*OUT, x*OUT + 64*CPL) reaches cols
 // is the last one
 int strips_for(int cols, int cpl, int steps) {
@@ -561,8 +733,9 @@ extern "C" int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int ro
         (((uintptr_t)u | (uintptr_t)out) & 15))
         return -1;
     const int o_cpl = shape & 0xff, o_rpw = (shape >> 8) & 0xff, o_ahead = (shape >> 16) & 0xff;
+    const int o_pair = (shape >> 24) & 0x3;  // 1: paired waves, 2: unpaired, 0: the rule below
     if ((o_cpl != 0 && o_cpl != 4 && o_cpl != 8) || (o_ahead != 0 && o_ahead != 3 && o_ahead != 6 && o_ahead != 9) ||
-        (shape >> 24) != 0)
+        (shape >> 26) != 0 || o_pair == 3)
         return -1;
     const bool top_global = global_row0 == 0, bot_global = global_row0 + rows == global_rows;
     const int lo_lim = top_global ? 0 : -max(0, halo - steps), hi_lim = bot_global ? rows : rows + max(0, halo - steps);
@@ -619,13 +792,29 @@ extern "C" int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int ro
     // prefetch ring depth (rows in flight per wave; a multiple of 3, see stencil5xT_body)
     int ahead = (steps >= 6 && rpw >= 64) ? 9 : (rpw <= 4 || (rpw > 16 && rpw <= 20)) ? 3 : 6;
     if (o_ahead) ahead = o_ahead;
+    // paired waves (stencil5xT2p_kernel): the two waves of a pair share their common trapezoid through LDS. A lab
+    // shape only (T = 6 with 4 columns per lane, the N = 8 short slab; any other paired shape is refused): bit-exact,
+    // but no faster — the pair's T - 1 drain hand-offs keep the wave's critical path, and the extra code raises the
+    // kernel from 88 to 110 VGPRs (5 -> 4 waves per SIMD; forcing 5 spills and runs 1.8x slower):
+    // profiles/r6_stencil/README.md.
+    bool paired = PairedDefault(steps, edge, rpw);
+    if (o_pair) paired = o_pair == 1;
+    if (steps < 3 || rpw < steps) paired = false;
     const int per = kWaves * rpw;
     const RowSpans sp{r0a, r1a, r0b, r1b, (r1a - r0a + per - 1) / per, rpw};
     const dim3 g(strips_for(cols, steps == 2 ? 8 : cpl, steps), sp.nby_a + (r1b - r0b + per - 1) / per);
 #define PCMX_STENCIL_V2_KA(T, KA, C)                                                                                \
     case KA:                                                                                                        \
-        stencil5xT2_kernel<T, KA, 1, C><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0,    \
-                                                                   global_rows, k);                                 \
+        if (paired) {                                                                                               \
+            if constexpr (T == 6 && C == 4)                                                                         \
+                stencil5xT2p_kernel<T, KA, 1, C><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp,        \
+                                                                            global_row0, global_rows, k);           \
+            else                                                                                                    \
+                return -1;                                                                                          \
+        } else {                                                                                                    \
+            stencil5xT2_kernel<T, KA, 1, C><<<g, kWaves * 64, 0, s>>>(ui, uo, rows, cols, ld, halo, sp, global_row0, \
+                                                                       global_rows, k);                             \
+        }                                                                                                           \
         break;
 #define PCMX_STENCIL_V2C(T, C)                                                                                      \
     switch (ahead) {                                                                                                \

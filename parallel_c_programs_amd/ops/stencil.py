@@ -97,11 +97,14 @@ def stencil5_fused_spans_(u: torch.Tensor, out: torch.Tensor, spans, global_row0
     return out
 
 
-def launch_shape(cpl: int = 0, rpw: int = 0, ahead: int = 0) -> int:
-    """The `shape` word of an explicit stencil launch shape (each field 0: the production rule's value)."""
+def launch_shape(cpl: int = 0, rpw: int = 0, ahead: int = 0, paired: bool | None = None) -> int:
+    """The `shape` word of an explicit stencil launch shape (each field 0 / None: the production rule's value).
+    paired: True = paired waves (two vertically adjacent waves share their common trapezoid through LDS, round 6),
+    False = independent waves."""
     if cpl not in (0, 4, 8) or not 0 <= rpw <= 255 or ahead not in (0, 3, 6, 9):
         raise ValueError("launch_shape: cpl 0/4/8, rpw 0..255, ahead 0/3/6/9")
-    return cpl | (rpw << 8) | (ahead << 16)
+    pair = 0 if paired is None else (1 if paired else 2)
+    return cpl | (rpw << 8) | (ahead << 16) | (pair << 24)
 
 
 def stencil5x2_step_(u, out, global_row0=0, global_rows=None, k=DEFAULT_K, halo=1, row_range=None):

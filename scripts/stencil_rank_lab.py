@@ -15,7 +15,8 @@ Run: python scripts/stencil_rank_lab.py [fuse ...]
 Env: STENCIL_LAB_WORLDS=8 (subset of 1,2,4,8), STENCIL_LAB_RPW=0,18 (rows per wave forced on the non-edge launches
 as an explicit launch shape of each call, ops.stencil.launch_shape; 0 = production rule; one line per value, all in one
 process for an A/B); STENCIL_LAB_DEEP=2,3,4 (halo depths m); STENCIL_LAB_ONLY=full (subset of full, split3, split2, split2c); STENCIL_LAB_AHEAD=3 / 6 / 9 (prefetch ring
-of the forced shapes); STENCIL_LAB_CPL=4 / 8 (columns per lane of the forced shapes); STENCIL_LAB_RCCL=1 (round 6:
+of the forced shapes); STENCIL_LAB_CPL=4 / 8 (columns per lane of the forced shapes); STENCIL_LAB_PAIRED=0,1 (round 6:
+paired waves off / on for the non-edge launches, one line per value); STENCIL_LAB_RCCL=1 (round 6:
 each deep-halo variant also runs WITH its exchange: the real halo bytes, 2 x mT rows, through the native exchange on a
 world-1 RCCL communicator, posted before the interior launch and waited before the edge launch as StencilSlab.step
 does; printed as deepM+x).
@@ -60,8 +61,10 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1)
     worlds = [int(w) for w in os.environ.get("STENCIL_LAB_WORLDS", "1,2,4,8").split(",")]
     rpws = [int(r) for r in os.environ.get("STENCIL_LAB_RPW", "0").split(",")]
-    for T, world, rpw in [(T, w, r) for T in fuses for w in worlds for r in rpws]:
-        shape = launch_shape(int(os.environ.get("STENCIL_LAB_CPL", "0")), rpw, int(os.environ.get("STENCIL_LAB_AHEAD", "0")))
+    pairs = [{"": None, "1": True, "0": False}[p] for p in os.environ.get("STENCIL_LAB_PAIRED", "").split(",")]
+    for T, world, rpw, paired in [(T, w, r, p) for T in fuses for w in worlds for r in rpws for p in pairs]:
+        shape = launch_shape(int(os.environ.get("STENCIL_LAB_CPL", "0")), rpw, int(os.environ.get("STENCIL_LAB_AHEAD", "0")),
+                             paired)
 
         def step(*a, shape=shape, **kw):  # the non-edge launches take the forced rows per wave
             return ops.stencil5_fused_step_(*a, shape=shape, **kw)
@@ -148,7 +151,7 @@ def main():
                 res[name] = (timed(fn), same)
             line = " ".join(f"{k} {ms:.4f} ms {rows * N * T / ms / 1e6:7.0f} GLUP/s{'' if ok else ' MISMATCH'}"
                             for k, (ms, ok) in res.items())
-            tag = f" rpw={rpw}" if rpw else ""
+            tag = (f" rpw={rpw}" if rpw else "") + ("" if paired is None else f" paired={int(paired)}")
             print(f"fuse={T} N={world} rows={rows:5d}{tag}  {line}", flush=True)
             del u, ref, out, deeps
             torch.cuda.empty_cache()

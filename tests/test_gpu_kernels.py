@@ -283,6 +283,45 @@ def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
         ops.stencil5_fused_step_(a, b, 0, rows, halo=1, steps=steps, shape=5)  # 5 columns per lane: refused
 
 
+@pytest.mark.parametrize("steps", [6])
+def test_stencil_paired_waves_bit_identical(gpu, steps):
+    """Paired waves (round 6, stencil5xT2p_kernel: two vertically adjacent waves march down / up and trade their
+    common trapezoid through LDS; a measured, not adopted lab shape) give the bits of the unpaired kernel and of the CPU oracle: a rank's slab inside a
+    larger grid (no Dirichlet row in reach, so the paired path runs), rows per wave from T up, last blocks whose lower
+    wave has 1 row, several rows, or none, a two-span launch, and a slab touching the global edge (the unpaired
+    fall-back of such blocks)."""
+    from parallel_c_programs_amd.ops.stencil import launch_shape
+
+    cols = 1032
+    for rpw in sorted({steps, steps + 1, 18, 24, 64}):
+        for rows in (4 * rpw + rpw + 1, 8 * rpw + 3, 4 * rpw + 2 * rpw, 2 * rpw):
+            g = torch.Generator().manual_seed(rows * 31 + rpw + steps)
+            u = (torch.rand(rows + 2 * steps, cols, generator=g) * 4 - 2).to(torch.bfloat16)
+            for row0, grows in ((5000, 100000), (0, rows)):
+                ref = u.clone()
+                ops.stencil5_fused_step_(u, ref, row0, grows, halo=steps, steps=steps)  # CPU oracle
+                a = u.to(gpu)
+                for paired in (True, False):
+                    b = torch.zeros_like(a)
+                    ops.stencil5_fused_step_(a, b, row0, grows, halo=steps, steps=steps,
+                                             shape=launch_shape(4, rpw, 0, paired))
+                    got = b.cpu()[steps:-steps].view(torch.int16)
+                    assert torch.equal(got, ref[steps:-steps].view(torch.int16)), (rpw, rows, row0, paired)
+            # two spans in one launch (the distributed step's edge bands, here wide enough for pairs)
+            row0, grows = 5000, 100000
+            ref = u.clone()
+            ops.stencil5_fused_step_(u, ref, row0, grows, halo=steps, steps=steps)
+            a = u.to(gpu)
+            b = a.clone()
+            mid = rows // 2
+            ops.stencil5_fused_spans_(a, b, ((0, mid - 7), (mid + 5, rows)), row0, grows, halo=steps, steps=steps,
+                                      shape=launch_shape(4, rpw, 0, True))
+            ops.stencil5_fused_step_(a, b, row0, grows, halo=steps, steps=steps, row_range=(mid - 7, mid + 5))
+            assert torch.equal(b.cpu()[steps:-steps].view(torch.int16), ref[steps:-steps].view(torch.int16)), (rpw, rows)
+    with pytest.raises(RuntimeError):  # paired waves exist for T = 6 with 4 columns per lane only (a lab shape)
+        ops.stencil5_fused_step_(a, b, 5000, 100000, halo=steps, steps=steps, shape=launch_shape(8, 24, 0, True))
+
+
 @pytest.mark.parametrize("steps", [2, 4, 6])
 @pytest.mark.parametrize("global_row0,global_rows", [(0, 300), (40, 340), (40, 300)])
 def test_stencil_fused_deep_halo_slab_and_row_split(gpu, global_row0, global_rows, steps):
