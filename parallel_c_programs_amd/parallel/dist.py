@@ -176,16 +176,24 @@ class NativeExchange:
     def __init__(self, ctx: Context):
         from .. import _C
 
-        self.C, self.device = _C, ctx.device.index
+        self.C, self.device, self.handle = _C, ctx.device.index, 0
         obj = [_C.xcomm_unique_id() if ctx.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        self.handle = _C.xcomm_create(obj[0], ctx.world, ctx.rank, self.device)
         # proven before first use: one float to / from every peer, host-waited with a timeout (a hung or failed probe
-        # aborts the communicator), then agreed over the job's own process group; any failure -> the torch path
-        rc = _C.xcomm_probe(self.handle, int(float(os.environ.get("PCMX_XCOMM_PROBE_S", "60")) * 1000))
+        # aborts the communicator), then agreed over the job's own process group — a failure on ANY rank (creation
+        # included) sends every rank to the torch path together, so no rank is left in a collective the others skip
+        rc = 0
+        try:
+            self.handle = _C.xcomm_create(obj[0], ctx.world, ctx.rank, self.device)
+        except RuntimeError:
+            rc = -1
+        if self.handle:
+            rc = _C.xcomm_probe(self.handle, int(float(os.environ.get("PCMX_XCOMM_PROBE_S", "60")) * 1000))
+        if os.environ.get("PCMX_XCOMM_FAIL_RANK") == str(ctx.rank):  # test hook: this rank reports a failed probe
+            rc = rc or -2
         if ctx.max_over_ranks(0.0 if rc == 0 else 1.0) != 0.0:
             self.close()
-            raise RuntimeError(f"native exchange probe failed (rank {ctx.rank}: rc {rc})")
+            raise RuntimeError(f"native exchange unavailable (rank {ctx.rank}: rc {rc})")
 
     def post(self, slot, send, soff, scnt, recv, roff, rcnt) -> list:
         self.C.xcomm_exchange(self.handle, int(slot), send, soff, scnt, recv, roff, rcnt)

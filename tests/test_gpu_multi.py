@@ -375,6 +375,33 @@ print("deferred spmv pipeline on rccl ok", err2)
 dist.destroy_process_group()
 """
 
+_NATIVE_FALLBACK_SCRIPT = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["PCMX_ROOT"])
+from parallel_c_programs_amd.parallel.dist import init, native_exchange, native_exchange_active
+os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", PCMX_XCOMM_FAIL_RANK="0")
+ctx = init()
+if not dist.is_initialized():
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=ctx.device)
+ctx.backend, ctx.world = "nccl", 1
+dev = ctx.device
+class Ctx(type(ctx)):
+    @property
+    def distributed(self):
+        return True
+c = Ctx(0, 1, 0, dev, "nccl")
+# a rank that reports a failed probe sends the job to the torch path (the communicator closed, no exception)
+assert native_exchange(c) is None and not native_exchange_active(c)
+snd = torch.arange(10, dtype=torch.float32, device=dev) + 1
+rcv = torch.zeros(16, device=dev)
+for w in c.exchange_segments(3, snd, [2], [5], rcv, [9], [5]):
+    w.wait()
+torch.cuda.synchronize()
+assert torch.equal(rcv[9:14], snd[2:7]), rcv
+print("native fallback ok")
+dist.destroy_process_group()
+"""
+
 _ITERATE_SCRIPT = r"""
 import os, sys, torch
 sys.path.insert(0, os.environ["PCMX_ROOT"])
@@ -412,6 +439,19 @@ def test_neighbour_exchange_rccl_call_shape(gpu, tmp_path):
     assert r.returncode == 0 and "neighbour_exchange ok" in r.stdout, r.stderr[-3000:]
     assert "rccl call shapes ok" in r.stdout and "distributed spmv/scan branches ok" in r.stdout, r.stderr[-3000:]
     assert "deferred spmv pipeline on rccl ok" in r.stdout, r.stderr[-3000:]
+    assert "native exchange ok" in r.stdout, r.stderr[-3000:]
+
+
+def test_native_exchange_probe_failure_falls_back(gpu, tmp_path):
+    """A rank whose native-exchange probe fails (test hook PCMX_XCOMM_FAIL_RANK) makes the job agree on the torch
+    path: native_exchange() returns None, the dedicated communicator is closed, and exchanges still deliver."""
+    from parallel_c_programs_amd.parallel import free_port
+
+    script = tmp_path / "fallback.py"
+    script.write_text(_NATIVE_FALLBACK_SCRIPT)
+    env = dict(cli_env(), PCMX_ROOT=str(ROOT), MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "native fallback ok" in r.stdout, r.stderr[-3000:]
 
 
 @pytest.mark.parametrize("world", [2, 4])
