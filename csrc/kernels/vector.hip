@@ -242,11 +242,13 @@ inline int stream_grid(long long n, int per_thread) {
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-int device_cus() {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 256;
-    return cus > 0 ? cus : 256;
+int device_cus() {  // cached per device (no attribute query on the launch path)
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+    return cus[dev] > 0 ? cus[dev] : 256;
 }
 
 // The self-resetting counter pair of (device, stream), allocated and zeroed on first use (kept for the process);
