@@ -7,7 +7,7 @@
 // step, so the GPU idled between launches (profiles/r6_spmv/). This path issues the same grouped ncclSend / ncclRecv
 // per peer straight from C++ on the communicator's own stream, ordered against the caller's stream with two events:
 //   exchange(slot): record `ready[slot]` on the compute stream -> the comm stream waits for it -> ncclGroupStart,
-//                   one ncclSend / ncclRecv per peer with data (offsets and counts in floats), ncclGroupEnd ->
+//                   one ncclSend / ncclRecv per peer with data (offsets and counts in bytes), ncclGroupEnd ->
 //                   record `done[slot]` on the comm stream;
 //   wait(slot):     the compute stream waits for `done[slot]` (no host sync).
 // A slot is one exchange in flight (the SpMV step keeps one per row chunk). The communicator is separate from
@@ -67,7 +67,12 @@ extern "C" int pcmx_xcomm_create(const void* id, int world, int rank, int device
     for (int s = 0; rc == 0 && s < kSlots; ++s)
         if (hipEventCreateWithFlags(&x->ready[s], rf) != hipSuccess || hipEventCreateWithFlags(&x->done[s], df) != hipSuccess)
             rc = PCMX_ERR_COMM;
-    if (rc != 0) {
+    if (rc != 0) {  // release whatever was created before the failure
+        for (int s = 0; s < kSlots; ++s) {
+            if (x->ready[s]) (void)hipEventDestroy(x->ready[s]);
+            if (x->done[s]) (void)hipEventDestroy(x->done[s]);
+        }
+        if (x->stream) (void)hipStreamDestroy(x->stream);
         if (x->comm) ncclCommDestroy(x->comm);
         delete x;
         return rc;
