@@ -11,7 +11,7 @@ def main():
     which = int(sys.argv[3]) if len(sys.argv) > 3 else -5
     before = float(sys.argv[4]) if len(sys.argv) > 4 else 250.0
     after = float(sys.argv[5]) if len(sys.argv) > 5 else 120.0
-    c = sqlite3.connect(db)
+    c = sqlite3.connect(f"file:{db}?mode=ro", uri=True)  # read-only: a wrong path fails instead of creating a file
     ks = c.execute("select name, start, end, stream_id, corr_id from kernels where name like ? order by start",
                    (f"%{sub}%",)).fetchall()
     if not ks:

@@ -9,7 +9,7 @@ import sys
 
 def main():
     db, sub = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "")
-    c = sqlite3.connect(db)
+    c = sqlite3.connect(f"file:{db}?mode=ro", uri=True)  # read-only: a wrong path fails instead of creating a file
     rows = c.execute("select name, grid_x, workgroup_x, duration from kernels order by start").fetchall()
     runs, index = [], {}
     for name, gx, wx, dur in rows:
