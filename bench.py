@@ -466,6 +466,7 @@ def main(argv=None):
                     del ybuf
             if runner.injected(name, "perturb") and mode == "weak":
                 if name == "reduce":
+                    w.settle()  # (the last timed all-reduce's total stored first, then perturbed)
                     w.total.mul_(1.001)
                 else:
                     w.y[w.y.numel() // 3] += 1.0

@@ -97,20 +97,39 @@ class Sgemm(Workload):
 
 
 class Reduce(Workload):
-    """Global sum of world x n f32: local HBM-bound reduction + one-scalar RCCL all-reduce."""
+    """Global sum of world x n f32: local HBM-bound reduction + one-scalar RCCL all-reduce.
+
+    With several ranks a step's all-reduce is left in flight on RCCL's stream and overlaps the NEXT step's local
+    reduction: step k launches its reduction, then makes the compute stream wait for step k-1's all-reduce and stores
+    that global total, then posts its own all-reduce. Every all-reduce is enqueued inside the step that computed its
+    input and completes on the device before the bench's closing synchronize; settle() (called by check()) stores the
+    last one's total."""
 
     def __init__(self, ctx, n=10**9, **_):
         super().__init__(ctx, {"n": n}, "reduce", "GB/s")
         self.x = torch.empty(int(n), device=ctx.device)
         ops.rand_uniform_(self.x, 3000 + ctx.rank, 0.0, 1.0)
         self.total = torch.zeros((), device=ctx.device)
+        self._pending = None  # (work, partial sum) of the all-reduce still in flight
 
     def step(self):
         s = ops.reduce(self.x, "sum").reshape(1).float()
-        self.ctx.all_reduce_(s)
-        self.total.copy_(s.reshape(()))
+        if not self.ctx.distributed:
+            self.total.copy_(s.reshape(()))
+            return
+        self.settle()
+        self._pending = (self.ctx.all_reduce_async(s), s)
+
+    def settle(self):
+        """The compute stream waits for the all-reduce in flight (if any) and stores its global total."""
+        if self._pending is not None:
+            work, s = self._pending
+            self._pending = None
+            work.wait()
+            self.total.copy_(s.reshape(()))
 
     def compute_only_step(self):
+        self.settle()
         self.total.copy_(ops.reduce(self.x, "sum").reshape(()).float())
 
     def bytes_exchanged_per_step(self):
@@ -120,6 +139,7 @@ class Reduce(Workload):
         return 4.0 * self.x.numel()
 
     def check(self, reduce: bool = True):
+        self.settle()
         ref = self.x.double().sum().reshape(1)
         self.ctx.all_reduce_(ref)  # (the one collective, before the local comparison)
         e = abs(self.total.item() - ref.item()) / max(abs(ref.item()), 1e-300)

@@ -45,6 +45,13 @@ class Context:
             dist.all_reduce(t, op=_OPS[op])
         return t
 
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum"):
+        """In-place all-reduce left in flight: returns the work whose wait() orders the caller's stream after it (None
+        when not distributed). Lets a step's collective overlap the next step's compute (Reduce.step)."""
+        if not self.distributed:
+            return None
+        return dist.all_reduce(t, op=_OPS[op], async_op=True)
+
     def all_gather(self, t: torch.Tensor) -> list[torch.Tensor]:
         if not self.distributed:
             return [t]
