@@ -173,6 +173,28 @@ def test_global_reduce_and_scan_world3():
     assert torch.allclose(ys, torch.cumsum(cat, 0), rtol=1e-5, atol=1e-3)
 
 
+def _reduce_overlap(ctx, q):
+    """Reduce workload: each step's all-reduce stays in flight behind the next step (round 6)."""
+    from parallel_c_programs_amd.models import workloads as W
+
+    w = W.Reduce(ctx, n=5000)
+    inflight = []
+    for _ in range(3):
+        w.step()
+        inflight.append(w._pending is not None)
+    c = w.check(reduce=True)
+    q.put((ctx.rank, (inflight, w._pending is None, float(w.total), c["check_passed"], float(w.x.double().sum()))))
+
+
+def test_reduce_workload_overlapped_allreduce_world2():
+    res = _collect(2, _reduce_overlap)
+    total = sum(res[r][4] for r in range(2))
+    for r in range(2):
+        inflight, settled, got, passed, _ = res[r]
+        assert inflight == [True, True, True] and settled and passed
+        assert abs(got - total) <= 1e-5 * total
+
+
 def _region(ctx, q, path):
     img = torch.from_numpy(bmp.read(path)) if ctx.is_root else None
     stats = {}
