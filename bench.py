@@ -16,8 +16,9 @@ max) and its longest host enqueue:
            against an fp64 GEMM; the hipBLASLt torch.matmul of the same operands is timed alongside for reference,
            and so is the fp32 GEMM on the bf16 matrix cores (exact 3-way operand split, 6 piece products: fp32
            accuracy, its own full fp64 check; an extra field, never the headline value)
-  reduce   global sum, local HBM reduce + one-scalar RCCL all-reduce: weak (1e9 f32 per GPU) and strong
-           (1e9 f32 in total, 1e9/N per GPU); fp64 check
+  reduce   global sum, local HBM reduce + one-scalar RCCL all-reduce (left in flight behind the next step's local
+           reduce, completed inside the timed region): weak (1e9 f32 per GPU) and strong (1e9 f32 in total, 1e9/N
+           per GPU); fp64 check of the last step's global total
   scan     global inclusive prefix sum over the rank-ordered concatenation (reduce-then-scan): weak and
            strong like reduce; fp64 check of EVERY output of every rank incl. its rank offset, and the stream's
            look-back error word
