@@ -3,6 +3,7 @@ exposes step() (one timed unit of work, including its collectives) and report(se
 throughput = sum over ranks), and check() (a numerics check against an independent reference)."""
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -111,10 +112,12 @@ class Reduce(Workload):
         ops.rand_uniform_(self.x, 3000 + ctx.rank, 0.0, 1.0)
         self.total = torch.zeros((), device=ctx.device)
         self._pending = None  # (work, partial sum) of the all-reduce still in flight
+        self.overlap = os.environ.get("PCMX_REDUCE_OVERLAP", "1") != "0"  # 0: the round-5 blocking all-reduce
 
     def step(self):
         s = ops.reduce(self.x, "sum").reshape(1).float()
-        if not self.ctx.distributed:
+        if not self.ctx.distributed or not self.overlap:
+            self.ctx.all_reduce_(s)
             self.total.copy_(s.reshape(()))
             return
         self.settle()
@@ -222,11 +225,14 @@ class Scan(Workload):
         # 4 B/element reduce pass that seeds each rank's offset counts as time, not as work
         return 8.0 * self.x.numel()
 
-    def check(self, reduce: bool = True, chunk: int = 1 << 26):
+    def check(self, reduce: bool = True, chunk: int = 1 << 26, one_rank_at_a_time: bool = False):
         """Every output of the timed scan (all n, not a prefix) against an fp64 cumsum carried across chunks, seeded
         with this rank's offset (the fp64 sum of the lower ranks' totals), and the look-back error word of the
         stream (lookback_ok False if any timed scan gave up a look-back). The totals' all-gather runs first: a rank
-        whose stream reports a timed-out look-back still joins it, then reports the flag instead of raising."""
+        whose stream reports a timed-out look-back still joins it, then reports the flag instead of raising.
+        one_rank_at_a_time (ranks sharing one GPU): the ranks take turns for the fp64 cumsums, behind barriers.
+        torch.cumsum is rocPRIM's look-back scan, which waits on blocks by index, and several processes' copies of it
+        on one GPU can starve each other's predecessors."""
         tot = self.x.double().sum().reshape(1)
         totals = self.ctx.all_gather(tot)
         lookback_ok = True
@@ -240,10 +246,18 @@ class Scan(Workload):
             carry = carry + t.to(carry.device).reshape(())
         err = torch.zeros((), dtype=torch.float64, device=self.x.device)
         n = self.x.numel()
-        for s in range(0, n, chunk):
-            ref = torch.cumsum(self.x[s:s + chunk].double(), 0) + carry
-            err = torch.maximum(err, (self.y[s:s + chunk].double() - ref).abs().max())
-            carry = ref[-1]
+        for turn in range(self.ctx.world if one_rank_at_a_time else 1):
+            if one_rank_at_a_time and turn != self.ctx.rank:
+                self.ctx.barrier()
+                continue
+            for s in range(0, n, chunk):
+                ref = torch.cumsum(self.x[s:s + chunk].double(), 0) + carry
+                err = torch.maximum(err, (self.y[s:s + chunk].double() - ref).abs().max())
+                carry = ref[-1]
+            if one_rank_at_a_time:
+                if self.x.is_cuda:
+                    torch.cuda.synchronize(self.x.device)
+                self.ctx.barrier()
         # relative to this rank's largest prefix (its last one: the inputs are non-negative)
         e = (err / carry.abs().clamp_min(1e-30)).item()
         if reduce:

@@ -195,6 +195,24 @@ def test_reduce_workload_overlapped_allreduce_world2():
         assert abs(got - total) <= 1e-5 * total
 
 
+def _scan_turns(ctx, q):
+    from parallel_c_programs_amd.models import workloads as W
+
+    w = W.Scan(ctx, n=3000)
+    w.step()
+    a = w.check(reduce=True, chunk=1000)
+    b = w.check(reduce=True, chunk=1000, one_rank_at_a_time=True)
+    q.put((ctx.rank, (a["check_passed"], b["check_passed"], a["rel_err_vs_fp64"], b["rel_err_vs_fp64"])))
+
+
+def test_scan_check_one_rank_at_a_time_world3():
+    """The shared-GPU form of the scan check (ranks take turns for the fp64 cumsums) gives the same verdict."""
+    res = _collect(3, _scan_turns)
+    for r in range(3):
+        pa, pb, ea, eb = res[r]
+        assert pa and pb and ea == eb
+
+
 def _region(ctx, q, path):
     img = torch.from_numpy(bmp.read(path)) if ctx.is_root else None
     stats = {}
