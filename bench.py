@@ -178,8 +178,7 @@ def rocsparse_bar(n_rows: int, nnz: int, reps: int, warmup: int, rows: tuple[int
 
 def ranks_share_gpu(ctx) -> bool:
     """More ranks on this node than GPUs (gloo rehearsals): the same answer on every rank of the node."""
-    return (ctx.distributed and ctx.device.type == "cuda"
-            and int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world)) > torch.cuda.device_count())
+    return ctx.distributed and int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world)) > torch.cuda.device_count()
 
 
 def rocsparse_bar_ranks(ctx, n_rows: int, nnz: int, reps: int, warmup: int, rows: tuple[int, int]) -> dict:
@@ -482,7 +481,8 @@ def main(argv=None):
                 else:
                     w.y[w.y.numel() // 3] += 1.0
             yield
-            c = w.check(reduce=False, **({"one_rank_at_a_time": True} if name == "scan" and ranks_share_gpu(ctx) else {}))
+            turns = name == "scan" and dev.type == "cuda" and ranks_share_gpu(ctx)
+            c = w.check(reduce=False, **({"one_rank_at_a_time": True} if turns else {}))
             chk.error(f"{name}_{mode}_rel_err_vs_fp64", c["rel_err_vs_fp64"], LIM)
             if name == "scan":  # every timed output checked (not a prefix), rank offsets included
                 chk.flag(f"scan_{mode}_lookback_ok", c["lookback_ok"])
