@@ -87,6 +87,10 @@ at::Tensor copy_(at::Tensor dst, const at::Tensor& src) {
     TORCH_CHECK(src.numel() == dst.numel() && src.device() == dst.device(), "copy_: size / device mismatch");
     const at::DeviceGuard g(dst.device());
     auto sc = aligned_contig(src);
+    // tiles run in any order: a source that partly overlaps the destination is copied out first (memmove semantics)
+    const auto s0 = reinterpret_cast<uintptr_t>(sc.data_ptr()), d0 = reinterpret_cast<uintptr_t>(dst.data_ptr());
+    const uintptr_t nb = (uintptr_t)dst.numel() * sizeof(float);
+    if (s0 != d0 && s0 < d0 + nb && d0 < s0 + nb) sc = sc.clone();
     check_rc(pcmx_copy_f32(sc.data_ptr<float>(), dst.data_ptr<float>(), dst.numel(), cur_stream(dst)), "copy_");
     return dst;
 }

@@ -42,6 +42,23 @@ def test_ticket_streams_copy_fill_exact(gpu, n):
         assert bool((d == 1.25).all())
 
 
+def test_copy_overlapping_ranges_is_memmove(gpu):
+    """ops.copy_ between overlapping views of one buffer (tiles run in any order): the result is the source as it
+    was before the copy, in both directions; an identical range is a no-op."""
+    n = 3 * 32768 + 12
+    base = torch.rand(n + 64, device=gpu)
+    for shift in (4, -4, 32768):
+        buf = base.clone()
+        lo, hi = max(0, shift), max(0, -shift)
+        src, dst = buf[hi:hi + n - abs(shift)], buf[lo:lo + n - abs(shift)]
+        want = src.clone()
+        ops.copy_(dst, src)
+        assert torch.equal(dst, want), shift
+    buf = base.clone()
+    ops.copy_(buf, buf)
+    assert torch.equal(buf, base)
+
+
 def test_ticket_streams_per_stream_counters_and_capture(gpu):
     """Launches on two streams at once (each stream has its own counter pair) and inside a hipGraph capture (the
     grid-stride form: no counter is allocated while capturing) all give exact results."""
