@@ -71,12 +71,20 @@ at::Tensor gather_(const at::Tensor& src, const at::Tensor& idx, at::Tensor out)
     return out;
 }
 
+// The streaming kernels take their tiles in any order: an input that PARTLY overlaps the output is copied out first
+// (an input identical to the output, element for element, is fine: each element is read before it is written).
+at::Tensor unaliased(const at::Tensor& in, const at::Tensor& out) {
+    const auto i0 = reinterpret_cast<uintptr_t>(in.data_ptr()), o0 = reinterpret_cast<uintptr_t>(out.data_ptr());
+    const uintptr_t ib = (uintptr_t)in.numel() * in.element_size(), ob = (uintptr_t)out.numel() * out.element_size();
+    return (i0 != o0 && i0 < o0 + ob && o0 < i0 + ib) ? in.clone() : in;
+}
+
 at::Tensor axpy_(at::Tensor y, double alpha, const at::Tensor& x) {
     check_gpu(y, "y", at::kFloat), check_gpu(x, "x", at::kFloat);
     TORCH_CHECK(y.is_contiguous() && (reinterpret_cast<uintptr_t>(y.data_ptr()) & 15u) == 0, "axpy_: y must be contiguous, 16-B aligned");
     TORCH_CHECK(x.numel() == y.numel(), "axpy_: size mismatch");
     const at::DeviceGuard g(y.device());
-    auto xc = aligned_contig(x);
+    auto xc = unaliased(aligned_contig(x), y);
     check_rc(pcmx_axpy_f32((float)alpha, xc.data_ptr<float>(), y.data_ptr<float>(), y.numel(), cur_stream(y)), "axpy_");
     return y;
 }
@@ -86,11 +94,7 @@ at::Tensor copy_(at::Tensor dst, const at::Tensor& src) {
     TORCH_CHECK(dst.is_contiguous() && (reinterpret_cast<uintptr_t>(dst.data_ptr()) & 15u) == 0, "copy_: dst must be contiguous, 16-B aligned");
     TORCH_CHECK(src.numel() == dst.numel() && src.device() == dst.device(), "copy_: size / device mismatch");
     const at::DeviceGuard g(dst.device());
-    auto sc = aligned_contig(src);
-    // tiles run in any order: a source that partly overlaps the destination is copied out first (memmove semantics)
-    const auto s0 = reinterpret_cast<uintptr_t>(sc.data_ptr()), d0 = reinterpret_cast<uintptr_t>(dst.data_ptr());
-    const uintptr_t nb = (uintptr_t)dst.numel() * sizeof(float);
-    if (s0 != d0 && s0 < d0 + nb && d0 < s0 + nb) sc = sc.clone();
+    auto sc = unaliased(aligned_contig(src), dst);  // memmove semantics
     check_rc(pcmx_copy_f32(sc.data_ptr<float>(), dst.data_ptr<float>(), dst.numel(), cur_stream(dst)), "copy_");
     return dst;
 }

@@ -44,7 +44,7 @@ def test_ticket_streams_copy_fill_exact(gpu, n):
 
 def test_copy_overlapping_ranges_is_memmove(gpu):
     """ops.copy_ between overlapping views of one buffer (tiles run in any order): the result is the source as it
-    was before the copy, in both directions; an identical range is a no-op."""
+    was before the copy, in both directions; an identical range is a no-op. Same for axpy_'s x overlapping y."""
     n = 3 * 32768 + 12
     base = torch.rand(n + 64, device=gpu)
     for shift in (4, -4, 32768):
@@ -57,6 +57,11 @@ def test_copy_overlapping_ranges_is_memmove(gpu):
     buf = base.clone()
     ops.copy_(buf, buf)
     assert torch.equal(buf, base)
+    buf = base.clone()  # axpy_ with x a shifted view of y: x as it was before the update
+    y, x = buf[0:n - 8], buf[8:n]
+    want = y + 0.5 * x
+    ops.axpy_(y, 0.5, x)
+    torch.testing.assert_close(y, want, rtol=0, atol=0)
 
 
 def test_ticket_streams_per_stream_counters_and_capture(gpu):
