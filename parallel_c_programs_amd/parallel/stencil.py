@@ -34,7 +34,9 @@ def auto_fuse(slab_rows: int) -> int:
     the distributed step shape (interior launch + the two-span edge launch, 16384 columns, round-3 lane geometries:
     4 columns per lane at T >= 6 below 12288 rows, 2-row edge waves; scripts/stencil_lanes_lab.py,
     profiles/r3_stencil/lanes_*.txt), GLUP/s: 16384 rows T=8 5.5k; 8192 T=8 4.9k / T=6 4.8k; 4096 T=6 4.4k / T=8 4.2k
-    / T=4 3.9k; 2048 T=6 3.4k / T=8 3.3k / T=4 3.3k."""
+    / T=4 3.9k; 2048 T=6 3.4k / T=8 3.3k / T=4 3.3k. Re-checked in round 6 with the current kernel and deep halo
+    (profiles/r6_stencil/t6_t8_ab.txt): 2048 rows T=6 deep5 3.65-3.76k / T=8 3.41-3.72k; 4096 T=6 4.39-4.45k /
+    T=8 4.32-4.38k."""
     return 8 if slab_rows >= 6144 else 6
 
 
