@@ -835,6 +835,7 @@ extern "C" int pcmx_stencil5xT_bf16_spans_shape(const void* u, void* out, int ro
             break;
         case 3: PCMX_STENCIL_V2C(3, 8) break;
         case 4: PCMX_STENCIL_V2(4) break;
+        case 5: PCMX_STENCIL_V2(5) break;
         case 6: PCMX_STENCIL_V2(6) break;
         case 8: PCMX_STENCIL_V2(8) break;
         default: return -1;
@@ -852,7 +853,7 @@ extern "C" int pcmx_stencil5xT_bf16_spans(const void* u, void* out, int rows, in
                                             global_rows, k, 0, s);
 }
 
-// T fused updates over local rows [r0, r1) of a slab with `halo` rows above and below (T = 2, 3, 4, 6, 8).
+// T fused updates over local rows [r0, r1) of a slab with `halo` rows above and below (T = 2, 3, 4, 5, 6, 8).
 extern "C" int pcmx_stencil5xT_bf16(const void* u, void* out, int rows, int cols, int ld, int halo, int steps, int r0,
                                     int r1, long long global_row0, long long global_rows, float k, hipStream_t s) {
     return pcmx_stencil5xT_bf16_spans(u, out, rows, cols, ld, halo, steps, r0, r1, 0, 0, global_row0, global_rows, k, s);

@@ -49,7 +49,7 @@ def stencil5_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, glo
     return out
 
 
-FUSED_STEPS = (2, 3, 4, 6, 8)
+FUSED_STEPS = (2, 3, 4, 5, 6, 8)
 
 
 def stencil5_fused_step_(u: torch.Tensor, out: torch.Tensor, global_row0: int = 0, global_rows: int | None = None,

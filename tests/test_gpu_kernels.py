@@ -232,7 +232,7 @@ def test_stencil_row_range_split(gpu):
     assert torch.equal(full, part)
 
 
-@pytest.mark.parametrize("steps", [2, 3, 4, 6, 8])
+@pytest.mark.parametrize("steps", [2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("shape", [(256, 512), (1000, 1000), (515, 4096), (9, 2000), (4000, 800), (8300, 1000),
                                    (12400, 600)])
 def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
@@ -253,7 +253,7 @@ def test_stencil_fused_steps_bit_exact(gpu, shape, steps):
     assert torch.equal(b.cpu()[1:-1].view(torch.int16), ref[1:-1].view(torch.int16))
 
 
-@pytest.mark.parametrize("steps", [3, 4, 6, 8])
+@pytest.mark.parametrize("steps", [3, 4, 5, 6, 8])
 @pytest.mark.parametrize("shape", [(515, 1000), (70, 2056), (200, 264)])
 def test_stencil_fused_every_lane_geometry(gpu, shape, steps):
     """Every explicit launch shape (ops.stencil.launch_shape: 4 or 8 columns per lane x 2..133 rows per wave x prefetch
