@@ -10,7 +10,7 @@ import sys
 def main():
     db, count = sys.argv[1], int(sys.argv[2])
     subs = sys.argv[3].split(",") if len(sys.argv) > 3 else [""]
-    c = sqlite3.connect(db)
+    c = sqlite3.connect(f"file:{db}?mode=ro", uri=True)  # read-only: a wrong path fails instead of creating a file
     rows = c.execute("select name, start, end, stream_id, queue_id, grid_x / max(workgroup_x, 1) "
                      "from kernels order by start").fetchall()
     rows = [r for r in rows if any(s in r[0] for s in subs)][-count:]

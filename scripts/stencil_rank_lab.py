@@ -19,7 +19,8 @@ of the forced shapes); STENCIL_LAB_CPL=4 / 8 (columns per lane of the forced sha
 paired waves off / on for the non-edge launches, one line per value); STENCIL_LAB_RCCL=1 (round 6:
 each deep-halo variant also runs WITH its exchange: the real halo bytes, 2 x mT rows, through the native exchange on a
 world-1 RCCL communicator, posted before the interior launch and waited before the edge launch as StencilSlab.step
-does; printed as deepM+x).
+does; printed as deepM+x); STENCIL_LAB_DEEP_BUFS=2 (round 6 default: the deep-halo phases ping-pong between two
+buffers as StencilSlab does; 0 = one buffer per phase, the rounds 4-6 lab numbers).
 """
 import os
 import sys
@@ -101,14 +102,19 @@ def main():
             # launch + ONE two-span edge launch over local rows [-(m-1)T, T) and [rows - T, rows + (m-1)T), then
             # launches over [-e, rows + e) for e = (m-2)T .. 0; checked against the same m steps as single launches
             deeps = {}
+            # STENCIL_LAB_DEEP_BUFS (round 6): 2 = the production ping-pong pair (StencilSlab's u / v; at N = 8 the
+            # pair, 2 x ~68 MB, can stay in the 256-MB Infinity Cache like the single-launch variants' pair);
+            # 0 = one buffer per phase (M + 1, the rounds 4-6 lab numbers: every phase streams from HBM)
+            nbufs = int(os.environ.get("STENCIL_LAB_DEEP_BUFS", "2"))
             for M in [int(v) for v in os.environ.get("STENCIL_LAB_DEEP", "2,3,4").split(",")]:
                 u4 = (torch.rand(rows + 2 * M * T, N, generator=g, device=dev) * 4 - 2).to(torch.bfloat16)
-                b4 = [u4.clone() for _ in range(M + 1)]
+                nb = nbufs if nbufs >= 2 else M + 1
+                b4 = [u4.clone() for _ in range(nb)]
                 c4 = [u4.clone() for _ in range(M + 1)]
 
                 rbuf = torch.empty(2 * M * T * N, dtype=torch.bfloat16, device=dev)
 
-                def deep(M=M, b4=b4, comm=False, rbuf=rbuf):
+                def deep(M=M, b4=b4, comm=False, rbuf=rbuf, nb=nb):
                     e0 = (M - 1) * T
                     works = []
                     if comm:  # both neighbours' halo payload (2 x mT rows) through RCCL, to itself
@@ -121,7 +127,7 @@ def main():
                                               halo=M * T, steps=T)
                     for ph in range(1, M):
                         e = (M - 1 - ph) * T
-                        step(b4[ph], b4[ph + 1], row0, N, halo=M * T, steps=T, row_range=(-e, rows + e))
+                        step(b4[ph % nb], b4[(ph + 1) % nb], row0, N, halo=M * T, steps=T, row_range=(-e, rows + e))
 
                 for ph in range(M):
                     e = (M - 1 - ph) * T
@@ -144,7 +150,7 @@ def main():
                 if name in deeps:
                     M, _, b4, c4 = deeps[name]
                     hh = M * T
-                    same = torch.equal(b4[M][hh:-hh], c4[M][hh:-hh])
+                    same = torch.equal(b4[M % len(b4)][hh:-hh], c4[M][hh:-hh])
                     res[name] = (timed(fn) / M, same)
                     continue
                 same = name == "full" or torch.equal(out[T:-T], ref[T:-T])
