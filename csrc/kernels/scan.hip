@@ -346,10 +346,11 @@ __device__ __forceinline__ void parked_flush(float* __restrict__ out, long long 
 
 // One iteration: scan `cur` (in v) and publish its aggregate, issue the loads of `next` into vn, take a ticket,
 // flush `prev` from the park buffer, park `cur`. Returns cur's aggregate (thread 0 needs it one iteration later).
-// kLoadFirst (round 6): the loads of `next` go out at the TOP of the iteration, before cur's scan (vn is free there:
-// its last tile was parked an iteration ago), so they have the scan's time too and the block keeps a tile of loads
-// in flight while it computes.
-template <int R, int W, bool kEarly, bool kLoadFirst = false>
+// kLoadAt (round 6 lab): where the loads of `next` go out. 0 (production): after cur's scan and publish. 1: at the TOP
+// of the iteration (vn is free there: its last tile was parked an iteration ago), before wave 0's early polls. 2:
+// right AFTER the early polls, before the scan. vmcnt retires in issue order, so under 1 the look-back's wait for its
+// polls also waits for the whole next tile; 2 keeps the polls ahead of the loads.
+template <int R, int W, bool kEarly, int kLoadAt = 0>
 __device__ __forceinline__ float parked_step(const float* __restrict__ in, float* __restrict__ out, long long n,
                                              long long cur, f32x4 (&v)[R], long long next, f32x4 (&vn)[R],
                                              long long prev, float agg_prev, long long ntiles, int exclusive, float init,
@@ -358,10 +359,11 @@ __device__ __forceinline__ float parked_step(const float* __restrict__ in, float
     unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
     const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
     // kEarly: wave 0 sends prev's first round of polls BEFORE this tile's scan, so their round trip overlaps it
-    if (kLoadFirst && next < ntiles) load_tile<R, W>(in, n, next, vn);
+    if (kLoadAt == 1 && next < ntiles) load_tile<R, W>(in, n, next, vn);
     ParkPoll sv;
     const bool polled = kEarly && wave == 0 && prev > 0;
     if (polled) parked_poll(prev, prev - 1, ws, sv);
+    if (kLoadAt == 2 && next < ntiles) load_tile<R, W>(in, n, next, vn);
     float carry = 0.f;
     float lane_excl[R];
 #pragma unroll
@@ -387,7 +389,7 @@ __device__ __forceinline__ float parked_step(const float* __restrict__ in, float
     if (threadIdx.x == 0)
         __hip_atomic_store(&status[cur], pack(cur == 0 ? kFlagIncl : kFlagAgg, agg), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    if (!kLoadFirst && next < ntiles) load_tile<R, W>(in, n, next, vn);
+    if (kLoadAt == 0 && next < ntiles) load_tile<R, W>(in, n, next, vn);
     const unsigned ticket = threadIdx.x == 0 ? atomicAdd(&ws->ticket, 1u) : 0u;
     parked_flush<R, W>(out, n, prev, agg_prev, init, ws, err_flag, park, s_prefix, s_next, ticket, sv, polled);
 #pragma unroll
@@ -407,7 +409,7 @@ __device__ __forceinline__ float parked_step(const float* __restrict__ in, float
     return agg;
 }
 
-template <int R, int W, bool kEarly, bool kLoadFirst = false>
+template <int R, int W, bool kEarly, int kLoadAt = 0>
 __global__ __launch_bounds__(W * kWave) void scan_parked_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                                 long long n, long long ntiles, int exclusive,
                                                                 const float* init_dev, ScanWs* ws, unsigned* err_flag) {
@@ -429,12 +431,12 @@ __global__ __launch_bounds__(W * kWave) void scan_parked_kernel(const float* __r
     // unrolled by two so both register buffers are statically named; every exit is block-uniform and ends with
     // the flush of the last parked tile
     while (true) {
-        agg_prev = parked_step<R, W, kEarly, kLoadFirst>(in, out, n, ta, va, tb, vb, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
+        agg_prev = parked_step<R, W, kEarly, kLoadAt>(in, out, n, ta, va, tb, vb, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
                                      park, s_wave_tot, &s_prefix, &s_tile[0]);
         prev = ta;
         ta = s_tile[0];
         if (tb >= ntiles) break;
-        agg_prev = parked_step<R, W, kEarly, kLoadFirst>(in, out, n, tb, vb, ta, va, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
+        agg_prev = parked_step<R, W, kEarly, kLoadAt>(in, out, n, tb, vb, ta, va, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
                                      park, s_wave_tot, &s_prefix, &s_tile[0]);
         prev = tb;
         tb = s_tile[0];
@@ -462,7 +464,7 @@ extern "C" long long pcmx_scan_workspace_bytes(long long n) { return (long long)
 extern "C" int pcmx_scan_f32_variant(const float* x, float* out, long long n, int exclusive, const float* init_dev,
                                      void* workspace, unsigned* err_flag, int variant, hipStream_t s) {
     if (n <= 0) return 0;
-    if (variant < 0 || variant > 5) return PCMX_ERR_ARG;
+    if (variant < 0 || variant > 6) return PCMX_ERR_ARG;
     if ((((uintptr_t)x) & 15u) || (((uintptr_t)out) & 15u) || !workspace) return PCMX_ERR_ARG;
     const long long tiles = num_tiles(n);
     if (tiles > 0x7fffffffLL) return PCMX_ERR_ARG;
@@ -474,7 +476,8 @@ extern "C" int pcmx_scan_f32_variant(const float* x, float* out, long long n, in
         case 1: scan_persistent_kernel<8, 16><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
         case 2: scan_parked_kernel<16, 8, false><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
         case 3: scan_parked_kernel<8, 16, false><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
-        case 5: scan_parked_kernel<16, 8, true, true><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        case 5: scan_parked_kernel<16, 8, true, 1><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        case 6: scan_parked_kernel<16, 8, true, 2><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
         default: scan_parked_kernel<16, 8, true><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
     }
     return (int)hipGetLastError();
