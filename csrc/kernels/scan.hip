@@ -80,6 +80,24 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ in, long lon
     }
 }
 
+// Branch-free form (round 6 lab): one buffer descriptor per tile whose range ends at n, so the tail of the last tile
+// needs no branch. A raw buffer load checks its range per dword: the dwords past the end read as 0 (probed on the
+// MI355X, scripts/buffer_oob_probe.hip). Loads carry the nontemporal bit like load_tile's.
+template <int R, int W>
+__device__ __forceinline__ void load_tile_rs(const float* __restrict__ in, long long n, long long tile, f32x4 (&v)[R]) {
+    const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
+    const long long t0 = tile * Tile<R, W>::kElems;
+    const long long rem = n - t0;
+    // a tile past the end (the schedule's "next" after the last tile) gets an empty range: every load reads 0 and
+    // touches no memory, so the caller issues it without a branch
+    const int bytes = (int)((rem <= 0 ? 0 : rem < Tile<R, W>::kElems ? rem : (long long)Tile<R, W>::kElems) * 4);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in + t0), 0, bytes, 0x00020000);
+    const int off = (wave * Tile<R, W>::kWaveItems + lane * 4) * 4;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        v[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + r * 1024, 0, 2));
+}
+
 // Scans tile `tile` held in v, publishes it, issues the loads of `next` into vn, looks back, stores.
 template <int R, int W>
 __device__ __forceinline__ void finish_tile(const float* __restrict__ in, float* __restrict__ out, long long n, long long tile,
@@ -350,7 +368,7 @@ __device__ __forceinline__ void parked_flush(float* __restrict__ out, long long 
 // of the iteration (vn is free there: its last tile was parked an iteration ago), before wave 0's early polls. 2:
 // right AFTER the early polls, before the scan. vmcnt retires in issue order, so under 1 the look-back's wait for its
 // polls also waits for the whole next tile; 2 keeps the polls ahead of the loads.
-template <int R, int W, bool kEarly, int kLoadAt = 0>
+template <int R, int W, bool kEarly, int kLoadAt = 0, bool kRs = false>
 __device__ __forceinline__ float parked_step(const float* __restrict__ in, float* __restrict__ out, long long n,
                                              long long cur, f32x4 (&v)[R], long long next, f32x4 (&vn)[R],
                                              long long prev, float agg_prev, long long ntiles, int exclusive, float init,
@@ -359,11 +377,21 @@ __device__ __forceinline__ float parked_step(const float* __restrict__ in, float
     unsigned long long* status = reinterpret_cast<unsigned long long*>(ws + 1);
     const int lane = pcmx::lane_id(), wave = threadIdx.x / kWave;
     // kEarly: wave 0 sends prev's first round of polls BEFORE this tile's scan, so their round trip overlaps it
-    if (kLoadAt == 1 && next < ntiles) load_tile<R, W>(in, n, next, vn);
+    if constexpr (kLoadAt == 1) {
+        if constexpr (kRs)
+            load_tile_rs<R, W>(in, n, next, vn);  // branch-free (an empty range past the last tile)
+        else if (next < ntiles)
+            load_tile<R, W>(in, n, next, vn);
+    }
     ParkPoll sv;
     const bool polled = kEarly && wave == 0 && prev > 0;
     if (polled) parked_poll(prev, prev - 1, ws, sv);
-    if (kLoadAt == 2 && next < ntiles) load_tile<R, W>(in, n, next, vn);
+    if constexpr (kLoadAt == 2) {
+        if constexpr (kRs)
+            load_tile_rs<R, W>(in, n, next, vn);  // branch-free (an empty range past the last tile)
+        else if (next < ntiles)
+            load_tile<R, W>(in, n, next, vn);
+    }
     float carry = 0.f;
     float lane_excl[R];
 #pragma unroll
@@ -389,7 +417,12 @@ __device__ __forceinline__ float parked_step(const float* __restrict__ in, float
     if (threadIdx.x == 0)
         __hip_atomic_store(&status[cur], pack(cur == 0 ? kFlagIncl : kFlagAgg, agg), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    if (kLoadAt == 0 && next < ntiles) load_tile<R, W>(in, n, next, vn);
+    if constexpr (kLoadAt == 0) {
+        if constexpr (kRs)
+            load_tile_rs<R, W>(in, n, next, vn);  // branch-free (an empty range past the last tile)
+        else if (next < ntiles)
+            load_tile<R, W>(in, n, next, vn);
+    }
     const unsigned ticket = threadIdx.x == 0 ? atomicAdd(&ws->ticket, 1u) : 0u;
     parked_flush<R, W>(out, n, prev, agg_prev, init, ws, err_flag, park, s_prefix, s_next, ticket, sv, polled);
 #pragma unroll
@@ -409,7 +442,7 @@ __device__ __forceinline__ float parked_step(const float* __restrict__ in, float
     return agg;
 }
 
-template <int R, int W, bool kEarly, int kLoadAt = 0>
+template <int R, int W, bool kEarly, int kLoadAt = 0, bool kRs = false>
 __global__ __launch_bounds__(W * kWave) void scan_parked_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                                 long long n, long long ntiles, int exclusive,
                                                                 const float* init_dev, ScanWs* ws, unsigned* err_flag) {
@@ -427,16 +460,19 @@ __global__ __launch_bounds__(W * kWave) void scan_parked_kernel(const float* __r
     long long ta = s_tile[0], tb = s_tile[1], prev = -1;
     if (ta >= ntiles) return;
     float agg_prev = 0.f;
-    load_tile<R, W>(in, n, ta, va);
+    if constexpr (kRs)
+        load_tile_rs<R, W>(in, n, ta, va);
+    else
+        load_tile<R, W>(in, n, ta, va);
     // unrolled by two so both register buffers are statically named; every exit is block-uniform and ends with
     // the flush of the last parked tile
     while (true) {
-        agg_prev = parked_step<R, W, kEarly, kLoadAt>(in, out, n, ta, va, tb, vb, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
+        agg_prev = parked_step<R, W, kEarly, kLoadAt, kRs>(in, out, n, ta, va, tb, vb, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
                                      park, s_wave_tot, &s_prefix, &s_tile[0]);
         prev = ta;
         ta = s_tile[0];
         if (tb >= ntiles) break;
-        agg_prev = parked_step<R, W, kEarly, kLoadAt>(in, out, n, tb, vb, ta, va, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
+        agg_prev = parked_step<R, W, kEarly, kLoadAt, kRs>(in, out, n, tb, vb, ta, va, prev, agg_prev, ntiles, exclusive, init, ws, err_flag,
                                      park, s_wave_tot, &s_prefix, &s_tile[0]);
         prev = tb;
         tb = s_tile[0];
@@ -464,7 +500,7 @@ extern "C" long long pcmx_scan_workspace_bytes(long long n) { return (long long)
 extern "C" int pcmx_scan_f32_variant(const float* x, float* out, long long n, int exclusive, const float* init_dev,
                                      void* workspace, unsigned* err_flag, int variant, hipStream_t s) {
     if (n <= 0) return 0;
-    if (variant < 0 || variant > 6) return PCMX_ERR_ARG;
+    if (variant < 0 || variant > 8) return PCMX_ERR_ARG;
     if ((((uintptr_t)x) & 15u) || (((uintptr_t)out) & 15u) || !workspace) return PCMX_ERR_ARG;
     const long long tiles = num_tiles(n);
     if (tiles > 0x7fffffffLL) return PCMX_ERR_ARG;
@@ -478,6 +514,8 @@ extern "C" int pcmx_scan_f32_variant(const float* x, float* out, long long n, in
         case 3: scan_parked_kernel<8, 16, false><<<grid, 16 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
         case 5: scan_parked_kernel<16, 8, true, 1><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
         case 6: scan_parked_kernel<16, 8, true, 2><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        case 7: scan_parked_kernel<16, 8, true, 0, true><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
+        case 8: scan_parked_kernel<16, 8, true, 2, true><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
         default: scan_parked_kernel<16, 8, true><<<grid, 8 * kWave, 0, s>>>(x, out, n, tiles, exclusive, init_dev, ws, err_flag); break;
     }
     return (int)hipGetLastError();

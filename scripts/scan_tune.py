@@ -1,6 +1,7 @@
 """Scan schedule A/B on 1e9 f32 (pcmx_scan_f32_variant through ctypes): 0 persistent R16xW8, 1 persistent R8xW16,
 2 parked-tile R16xW8, 3 parked-tile R8xW16, 4 parked-tile R16xW8 + early polls (production), 5 = 4 with the next tile's loads issued before the scan
-(round 6), 6 = the same loads issued after wave 0's early polls. Device time, GB/s
+(round 6), 6 = the same loads issued after wave 0's early polls, 7 / 8 = 4 / 6 with
+branch-free buffer-descriptor tile loads. Device time, GB/s
 (8 B/element), error vs fp64. Before timing, every variant is checked on ragged sizes, exclusive mode, an init
 offset and in place.
 usage: python scripts/scan_tune.py [n] [variants, comma separated] [rounds]"""

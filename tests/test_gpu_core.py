@@ -170,7 +170,7 @@ def test_scan_integer_exact(gpu):
     assert torch.equal(out.long(), torch.cumsum(x.long(), 0))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_scan_schedules_exact(gpu, variant):
     """Every scan schedule (persistent / parked-tile / parked + early polls) on ragged sizes, exclusive, a device
     init and in place; small integers keep every prefix exact in f32."""
