@@ -20,7 +20,8 @@ paired waves off / on for the non-edge launches, one line per value); STENCIL_LA
 each deep-halo variant also runs WITH its exchange: the real halo bytes, 2 x mT rows, through the native exchange on a
 world-1 RCCL communicator, posted before the interior launch and waited before the edge launch as StencilSlab.step
 does; printed as deepM+x); STENCIL_LAB_DEEP_BUFS=2 (round 6 default: the deep-halo phases ping-pong between two
-buffers as StencilSlab does; 0 = one buffer per phase, the rounds 4-6 lab numbers).
+buffers as StencilSlab does; 0 = one buffer per phase, the rounds 4-6 lab numbers); STENCIL_LAB_EDGE=4:2 (an explicit
+cpl:rpw[:ahead] shape for the deep-halo step's edge launch).
 """
 import os
 import sys
@@ -63,6 +64,10 @@ def main():
     worlds = [int(w) for w in os.environ.get("STENCIL_LAB_WORLDS", "1,2,4,8").split(",")]
     rpws = [int(r) for r in os.environ.get("STENCIL_LAB_RPW", "0").split(",")]
     pairs = [{"": None, "1": True, "0": False}[p] for p in os.environ.get("STENCIL_LAB_PAIRED", "").split(",")]
+    # STENCIL_LAB_EDGE=cpl:rpw[:ahead] (round 6): an explicit shape for the deep-halo step's edge launch (the two rank-edge
+    # bands, <= 64 rows: production 4 columns per lane x 2-row waves)
+    edge_spec = [int(v) for v in os.environ.get("STENCIL_LAB_EDGE", "0:0").split(":")] + [0]
+    edge_shape = launch_shape(edge_spec[0], edge_spec[1], edge_spec[2]) if any(edge_spec) else 0
     for T, world, rpw, paired in [(T, w, r, p) for T in fuses for w in worlds for r in rpws for p in pairs]:
         shape = launch_shape(int(os.environ.get("STENCIL_LAB_CPL", "0")), rpw, int(os.environ.get("STENCIL_LAB_AHEAD", "0")),
                              paired)
@@ -124,7 +129,7 @@ def main():
                     for w in works:
                         w.wait()
                     ops.stencil5_fused_spans_(b4[0], b4[1], ((-e0, T), (rows - T, rows + e0)), row0, N,
-                                              halo=M * T, steps=T)
+                                              halo=M * T, steps=T, shape=edge_shape)
                     for ph in range(1, M):
                         e = (M - 1 - ph) * T
                         step(b4[ph % nb], b4[(ph + 1) % nb], row0, N, halo=M * T, steps=T, row_range=(-e, rows + e))
